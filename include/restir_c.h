@@ -1,0 +1,249 @@
+/*
+ * restir_c.h -- C ABI of the MI355X-native ReSTIR direct-lighting sampler (libromis_amd.so).
+ *
+ * Drop-in boundary for the reference's ReSTIR render entry:
+ *   renderRayTraced(prevGrid, Scene, Trackball, EmbreeInterface, Screen, Features)   src/rendering/render.cpp:268-290
+ *   renderReSTIR   (prevGrid, Scene, Trackball, EmbreeInterface, Screen, Features)   src/rendering/render.cpp:28-62
+ * Plain pointers and sizes only: no C++ / torch types cross this line.  The C++ wrapper that keeps the
+ * reference's call surface (value-typed grids, exceptions) is include/romis_amd/restir.hpp.
+ *
+ * Conventions (mirroring the reference):
+ *  - every entry point returns restir_status; the message of the last failure on the calling thread is
+ *    restir_last_error() (the C++ wrapper rethrows it as std::runtime_error, as render.cpp:99/278 do);
+ *  - a context owns one HIP device, one HIP stream and all device buffers; calls on one context are
+ *    serialised by the context, different contexts are independent (main.cpp:213-230 renders per thread);
+ *  - a restir_frame is the device-resident replacement of std::shared_ptr<ReservoirGrid> (main.cpp:165):
+ *    reference-counted, never copied to the host unless downloaded.
+ *  - pixel (x, y) uses the reference's convention: y = 0 is the BOTTOM row (render_utils.cpp:24-25); the RGB
+ *    image handed back is laid out like Screen's texture (screen.cpp:37-43): row 0 = TOP.
+ *
+ * Keyed RNG (the parity contract; the reference's rand()/random_device/mt19937 are not seedable):
+ *   mix32(h)          = murmur3 fmix32
+ *   key(s,f,stage,p)  = mix32(mix32(mix32(s ^ 0x9E3779B9) + f) ^ (stage * 0x01000193 + p * 0x27D4EB2F))
+ *   pix(key, g)       = mix32(key ^ mix32(g * 0x9E3779B1 + 0x7F4A7C15))        g = global pixel id y*W + x
+ *   draw(pix, slot)   = mix32(pix + slot * 0x9E3779B9)
+ *   rand()            -> draw >> 1 ; u = linearMap(float(rand()), 0, RAND_MAX, 0, 1)   (utils.cpp:26-31)
+ *   U{0..L-1}         -> (uint64(draw) * L) >> 32
+ *   U{-r..r}          -> ((uint64(draw) * (2r+1)) >> 32) - r
+ * stages / slots:
+ *   RESTIR_STAGE_RIS      (pass 0): candidate c: light 4c, first rand 4c+1, second rand 4c+2, accept 4c+3
+ *   RESTIR_STAGE_TEMPORAL (pass 0): accept of the t-th Reservoir::update = t
+ *   RESTIR_STAGE_SPATIAL  (pass p): neighbour n: dx 2n, dy 2n+1; accept of the t-th update = 2k + t
+ */
+#ifndef RESTIR_C_H
+#define RESTIR_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RESTIR_ABI_VERSION 1
+
+#define RESTIR_STAGE_RIS      1u
+#define RESTIR_STAGE_TEMPORAL 2u
+#define RESTIR_STAGE_SPATIAL  3u
+#define RESTIR_DEFAULT_SEED   0x5EED0001u
+#define RESTIR_MAX_N          32u   /* numSamplesInReservoir slider range 1..32 (ui.cpp:305) */
+
+typedef enum restir_status {
+    RESTIR_OK              = 0,
+    RESTIR_ERR_INVALID     = 1,  /* bad argument (null pointer, size, range) */
+    RESTIR_ERR_HIP         = 2,  /* HIP runtime failure */
+    RESTIR_ERR_NO_DEVICE   = 3,  /* no usable gfx950 device */
+    RESTIR_ERR_STATE       = 4,  /* call out of order (e.g. render before set_scene) */
+    RESTIR_ERR_UNSUPPORTED = 5,  /* feature combination not implemented (e.g. RMIS / ROMIS modes) */
+    RESTIR_ERR_COMM        = 6   /* RCCL failure */
+} restir_status;
+
+/* RayTraceMode (src/utils/common.h:25-29). Only RESTIR is accelerated; the others return UNSUPPORTED. */
+typedef enum restir_mode { RESTIR_MODE_RESTIR = 0, RESTIR_MODE_RMIS = 1, RESTIR_MODE_ROMIS = 2 } restir_mode;
+
+/* std::variant<PointLight, SegmentLight, ParallelogramLight> (common.h:72-87) flattened. 88 bytes. */
+typedef enum restir_light_type {
+    RESTIR_LIGHT_POINT = 0, RESTIR_LIGHT_SEGMENT = 1, RESTIR_LIGHT_PARALLELOGRAM = 2
+} restir_light_type;
+typedef struct restir_light {
+    uint32_t type;
+    float p0[3];   /* Point.position | Segment.endpoint0 | Parallelogram.v0     */
+    float p1[3];   /*                | Segment.endpoint1 | Parallelogram.edge01 */
+    float p2[3];   /*                                    | Parallelogram.edge02 */
+    float c0[3];   /* Point.color    | Segment.color0    | Parallelogram.color0 */
+    float c1[3];   /*                | Segment.color1    | Parallelogram.color1 */
+    float c2[3];   /*                                    | Parallelogram.color2 */
+    float c3[3];   /*                                    | Parallelogram.color3 */
+} restir_light;
+
+/* Material (framework/include/framework/mesh.h:22-34); kdTexture is not carried. */
+typedef struct restir_material {
+    float kd[3];
+    float ks[3];
+    float shininess;
+    float transparency;
+} restir_material;
+
+/* Mesh (mesh.h:36-43): one material per mesh, like loadMesh's per-material sub-meshes. */
+typedef struct restir_mesh {
+    const float*    positions;     /* [num_vertices][3] */
+    const float*    normals;       /* [num_vertices][3] */
+    uint32_t        num_vertices;
+    const uint32_t* triangles;     /* [num_triangles][3] vertex indices */
+    uint32_t        num_triangles;
+    restir_material material;
+} restir_mesh;
+
+/* Trackball state (framework/include/framework/trackball.h:13-66) as set by Trackball(window, fovy, dist)
+ * + setCamera(lookAt, rotation, dist) (main.cpp:223-224). Angles in radians. */
+typedef struct restir_camera {
+    float fovy;
+    float aspect;          /* Window::getAspectRatio() = float(w)/float(h) (window.cpp:380-385) */
+    float look_at[3];
+    float distance;
+    float rotation[3];     /* Euler angles (x, y, z) */
+} restir_camera;
+
+/* Derived per-frame camera constants (Trackball::position / generateRay, trackball.cpp:75-78,105-114). */
+typedef struct restir_camera_frame {
+    float origin[3];
+    float quat[4];         /* x, y, z, w of glm::quat(rotation) */
+    float half_w, half_h;  /* m_halfScreenSpaceWidth / Height */
+} restir_camera_frame;
+
+/* The Features fields read on the ReSTIR path (common.h:89-136). */
+typedef struct restir_features {
+    uint32_t ray_trace_mode;                 /* restir_mode */
+    uint32_t initial_light_samples;          /* M  */
+    uint32_t num_samples_in_reservoir;       /* N  (1..RESTIR_MAX_N) */
+    uint32_t num_neighbours_to_sample;       /* k  */
+    uint32_t spatial_resample_radius;        /* r  */
+    uint32_t spatial_resampling_passes;
+    uint32_t temporal_clamp_m;
+    uint8_t  initial_samples_visibility_check;
+    uint8_t  unbiased_combination;
+    uint8_t  spatial_reuse;
+    uint8_t  spatial_reuse_visibility_check;
+    uint8_t  temporal_reuse;
+    uint8_t  enable_shading;
+    uint8_t  enable_texture_mapping;         /* accepted; textures are not carried (no effect) */
+    uint8_t  enable_tone_mapping;
+    float    gamma;
+    float    exposure;
+} restir_features;
+
+/* Defaults of struct Features (common.h:89-136), rayTraceMode forced to ReSTIR. */
+void restir_features_default(restir_features* out);
+
+/* Keyed RNG (see header comment). Exposed for tests and tools. */
+uint32_t restir_rng_key(uint32_t seed, uint32_t frame, uint32_t stage, uint32_t pass);
+uint32_t restir_rng_draw(uint32_t key, uint32_t global_pixel, uint32_t slot);
+
+/* Host-side camera derivation, identical to the device path's constants. */
+void restir_camera_derive(const restir_camera* cam, restir_camera_frame* out);
+
+/* ---- screen tiling (multi-GPU) : pure host logic, callable without a GPU ---------------------------- */
+/* Tile (tx, ty) of a tiles_x x tiles_y grid over a global width x height image.  The tile's region is
+ * [x0, x0+w) x [y0, y0+h); its ghost region (what a rank must compute locally so that `passes` spatial
+ * passes of radius r give bit-identical results to a single-GPU frame) is the region grown by
+ * passes*r pixels, clipped to the image. */
+typedef struct restir_tile {
+    uint32_t global_width, global_height;
+    uint32_t x0, y0, width, height;          /* owned pixels */
+    uint32_t gx0, gy0, gwidth, gheight;      /* computed pixels (owned + ghost zone) */
+} restir_tile;
+restir_status restir_tile_plan(uint32_t global_width, uint32_t global_height, uint32_t tiles_x, uint32_t tiles_y,
+                               uint32_t rank, uint32_t ghost, restir_tile* out);
+
+/* ---- context ----------------------------------------------------------------------------------------- */
+typedef struct restir_ctx   restir_ctx;
+typedef struct restir_frame restir_frame;
+
+const char*   restir_last_error(void);
+int           restir_abi_version(void);
+restir_status restir_device_count(int* out);
+
+restir_status restir_create(int device, restir_ctx** out);
+void          restir_destroy(restir_ctx* ctx);
+restir_status restir_set_seed(restir_ctx* ctx, uint32_t seed, uint32_t frame_index);
+
+/* Uploads the scene: materials, light SoA table, and the flattened BVH built on the host (replaces
+ * EmbreeInterface(scene), embree_interface.cpp:14-51). */
+restir_status restir_set_scene(restir_ctx* ctx, const restir_mesh* meshes, uint32_t num_meshes,
+                               const restir_light* lights, uint32_t num_lights);
+
+/* renderReSTIR (render.cpp:28-62): primary hits -> initial RIS -> [temporal if prev] -> [spatial x P] ->
+ * final shading + tone map.  `prev` may be NULL (no temporal predecessor).  `out_next` (nullable) receives
+ * a new reference to the frame's final reservoir grid.  `out_rgb` (nullable, host, width*height*3 floats,
+ * row 0 = top) -- when NULL the call only enqueues work and returns without synchronising; the image stays
+ * on the device (restir_download_rgb).  `tile` (nullable) restricts the frame to one screen tile of a
+ * larger image (multi-GPU); NULL = the whole width x height image. */
+restir_status restir_render(restir_ctx* ctx, const restir_camera* cam, const restir_features* features,
+                            uint32_t width, uint32_t height, const restir_tile* tile,
+                            const restir_frame* prev, restir_frame** out_next, float* out_rgb);
+
+restir_status restir_frame_retain(restir_frame* frame);
+void          restir_frame_release(restir_frame* frame);
+restir_status restir_synchronize(restir_ctx* ctx);
+
+/* Last rendered image (owned pixels), host float RGB, row 0 = top. */
+restir_status restir_download_rgb(restir_ctx* ctx, float* out_rgb, size_t count);
+
+/* ---- stage-level access for parity tests and profiling ---------------------------------------------- *
+ * Buffers are the device SoA layout (DESIGN.md "Data layout"), one entry per pixel of the computed region
+ * (row-major, y = 0 bottom), and for reservoirs [N][pixels]:
+ *   gbuf_n_t   : float4 (N.xyz, t)         gbuf_p_mat : float4 (P.xyz, bits(material index))
+ *   res_a      : float4 (light pos.xyz, W) res_b      : float4 (light colour.xyz, bits(M))
+ *   res_dbg    : float2 (wSum, chosenSampleWeight)                                                   */
+typedef enum restir_buffer {
+    RESTIR_BUF_GBUF_N_T   = 0,   /* read by the spatial heuristic for every neighbour: keep it compact */
+    RESTIR_BUF_GBUF_P_MAT = 1,
+    RESTIR_BUF_RES_A      = 2,   /* reservoir slot 0 ("current") */
+    RESTIR_BUF_RES_B      = 3,
+    RESTIR_BUF_RES_DBG    = 4,
+    RESTIR_BUF_PREV_A     = 5,   /* reservoir slot 1 (temporal predecessor / spatial ping-pong) */
+    RESTIR_BUF_PREV_B     = 6,
+    RESTIR_BUF_PREV_DBG   = 7,
+    RESTIR_BUF_RGB        = 8    /* float3 per owned pixel, row 0 = top */
+} restir_buffer;
+
+/* Allocates stage buffers for a width x height region with N sub-reservoirs (idempotent). */
+restir_status restir_stage_configure(restir_ctx* ctx, uint32_t width, uint32_t height, uint32_t n);
+restir_status restir_stage_upload(restir_ctx* ctx, restir_buffer which, const void* host, size_t bytes);
+restir_status restir_stage_download(restir_ctx* ctx, restir_buffer which, void* host, size_t bytes);
+
+/* Individual passes on the stage buffers (the camera supplies the ray origin every pass shades from).
+ * `debug` != 0 also writes the (wSum, chosenSampleWeight) buffer of the pass output.
+ *   primary  : -> GBUF_*                         ris      : GBUF -> RES_*
+ *   temporal : RES_* (current) + PREV_* -> RES_*
+ *   spatial  : ONE pass, RES_* -> new RES_* (the input becomes PREV_*); call once per pass with that
+ *              pass's key restir_rng_key(seed, frame, RESTIR_STAGE_SPATIAL, pass)
+ *   final    : RES_* -> RGB                                                                                */
+restir_status restir_stage_primary(restir_ctx* ctx, const restir_camera* cam);
+restir_status restir_stage_ris(restir_ctx* ctx, const restir_camera* cam, const restir_features* f, uint32_t rng_key,
+                               int debug);
+restir_status restir_stage_temporal(restir_ctx* ctx, const restir_camera* cam, const restir_features* f,
+                                    uint32_t rng_key, int debug);
+restir_status restir_stage_spatial(restir_ctx* ctx, const restir_camera* cam, const restir_features* f,
+                                   uint32_t rng_key, int debug);
+restir_status restir_stage_final(restir_ctx* ctx, const restir_camera* cam, const restir_features* f);
+
+/* Device portable powf / expf over arrays (parity of the device math with the oracle's). */
+restir_status restir_debug_math(restir_ctx* ctx, const float* x, const float* y, float* out_pow, float* out_exp,
+                                size_t n);
+
+/* ---- timing ----------------------------------------------------------------------------------------- */
+/* When enabled, every kernel of restir_render / restir_stage_* is bracketed by HIP events on the
+ * context's stream; restir_timings returns the accumulated milliseconds and launch counts per kernel. */
+typedef enum restir_kernel {
+    RESTIR_K_PRIMARY = 0, RESTIR_K_RIS = 1, RESTIR_K_TEMPORAL = 2, RESTIR_K_SPATIAL = 3, RESTIR_K_FINAL = 4,
+    RESTIR_K_COUNT = 5
+} restir_kernel;
+restir_status restir_enable_timing(restir_ctx* ctx, int enable);
+restir_status restir_timings(restir_ctx* ctx, double* ms /*[RESTIR_K_COUNT]*/, uint64_t* launches /*[RESTIR_K_COUNT]*/);
+restir_status restir_reset_timings(restir_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RESTIR_C_H */

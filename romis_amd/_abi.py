@@ -1,0 +1,162 @@
+"""ctypes mirror of include/restir_c.h (the C ABI of libromis_amd.so).
+
+The library is built in-tree (romis_amd/_build/libromis_amd.so, see romis_amd/build.py).  Loading fails loudly
+when it is missing: there is no CPU fallback for the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libromis_amd.so")
+
+RESTIR_STAGE_RIS = 1
+RESTIR_STAGE_TEMPORAL = 2
+RESTIR_STAGE_SPATIAL = 3
+RESTIR_DEFAULT_SEED = 0x5EED0001
+RESTIR_MAX_N = 32
+
+LIGHT_POINT, LIGHT_SEGMENT, LIGHT_PARALLELOGRAM = 0, 1, 2
+MODE_RESTIR, MODE_RMIS, MODE_ROMIS = 0, 1, 2
+
+BUF_GBUF_N_T, BUF_GBUF_P_MAT, BUF_RES_A, BUF_RES_B, BUF_RES_DBG = 0, 1, 2, 3, 4
+BUF_PREV_A, BUF_PREV_B, BUF_PREV_DBG, BUF_RGB = 5, 6, 7, 8
+
+K_PRIMARY, K_RIS, K_TEMPORAL, K_SPATIAL, K_FINAL, K_COUNT = 0, 1, 2, 3, 4, 5
+KERNEL_NAMES = ["primary", "ris", "temporal", "spatial", "final"]
+
+STATUS_NAMES = {0: "OK", 1: "INVALID", 2: "HIP", 3: "NO_DEVICE", 4: "STATE", 5: "UNSUPPORTED", 6: "COMM"}
+
+F3 = C.c_float * 3
+
+
+class Light(C.Structure):
+    _fields_ = [("type", C.c_uint32), ("p0", F3), ("p1", F3), ("p2", F3),
+                ("c0", F3), ("c1", F3), ("c2", F3), ("c3", F3)]
+
+
+class Material(C.Structure):
+    _fields_ = [("kd", F3), ("ks", F3), ("shininess", C.c_float), ("transparency", C.c_float)]
+
+
+class Mesh(C.Structure):
+    _fields_ = [("positions", C.POINTER(C.c_float)), ("normals", C.POINTER(C.c_float)),
+                ("num_vertices", C.c_uint32), ("triangles", C.POINTER(C.c_uint32)),
+                ("num_triangles", C.c_uint32), ("material", Material)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("fovy", C.c_float), ("aspect", C.c_float), ("look_at", F3), ("distance", C.c_float),
+                ("rotation", F3)]
+
+
+class CameraFrame(C.Structure):
+    _fields_ = [("origin", F3), ("quat", C.c_float * 4), ("half_w", C.c_float), ("half_h", C.c_float)]
+
+
+class Features(C.Structure):
+    _fields_ = [("ray_trace_mode", C.c_uint32), ("initial_light_samples", C.c_uint32),
+                ("num_samples_in_reservoir", C.c_uint32), ("num_neighbours_to_sample", C.c_uint32),
+                ("spatial_resample_radius", C.c_uint32), ("spatial_resampling_passes", C.c_uint32),
+                ("temporal_clamp_m", C.c_uint32),
+                ("initial_samples_visibility_check", C.c_uint8), ("unbiased_combination", C.c_uint8),
+                ("spatial_reuse", C.c_uint8), ("spatial_reuse_visibility_check", C.c_uint8),
+                ("temporal_reuse", C.c_uint8), ("enable_shading", C.c_uint8),
+                ("enable_texture_mapping", C.c_uint8), ("enable_tone_mapping", C.c_uint8),
+                ("gamma", C.c_float), ("exposure", C.c_float)]
+
+
+class Tile(C.Structure):
+    _fields_ = [("global_width", C.c_uint32), ("global_height", C.c_uint32),
+                ("x0", C.c_uint32), ("y0", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("gx0", C.c_uint32), ("gy0", C.c_uint32), ("gwidth", C.c_uint32), ("gheight", C.c_uint32)]
+
+
+assert C.sizeof(Light) == 88
+assert C.sizeof(Material) == 32
+assert C.sizeof(Features) == 44
+
+
+def default_features(**overrides) -> Features:
+    """struct Features defaults (src/utils/common.h:89-136) with rayTraceMode = ReSTIR."""
+    f = Features(ray_trace_mode=MODE_RESTIR, initial_light_samples=32, num_samples_in_reservoir=2,
+                 num_neighbours_to_sample=5, spatial_resample_radius=10, spatial_resampling_passes=2,
+                 temporal_clamp_m=20, initial_samples_visibility_check=0, unbiased_combination=0,
+                 spatial_reuse=1, spatial_reuse_visibility_check=0, temporal_reuse=1, enable_shading=1,
+                 enable_texture_mapping=1, enable_tone_mapping=1, gamma=1.0, exposure=1.5)
+    for k, v in overrides.items():
+        if not hasattr(f, k):
+            raise AttributeError(f"Features has no field {k!r}")
+        setattr(f, k, v)
+    return f
+
+
+# Exported symbols of include/restir_c.h with their ctypes signatures.
+_P = C.c_void_p
+SIGNATURES = {
+    "restir_features_default": (None, [C.POINTER(Features)]),
+    "restir_rng_key": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "restir_rng_draw": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),
+    "restir_camera_derive": (None, [C.POINTER(Camera), C.POINTER(CameraFrame)]),
+    "restir_tile_plan": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                   C.POINTER(Tile)]),
+    "restir_last_error": (C.c_char_p, []),
+    "restir_abi_version": (C.c_int, []),
+    "restir_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "restir_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "restir_destroy": (None, [_P]),
+    "restir_set_seed": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
+    "restir_set_scene": (C.c_int, [_P, C.POINTER(Mesh), C.c_uint32, C.POINTER(Light), C.c_uint32]),
+    "restir_render": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Features), C.c_uint32, C.c_uint32,
+                                C.POINTER(Tile), _P, C.POINTER(_P), C.POINTER(C.c_float)]),
+    "restir_frame_retain": (C.c_int, [_P]),
+    "restir_frame_release": (None, [_P]),
+    "restir_synchronize": (C.c_int, [_P]),
+    "restir_download_rgb": (C.c_int, [_P, C.POINTER(C.c_float), C.c_size_t]),
+    "restir_stage_configure": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "restir_stage_upload": (C.c_int, [_P, C.c_int, _P, C.c_size_t]),
+    "restir_stage_download": (C.c_int, [_P, C.c_int, _P, C.c_size_t]),
+    "restir_stage_primary": (C.c_int, [_P, C.POINTER(Camera)]),
+    "restir_stage_ris": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Features), C.c_uint32, C.c_int]),
+    "restir_stage_temporal": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Features), C.c_uint32, C.c_int]),
+    "restir_stage_spatial": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Features), C.c_uint32, C.c_int]),
+    "restir_stage_final": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Features)]),
+    "restir_debug_math": (C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                    C.POINTER(C.c_float), C.c_size_t]),
+    "restir_enable_timing": (C.c_int, [_P, C.c_int]),
+    "restir_timings": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    "restir_reset_timings": (C.c_int, [_P]),
+}
+
+
+class RestirError(RuntimeError):
+    """Mirrors the reference's std::runtime_error convention (render.cpp:99,278)."""
+
+
+_lib = None
+
+
+def load_library(path: str | None = None) -> C.CDLL:
+    """Load libromis_amd.so and bind every symbol of include/restir_c.h.  Raises if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or os.environ.get("ROMIS_AMD_LIB", LIB_PATH)
+    if not os.path.exists(p):
+        raise RestirError(f"libromis_amd.so not found at {p}: build it with `python -m romis_amd.build` "
+                          "(there is no CPU fallback for the HIP path)")
+    lib = C.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(lib: C.CDLL, status: int, what: str = "") -> None:
+    if status != 0:
+        msg = lib.restir_last_error()
+        raise RestirError(f"{what}: {STATUS_NAMES.get(status, status)}: {msg.decode() if msg else ''}")

@@ -1,0 +1,75 @@
+"""Build libromis_amd.so in-tree (romis_amd/_build/) with hipcc for gfx950.
+
+    python -m romis_amd.build [--force]
+
+Flags that matter for parity (DESIGN.md "Floating point"): -ffp-contract=off (no FMA contraction, host and
+device), correctly rounded f32 division / sqrt, no fast-math.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "_build")
+LIB = os.path.join(OUT, "libromis_amd.so")
+ARCH = os.environ.get("ROMIS_AMD_ARCH", "gfx950")
+
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"-I{os.path.join(ROOT, 'include')}",
+          f"-I{CSRC}"]
+DEVICE = [f"--offload-arch={ARCH}", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-rdc"]
+
+SOURCES = [
+    ("kernels.hip", ["-x", "hip"] + DEVICE),
+    ("restir.cpp", ["-x", "hip"] + DEVICE),
+    ("bvh.cpp", ["-x", "c++"]),
+]
+HEADERS = ["device_math.h", "restir_types.h", "launch.h", "bvh.h"]
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src: str, extra: list[str], force: bool) -> str:
+    obj = os.path.join(OUT, os.path.basename(src) + ".o")
+    deps = [os.path.join(CSRC, src)] + [os.path.join(CSRC, h) for h in HEADERS] + \
+        [os.path.join(ROOT, "include", "restir_c.h"), __file__]
+    if force or _stale(obj, deps):
+        cmd = [HIPCC] + COMMON + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
+        subprocess.check_call(cmd)
+    return obj
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(OUT, exist_ok=True)
+    with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        objs = list(ex.map(lambda s: _compile(s[0], s[1], force), SOURCES))
+    if force or _stale(LIB, objs):
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fno-gpu-rdc", "-o", LIB] + objs
+        subprocess.check_call(cmd)
+    if verbose:
+        print(LIB)
+    return LIB
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    args = ap.parse_args(argv)
+    build(force=args.force, verbose=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,643 @@
+// kernels.hip -- hand-written gfx950 (CDNA4) kernels of the ReSTIR direct-lighting path.
+//
+//   k_primary   genPrimaryRayHits (render_utils.cpp:13-34) + closestHit (embree_interface.cpp:64-90)
+//   k_ris       genInitialSamples / genCanonicalSamples (render_utils.cpp:36-52, light.cpp:39-99)
+//   k_temporal  temporalReuse + Reservoir::combineBiased (render_utils.cpp:142-177, reservoir.cpp:40-66)
+//   k_spatial   spatialReuse, one pass (render_utils.cpp:87-140) + combineBiased / combineUnbiased
+//               (reservoir.cpp:40-104)
+//   k_final     final shading + tone map + Screen y-flip (render.cpp:38-58, render_utils.cpp:54-65,
+//               tone_mapping.cpp:8-11, screen.cpp:37-43)
+//
+// One lane per pixel throughout: the reservoir update (Reservoir::update, reservoir.cpp:10-32) is a serial
+// prefix over the candidate stream whose float rounding must match the reference order exactly, so it stays
+// a per-lane loop; the wave's 64 lanes work on 64 pixels.  Reservoirs and the G-buffer are SoA float4 planes
+// read with 16-byte coalesced loads.  Visibility uses a stackless threaded BVH (no scratch stack).
+#include "device_math.h"
+#include "restir_types.h"
+
+#include <float.h>
+
+namespace romis {
+
+#define ROMIS_FLT_MAX 3.402823466e+38F
+#define ROMIS_FLT_MIN 1.175494351e-38F
+
+// ---------------------------------------------------------------------------------------------------------
+// Ray / triangle, Moller-Trumbore, hit iff 0 < t <= tfar (Embree's (tnear, tfar] convention; the oracle
+// restates the same routine).
+__device__ __forceinline__ bool tri_hit(float4 v0, float4 e1_, float4 e2_, v3 o, v3 d, float tfar, float& t_out,
+                                        float& u_out, float& v_out) {
+    v3 e1 = xyz(e1_), e2 = xyz(e2_);
+    v3 pvec = vcross(d, e2);
+    float det = vdot(e1, pvec);
+    if (det == 0.0f) return false;
+    float inv = 1.0f / det;
+    v3 tvec = vsub(o, xyz(v0));
+    float u = vdot(tvec, pvec) * inv;
+    if (!(u >= 0.0f && u <= 1.0f)) return false;
+    v3 qvec = vcross(tvec, e1);
+    float v = vdot(d, qvec) * inv;
+    if (!(v >= 0.0f && u + v <= 1.0f)) return false;
+    float t = vdot(e2, qvec) * inv;
+    if (!(t > 0.0f && t <= tfar)) return false;
+    t_out = t; u_out = u; v_out = v;
+    return true;
+}
+
+// Conservative slab test (boxes are padded on the host, the interval is widened): it may accept extra boxes,
+// never reject one that holds a valid hit, so traversal results equal the brute-force oracle.
+__device__ __forceinline__ bool box_hit(float4 lo, float4 hi, v3 o, v3 invd, float tmax_box) {
+    float tx0 = (lo.x - o.x) * invd.x, tx1 = (hi.x - o.x) * invd.x;
+    float ty0 = (lo.y - o.y) * invd.y, ty1 = (hi.y - o.y) * invd.y;
+    float tz0 = (lo.z - o.z) * invd.z, tz1 = (hi.z - o.z) * invd.z;
+    float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax_box));
+    return tmin <= tmax;
+}
+
+__device__ __forceinline__ v3 safe_inv(v3 d) {
+    return mk(1.0f / (d.x == 0.0f ? copysignf(1e-30f, d.x) : d.x), 1.0f / (d.y == 0.0f ? copysignf(1e-30f, d.y) : d.y),
+              1.0f / (d.z == 0.0f ? copysignf(1e-30f, d.z) : d.z));
+}
+
+__device__ __forceinline__ float widen(float t) { return t * 1.0001f + 1e-4f; }
+
+// any hit in (0, tfar] -- EmbreeInterface::anyHit (embree_interface.cpp:58-62)
+__device__ bool occluded(const SceneDev& s, v3 o, v3 d, float tfar) {
+    v3 invd = safe_inv(d);
+    float tb = widen(tfar);
+    uint32_t i = 0;
+    while (i < s.num_nodes) {
+        float4 lo = s.nodes[2 * i], hi = s.nodes[2 * i + 1];
+        uint32_t miss = __float_as_uint(lo.w), leaf = __float_as_uint(hi.w);
+        if (box_hit(lo, hi, o, invd, tb)) {
+            if (leaf) {
+                uint32_t first = leaf & 0xFFFFFFu, cnt = leaf >> 24;
+                for (uint32_t k = 0; k < cnt; k++) {
+                    float t, u, v;
+                    if (tri_hit(s.tri_v0[first + k], s.tri_e1[first + k], s.tri_e2[first + k], o, d, tfar, t, u, v))
+                        return true;
+                }
+                i = miss;
+            } else {
+                i = i + 1;
+            }
+        } else {
+            i = miss;
+        }
+    }
+    return false;
+}
+
+// closest hit: minimal t, lowest original triangle index on ties
+__device__ bool closest(const SceneDev& s, v3 o, v3 d, float& t_best, float& u_best, float& v_best, uint32_t& tri_best) {
+    v3 invd = safe_inv(d);
+    bool found = false;
+    t_best = ROMIS_FLT_MAX;
+    tri_best = 0xFFFFFFFFu;
+    uint32_t i = 0;
+    while (i < s.num_nodes) {
+        float4 lo = s.nodes[2 * i], hi = s.nodes[2 * i + 1];
+        uint32_t miss = __float_as_uint(lo.w), leaf = __float_as_uint(hi.w);
+        if (box_hit(lo, hi, o, invd, widen(t_best))) {
+            if (leaf) {
+                uint32_t first = leaf & 0xFFFFFFu, cnt = leaf >> 24;
+                for (uint32_t k = 0; k < cnt; k++) {
+                    float4 v0 = s.tri_v0[first + k];
+                    float t, u, v;
+                    if (tri_hit(v0, s.tri_e1[first + k], s.tri_e2[first + k], o, d, ROMIS_FLT_MAX, t, u, v)) {
+                        uint32_t orig = __float_as_uint(v0.w);
+                        if (!found || t < t_best || (t == t_best && orig < tri_best)) {
+                            found = true; t_best = t; u_best = u; v_best = v; tri_best = orig;
+                        }
+                    }
+                }
+                i = miss;
+            } else {
+                i = i + 1;
+            }
+        } else {
+            i = miss;
+        }
+    }
+    return found;
+}
+
+// testVisibilityLightSample (utils.cpp:41-56)
+__device__ __forceinline__ bool visible(const SceneDev& s, v3 P, v3 y) {
+    v3 dir = vnormalize(vsub(y, P));
+    v3 P2 = vadd(P, vscale(dir, 1e-3f));
+    float tfar = vdistance(P2, y);
+    return !occluded(s, P2, dir, tfar);
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Pixel shading context
+struct Px {
+    v3 P, N, V;
+    float t;
+    float4 kd_sh;   // kd.xyz, shininess
+    float4 ks_tr;   // ks.xyz, transparency
+};
+
+__device__ __forceinline__ Px load_px(const SceneDev& s, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                      size_t p, v3 origin) {
+    Px r;
+    float4 a = n_t[p], b = p_mat[p];
+    r.N = xyz(a); r.t = a.w;
+    r.P = xyz(b);
+    uint32_t m = __float_as_uint(b.w);
+    if (m >= s.num_materials) m = s.num_materials - 1;
+    r.kd_sh = s.materials[2 * m];
+    r.ks_tr = s.materials[2 * m + 1];
+    r.V = vnormalize(vsub(origin, r.P));
+    return r;
+}
+
+// computeShading (shading.cpp:7-34)
+__device__ __forceinline__ v3 shade(const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
+    v3 kd = xyz(px.kd_sh);
+    if (!f.shading) return kd;
+    v3 L = vnormalize(vsub(lpos, px.P));
+    float dotNL = vdot(px.N, L);
+    if (dotNL < 0.0f) return mk(0.0f, 0.0f, 0.0f);
+    v3 R = vnormalize(vsub(vscale(px.N, 2.0f * dotNL), L));
+    float cosTheta = vdot(R, px.V);
+    v3 diffuse = vscale(vmul(lcol, kd), dotNL);
+    v3 specular = vscale(vmul(lcol, xyz(px.ks_tr)), pm_powf(cosTheta, px.kd_sh.w));
+    if (vany_nan(diffuse)) diffuse = mk(0.0f, 0.0f, 0.0f);
+    if (vany_nan(specular)) specular = mk(0.0f, 0.0f, 0.0f);
+    float d = vdistance(px.P, lpos);
+    if (fabsf(d) < 1e-5f) d = 1.0f;
+    return vdivs(vadd(diffuse, specular), d * d);
+}
+
+__device__ __forceinline__ float target_pdf(const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
+    return vlength(shade(f, px, lpos, lcol));
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Reservoir state (reservoir.h:28-73), one sub-reservoir
+struct Sub {
+    v3 pos, col;
+    float W;
+    uint32_t M;
+    float wsum, chosen;
+};
+
+__device__ __forceinline__ void sub_init(Sub& r) {
+    r.pos = mk(0.0f, 0.0f, 0.0f); r.col = mk(0.0f, 0.0f, 0.0f);
+    r.W = 0.0f; r.M = 1u; r.wsum = ROMIS_FLT_MIN; r.chosen = 0.0f;
+}
+
+// Reservoir::update (reservoir.cpp:10-32)
+__device__ __forceinline__ void sub_take(Sub& r, v3 pos, v3 col, float w, float u) {
+    r.M += 1u;
+    r.wsum += w;
+    if (u < (w / r.wsum)) { r.pos = pos; r.col = col; r.chosen = w; }
+}
+
+template <int NT>
+__device__ __forceinline__ uint32_t res_update(Sub* r, uint32_t N, v3 pos, v3 col, float w, float u) {
+    if (NT == 1) {
+        sub_take(r[0], pos, col, w, u);
+        return 0;
+    }
+    uint32_t k = 0;
+    float best = ROMIS_FLT_MAX;
+    const uint32_t n = NT > 0 ? (uint32_t)NT : N;
+    if (NT > 0) {
+        // compile-time N: predicated updates, no dynamic register indexing
+#pragma unroll
+        for (uint32_t j = 0; j < (uint32_t)(NT > 0 ? NT : 1); j++)
+            if (r[j].wsum < best) { k = j; best = r[j].wsum; }
+#pragma unroll
+        for (uint32_t j = 0; j < (uint32_t)(NT > 0 ? NT : 1); j++)
+            if (j == k) sub_take(r[j], pos, col, w, u);
+    } else {
+        for (uint32_t j = 0; j < n; j++)
+            if (r[j].wsum < best) { k = j; best = r[j].wsum; }
+        sub_take(r[k], pos, col, w, u);
+    }
+    return k;
+}
+
+template <int NT>
+__device__ __forceinline__ void macc_add(uint32_t* macc, uint32_t k, uint32_t m) {
+    if (NT > 0) {
+#pragma unroll
+        for (uint32_t j = 0; j < (uint32_t)(NT > 0 ? NT : 1); j++)
+            if (j == k) macc[j] += m;
+    } else {
+        macc[k] += m;
+    }
+}
+
+__device__ __forceinline__ float contribution_weight(float p, uint32_t M, float wsum) {
+    if (p == 0.0f) return 0.0f;
+    return ((1.0f / p) * (1.0f / (float)M)) * wsum;
+}
+
+__device__ __forceinline__ void sub_load(Sub& r, const float4* __restrict__ a, const float4* __restrict__ b, size_t i) {
+    float4 fa = a[i], fb = b[i];
+    r.pos = xyz(fa); r.W = fa.w;
+    r.col = xyz(fb); r.M = __float_as_uint(fb.w);
+    r.wsum = 0.0f; r.chosen = 0.0f;
+}
+
+__device__ __forceinline__ void sub_store(const Sub& r, float4* __restrict__ a, float4* __restrict__ b,
+                                          float2* __restrict__ dbg, size_t i) {
+    a[i] = make_float4(r.pos.x, r.pos.y, r.pos.z, r.W);
+    b[i] = make_float4(r.col.x, r.col.y, r.col.z, __uint_as_float(r.M));
+    if (dbg) dbg[i] = make_float2(r.wsum, r.chosen);
+}
+
+// Neighbour (x + dx, y + dy) clamped to the image (render_utils.cpp:109-110), then -- defensively -- to the
+// stored view (the host guarantees the view holds every reachable neighbour; this only prevents a fault).
+__device__ __forceinline__ size_t neighbour_index(const Region& rg, uint32_t x, uint32_t y, int dx, int dy) {
+    int nx = min(max((int)x + dx, 0), (int)rg.W - 1);
+    int ny = min(max((int)y + dy, 0), (int)rg.H - 1);
+    nx = min(max(nx, (int)rg.vx0), (int)(rg.vx0 + rg.vw) - 1);
+    ny = min(max(ny, (int)rg.vy0), (int)(rg.vy0 + rg.vh) - 1);
+    return (size_t)(ny - (int)rg.vy0) * rg.vw + (size_t)(nx - (int)rg.vx0);
+}
+
+__device__ __forceinline__ bool region_pixel(const Region& rg, uint32_t idx, uint32_t& x, uint32_t& y, size_t& p) {
+    if (idx >= rg.rw * rg.rh) return false;
+    x = rg.rx0 + idx % rg.rw;
+    y = rg.ry0 + idx / rg.rw;
+    p = (size_t)(y - rg.vy0) * rg.vw + (x - rg.vx0);
+    return true;
+}
+
+}  // namespace romis
+
+using namespace romis;
+
+// ---------------------------------------------------------------------------------------------------------
+// k_primary: one lane per pixel of rg's rect; writes n_t / p_mat.
+extern "C" __global__ __launch_bounds__(256) void k_primary(SceneDev s, Region rg, CameraDev cam, float4* __restrict__ n_t,
+                                                           float4* __restrict__ p_mat) {
+    uint32_t x, y;
+    size_t p;
+    if (!region_pixel(rg, blockIdx.x * blockDim.x + threadIdx.x, x, y, p)) return;
+    float nx = (float)x / (float)rg.W * 2.0f - 1.0f;
+    float ny = (float)y / (float)rg.H * 2.0f - 1.0f;
+    v3 csd = vnormalize(mk(-nx * cam.half_w, ny * cam.half_h, 1.0f));
+    v3 d = qrotate(cam.quat, csd);
+    v3 o = mk(cam.origin[0], cam.origin[1], cam.origin[2]);
+    float t, u = 0.0f, v = 0.0f;
+    uint32_t tri;
+    v3 n = mk(0.0f, 0.0f, 0.0f);
+    uint32_t m = s.num_materials - 1;
+    if (closest(s, o, d, t, u, v, tri)) {
+        float w0 = (1.0f - u) - v;
+        float4 a = s.tri_n0[tri], b = s.tri_n1[tri], c = s.tri_n2[tri];
+        n = vadd(vadd(vscale(xyz(a), w0), vscale(xyz(b), u)), vscale(xyz(c), v));
+        m = __float_as_uint(a.w);
+    } else {
+        t = ROMIS_FLT_MAX;
+    }
+    v3 P = vadd(o, vscale(d, t));
+    n_t[p] = make_float4(n.x, n.y, n.z, t);
+    p_mat[p] = make_float4(P.x, P.y, P.z, __uint_as_float(m));
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// k_ris: genCanonicalSamples per pixel.  Lane-serial candidate loop (M iterations) -- VALU bound.
+template <int NT>
+__device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
+                                         const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                         float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg) {
+    uint32_t x, y;
+    size_t p;
+    if (!region_pixel(rg, blockIdx.x * blockDim.x + threadIdx.x, x, y, p)) return;
+    const size_t npx = (size_t)rg.vw * rg.vh;
+    const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
+    Sub r[NT > 0 ? NT : RESTIR_MAX_N_DEV];
+    for (uint32_t j = 0; j < N; j++) sub_init(r[j]);
+    const uint32_t L = s.num_lights;
+    if (L != 0) {
+        Px px = load_px(s, n_t, p_mat, p, origin);
+        const uint32_t ps = pix_state(key, y * rg.W + x);
+        for (uint32_t j = 0; j < N; j++) r[j].M = 0u;
+        const float invL = 1.0f / (float)L;
+        for (uint32_t c = 0; c < f.M; c++) {
+            const float4* lt = s.lights + 7u * uniform_index(draw(ps, 4u * c), L);
+            float4 l0 = lt[0];
+            uint32_t type = __float_as_uint(l0.w);
+            v3 pos, col;
+            if (type == 0u) {
+                pos = xyz(l0);
+                col = xyz(lt[3]);
+            } else if (type == 1u) {
+                float fr = rand01(draw(ps, 4u * c + 1u));
+                pos = vmix(xyz(l0), xyz(lt[1]), fr);
+                col = vmix(xyz(lt[3]), xyz(lt[4]), fr);
+            } else {
+                float a = rand01(draw(ps, 4u * c + 1u));
+                float b = rand01(draw(ps, 4u * c + 2u));
+                pos = vadd(vadd(xyz(l0), vscale(xyz(lt[1]), a)), vscale(xyz(lt[2]), b));
+                v3 l01 = vmix(xyz(lt[3]), xyz(lt[4]), a);
+                v3 l23 = vmix(xyz(lt[5]), xyz(lt[6]), a);
+                col = vmix(l01, l23, b);
+            }
+            float w = target_pdf(f, px, pos, col) / invL;
+            res_update<NT>(r, N, pos, col, w, rand01(draw(ps, 4u * c + 3u)));
+        }
+        for (uint32_t j = 0; j < N; j++) {
+            if (f.initial_vis && !visible(s, px.P, r[j].pos)) r[j].W = 0.0f;
+            else r[j].W = contribution_weight(target_pdf(f, px, r[j].pos, r[j].col), r[j].M, r[j].wsum);
+        }
+    }
+    for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, j * npx + p);
+}
+
+#define ROMIS_RIS_KERNEL(NT)                                                                                          \
+    extern "C" __global__ __launch_bounds__(256) void k_ris_n##NT(SceneDev s, Region rg, FeaturesDev f, uint32_t key,  \
+                                                                 float ox, float oy, float oz, const float4* n_t,     \
+                                                                 const float4* p_mat, float4* ra, float4* rb,         \
+                                                                 float2* rdbg) {                                      \
+        ris_body<NT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg);                                        \
+    }
+ROMIS_RIS_KERNEL(1)
+ROMIS_RIS_KERNEL(2)
+ROMIS_RIS_KERNEL(0)
+
+// ---------------------------------------------------------------------------------------------------------
+// Combine state shared by temporal and spatial: out[] (Reservoir(N) of the current pixel) + routed M sums.
+template <int NT>
+struct Combiner {
+    Sub out[NT > 0 ? NT : RESTIR_MAX_N_DEV];
+    uint32_t macc[NT > 0 ? NT : RESTIR_MAX_N_DEV];
+    uint32_t N;
+    uint32_t t;      // update counter (RNG slot offset)
+    __device__ __forceinline__ void init(uint32_t n) {
+        N = NT > 0 ? (uint32_t)NT : n;
+        for (uint32_t j = 0; j < N; j++) { sub_init(out[j]); macc[j] = 0u; }
+        t = 0;
+    }
+    // combine one input sub-reservoir (reservoir.cpp:47-54 / :75-82)
+    __device__ __forceinline__ void consume(const FeaturesDev& f, const Px& cur, const Sub& in, uint32_t ps, uint32_t slot0) {
+        float pd = target_pdf(f, cur, in.pos, in.col);
+        float w = (pd * in.W) * (float)in.M;
+        uint32_t k = res_update<NT>(out, N, in.pos, in.col, w, rand01(draw(ps, slot0 + t)));
+        t++;
+        macc_add<NT>(macc, k, in.M);
+    }
+    __device__ __forceinline__ void finish_biased(const FeaturesDev& f, const Px& cur) {
+        for (uint32_t j = 0; j < N; j++) out[j].M = macc[j];
+        for (uint32_t j = 0; j < N; j++)
+            out[j].W = contribution_weight(target_pdf(f, cur, out[j].pos, out[j].col), out[j].M, out[j].wsum);
+    }
+};
+
+// k_temporal: temporalReuse (render_utils.cpp:142-177).  cur = (ca, cb), prev = (pa, pb); writes (oa, ob).
+template <int NT>
+__device__ __forceinline__ void temporal_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
+                                              v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                              const float4* ca, const float4* cb, const float4* __restrict__ pa,
+                                              const float4* __restrict__ pb, float4* oa, float4* ob, float2* odbg) {
+    uint32_t x, y;
+    size_t p;
+    if (!region_pixel(rg, blockIdx.x * blockDim.x + threadIdx.x, x, y, p)) return;
+    const size_t npx = (size_t)rg.vw * rg.vh;
+    const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
+    Px px = load_px(s, n_t, p_mat, p, origin);
+    Sub cur[NT > 0 ? NT : RESTIR_MAX_N_DEV], prev[NT > 0 ? NT : RESTIR_MAX_N_DEV];
+    unsigned long long mcur = 0, mprev = 0;
+    for (uint32_t j = 0; j < N; j++) {
+        sub_load(cur[j], ca, cb, j * npx + p);
+        sub_load(prev[j], pa, pb, j * npx + p);
+        mcur += cur[j].M;
+        mprev += prev[j].M;
+    }
+    unsigned long long C = (unsigned long long)f.clamp_m * mcur + 1ull;
+    if (mprev > C) {
+        for (uint32_t j = 0; j < N; j++)
+            if (prev[j].M != 0u) prev[j].M = (uint32_t)C;   // wSum scaling: never read by combineBiased
+    }
+    const uint32_t ps = pix_state(key, y * rg.W + x);
+    Combiner<NT> cmb;
+    cmb.init(N);
+    for (uint32_t j = 0; j < N; j++) cmb.consume(f, px, cur[j], ps, 0u);
+    for (uint32_t j = 0; j < N; j++) cmb.consume(f, px, prev[j], ps, 0u);
+    cmb.finish_biased(f, px);
+    for (uint32_t j = 0; j < N; j++) sub_store(cmb.out[j], oa, ob, odbg, j * npx + p);
+}
+
+#define ROMIS_TEMPORAL_KERNEL(NT)                                                                                      \
+    extern "C" __global__ __launch_bounds__(256) void k_temporal_n##NT(                                               \
+        SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,          \
+        const float4* p_mat, const float4* ca, const float4* cb, const float4* pa, const float4* pb, float4* oa,      \
+        float4* ob, float2* odbg) {                                                                                   \
+        temporal_body<NT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ca, cb, pa, pb, oa, ob, odbg);                   \
+    }
+ROMIS_TEMPORAL_KERNEL(1)
+ROMIS_TEMPORAL_KERNEL(2)
+ROMIS_TEMPORAL_KERNEL(0)
+
+// ---------------------------------------------------------------------------------------------------------
+// k_spatial: one spatialReuse pass.  Neighbours stream straight into the combine (accepted neighbours in draw
+// order, current last -- render_utils.cpp:108-124), so no per-lane candidate list is kept.
+template <int NT, bool UNBIASED>
+__device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
+                                             v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                             const float4* __restrict__ ia, const float4* __restrict__ ib,
+                                             float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg) {
+    uint32_t x, y;
+    size_t p;
+    if (!region_pixel(rg, blockIdx.x * blockDim.x + threadIdx.x, x, y, p)) return;
+    const size_t npx = (size_t)rg.vw * rg.vh;
+    const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
+    const uint32_t K = f.K;
+    const Px cur = load_px(s, n_t, p_mat, p, origin);
+    const uint32_t ps = pix_state(key, y * rg.W + x);
+    const uint32_t slot0 = 2u * K;
+    Combiner<NT> cmb;
+    cmb.init(N);
+    for (uint32_t n = 0; n < K; n++) {
+        const int dx = uniform_offset(draw(ps, 2u * n), f.R);
+        const int dy = uniform_offset(draw(ps, 2u * n + 1u), f.R);
+        const size_t q = neighbour_index(rg, x, y, dx, dy);
+        if (!UNBIASED) {
+            float4 g = n_t[q];
+            float depthFracDiff = fabsf(1.0f - (g.w / cur.t));
+            float normalsDotProd = vdot(xyz(g), cur.N);
+            if (depthFracDiff > 0.1f || normalsDotProd < 0.90630778703f) continue;
+        }
+        for (uint32_t j = 0; j < N; j++) {
+            Sub in;
+            sub_load(in, ia, ib, j * npx + q);
+            cmb.consume(f, cur, in, ps, slot0);
+        }
+    }
+    for (uint32_t j = 0; j < N; j++) {
+        Sub in;
+        sub_load(in, ia, ib, j * npx + p);
+        cmb.consume(f, cur, in, ps, slot0);
+    }
+    if (!UNBIASED) {
+        cmb.finish_biased(f, cur);
+    } else {
+        // combineUnbiased (reservoir.cpp:84-103): Z_j = sum over the stream of the input's total M where
+        // p_r(y_j) [* vis_r(y_j)] > 0.  The stream is re-derived from the same draws (no rejection here).
+        for (uint32_t j = 0; j < N; j++) cmb.out[j].M = cmb.macc[j];
+        unsigned long long Z[NT > 0 ? NT : RESTIR_MAX_N_DEV];
+        for (uint32_t j = 0; j < N; j++) Z[j] = 0ull;
+        for (uint32_t n = 0; n <= K; n++) {
+            size_t q = p;
+            if (n < K) q = neighbour_index(rg, x, y, uniform_offset(draw(ps, 2u * n), f.R),
+                                           uniform_offset(draw(ps, 2u * n + 1u), f.R));
+            Px rp = load_px(s, n_t, p_mat, q, origin);
+            unsigned long long tot = 0;
+            for (uint32_t j = 0; j < N; j++) tot += __float_as_uint(ib[j * npx + q].w);
+            for (uint32_t j = 0; j < N; j++) {
+                float pd = target_pdf(f, rp, cmb.out[j].pos, cmb.out[j].col);
+                if (f.spatial_vis) pd *= visible(s, rp.P, cmb.out[j].pos) ? 1.0f : 0.0f;
+                if (pd > 0.0f) Z[j] += tot;
+            }
+        }
+        for (uint32_t j = 0; j < N; j++) {
+            float pc = target_pdf(f, cur, cmb.out[j].pos, cmb.out[j].col);
+            if (pc == 0.0f || Z[j] == 0ull) cmb.out[j].W = 0.0f;
+            else cmb.out[j].W = ((1.0f / pc) * (1.0f / (float)Z[j])) * cmb.out[j].wsum;
+        }
+    }
+    for (uint32_t j = 0; j < N; j++) sub_store(cmb.out[j], oa, ob, odbg, j * npx + p);
+}
+
+#define ROMIS_SPATIAL_KERNEL(NT, UB, NAME)                                                                             \
+    extern "C" __global__ __launch_bounds__(256) void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
+                                                          float oy, float oz, const float4* n_t, const float4* p_mat,    \
+                                                          const float4* ia, const float4* ib, float4* oa, float4* ob,   \
+                                                          float2* odbg) {                                               \
+        spatial_body<NT, UB>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg);                          \
+    }
+ROMIS_SPATIAL_KERNEL(1, false, k_spatial_n1_biased)
+ROMIS_SPATIAL_KERNEL(2, false, k_spatial_n2_biased)
+ROMIS_SPATIAL_KERNEL(0, false, k_spatial_n0_biased)
+ROMIS_SPATIAL_KERNEL(1, true, k_spatial_n1_unbiased)
+ROMIS_SPATIAL_KERNEL(2, true, k_spatial_n2_unbiased)
+ROMIS_SPATIAL_KERNEL(0, true, k_spatial_n0_unbiased)
+
+// ---------------------------------------------------------------------------------------------------------
+// k_final: finalShading + exposureToneMapping + Screen::setPixel y-flip.  rgb rows: row 0 = top of rect.
+template <int NT>
+__device__ __forceinline__ void final_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, v3 origin,
+                                           const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                           const float4* __restrict__ ra, const float4* __restrict__ rb,
+                                           float* __restrict__ rgb) {
+    uint32_t x, y;
+    size_t p;
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!region_pixel(rg, idx, x, y, p)) return;
+    const size_t npx = (size_t)rg.vw * rg.vh;
+    const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
+    Px px = load_px(s, n_t, p_mat, p, origin);
+    v3 color = mk(0.0f, 0.0f, 0.0f);
+    for (uint32_t j = 0; j < N; j++) {
+        Sub r;
+        sub_load(r, ra, rb, j * npx + p);
+        v3 sc = shade(f, px, r.pos, r.col);
+        // The visibility test can only matter when the shaded value is non-zero: (vis ? sc : 0) * W equals
+        // sc * W when sc == 0 (both are 0 * W), so the shadow ray is skipped exactly then.
+        if ((sc.x != 0.0f || sc.y != 0.0f || sc.z != 0.0f) && !visible(s, px.P, r.pos)) sc = mk(0.0f, 0.0f, 0.0f);
+        sc = vscale(sc, r.W);
+        color = vadd(color, sc);
+    }
+    color = vdivs(color, (float)N);
+    if (f.tone_map) {
+        v3 e = vscale(mk(-color.x, -color.y, -color.z), f.exposure);
+        v3 mapped = mk(1.0f - pm_expf(e.x), 1.0f - pm_expf(e.y), 1.0f - pm_expf(e.z));
+        float g = 1.0f / f.gamma;
+        color = mk(pm_powf(mapped.x, g), pm_powf(mapped.y, g), pm_powf(mapped.z, g));
+    }
+    const uint32_t row = rg.rh - 1u - (y - rg.ry0);
+    float* o = rgb + 3 * ((size_t)row * rg.rw + (x - rg.rx0));
+    o[0] = color.x; o[1] = color.y; o[2] = color.z;
+}
+
+#define ROMIS_FINAL_KERNEL(NT)                                                                                         \
+    extern "C" __global__ __launch_bounds__(256) void k_final_n##NT(SceneDev s, Region rg, FeaturesDev f, float ox,      \
+                                                                   float oy, float oz, const float4* n_t,               \
+                                                                   const float4* p_mat, const float4* ra,               \
+                                                                   const float4* rb, float* rgb) {                      \
+        final_body<NT>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb);                                              \
+    }
+ROMIS_FINAL_KERNEL(1)
+ROMIS_FINAL_KERNEL(2)
+ROMIS_FINAL_KERNEL(0)
+
+// ---------------------------------------------------------------------------------------------------------
+// Test hooks: device powf / expf on arrays (parity of the portable math with the oracle).
+extern "C" __global__ void k_debug_math(const float* x, const float* y, float* pw, float* ex, uint32_t n) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    pw[i] = pm_powf(x[i], y[i]);
+    ex[i] = pm_expf(x[i]);
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Host launchers (launch.h)
+#include "launch.h"
+
+namespace romis {
+namespace {
+constexpr uint32_t kBlock = 256;
+inline dim3 grid_for(const Region& rg) { return dim3((rg.rw * rg.rh + kBlock - 1) / kBlock); }
+}  // namespace
+
+hipError_t launch_primary(const SceneDev& s, const Region& rg, const CameraDev& cam, float4* n_t, float4* p_mat,
+                          hipStream_t stream) {
+    if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_primary, grid_for(rg), dim3(kBlock), 0, stream, s, rg, cam, n_t, p_mat);
+    return hipGetLastError();
+}
+
+hipError_t launch_ris(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* o,
+                      const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, hipStream_t stream) {
+    if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
+    auto k = f.N == 1 ? k_ris_n1 : (f.N == 2 ? k_ris_n2 : k_ris_n0);
+    hipLaunchKernelGGL(k, grid_for(rg), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ra, rb,
+                       rdbg);
+    return hipGetLastError();
+}
+
+hipError_t launch_temporal(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* o,
+                           const float4* n_t, const float4* p_mat, const float4* ca, const float4* cb,
+                           const float4* pa, const float4* pb, float4* oa, float4* ob, float2* odbg,
+                           hipStream_t stream) {
+    if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
+    auto k = f.N == 1 ? k_temporal_n1 : (f.N == 2 ? k_temporal_n2 : k_temporal_n0);
+    hipLaunchKernelGGL(k, grid_for(rg), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ca, cb,
+                       pa, pb, oa, ob, odbg);
+    return hipGetLastError();
+}
+
+hipError_t launch_spatial(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* o,
+                          const float4* n_t, const float4* p_mat, const float4* ia, const float4* ib, float4* oa,
+                          float4* ob, float2* odbg, hipStream_t stream) {
+    if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
+    auto k = f.unbiased ? (f.N == 1 ? k_spatial_n1_unbiased : (f.N == 2 ? k_spatial_n2_unbiased : k_spatial_n0_unbiased))
+                        : (f.N == 1 ? k_spatial_n1_biased : (f.N == 2 ? k_spatial_n2_biased : k_spatial_n0_biased));
+    hipLaunchKernelGGL(k, grid_for(rg), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib,
+                       oa, ob, odbg);
+    return hipGetLastError();
+}
+
+hipError_t launch_final(const SceneDev& s, const Region& rg, const FeaturesDev& f, const float* o, const float4* n_t,
+                        const float4* p_mat, const float4* ra, const float4* rb, float* rgb, hipStream_t stream) {
+    if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
+    auto k = f.N == 1 ? k_final_n1 : (f.N == 2 ? k_final_n2 : k_final_n0);
+    hipLaunchKernelGGL(k, grid_for(rg), dim3(kBlock), 0, stream, s, rg, f, o[0], o[1], o[2], n_t, p_mat, ra, rb, rgb);
+    return hipGetLastError();
+}
+
+hipError_t launch_debug_math(const float* x, const float* y, float* pw, float* ex, uint32_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_debug_math, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, x, y, pw, ex, n);
+    return hipGetLastError();
+}
+
+}  // namespace romis

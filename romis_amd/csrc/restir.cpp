@@ -1,0 +1,838 @@
+// restir.cpp -- implementation of the C ABI in include/restir_c.h (host side of libromis_amd.so).
+//
+// Drop-in for renderReSTIR / renderRayTraced (src/rendering/render.cpp:28-62, :268-290): a context owns one
+// HIP device + stream, the uploaded scene (materials, lights, flattened BVH) and the per-frame device
+// buffers; every pass is one hand-written gfx950 kernel (kernels.hip) enqueued on the context's stream.
+#include "restir_c.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cfloat>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "bvh.h"
+#include "device_math.h"
+#include "launch.h"
+#include "restir_types.h"
+
+using namespace romis;
+
+// ---------------------------------------------------------------------------------------------------------
+// errors
+namespace {
+thread_local std::string g_err;
+
+restir_status fail(restir_status s, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return s;
+}
+
+#define HIP_TRY(expr)                                                                                   \
+    do {                                                                                                \
+        hipError_t e_ = (expr);                                                                         \
+        if (e_ != hipSuccess) return fail(RESTIR_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+#define ST_TRY(expr)                            \
+    do {                                        \
+        restir_status s_ = (expr);              \
+        if (s_ != RESTIR_OK) return s_;         \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    restir_status ensure(size_t n) {
+        if (n <= bytes && p) return RESTIR_OK;
+        release();
+        if (n == 0) n = 16;
+        hipError_t e = hipMalloc(&p, n);
+        if (e != hipSuccess) { p = nullptr; bytes = 0; return fail(RESTIR_ERR_HIP, "hipMalloc(%zu): %s", n, hipGetErrorString(e)); }
+        bytes = n;
+        return RESTIR_OK;
+    }
+    restir_status upload(const void* h, size_t n, hipStream_t s) {
+        ST_TRY(ensure(n));
+        HIP_TRY(hipMemcpyAsync(p, h, n, hipMemcpyHostToDevice, s));
+        return RESTIR_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+uint32_t f2u(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+float u2f(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+
+struct Pending {
+    int kernel;
+    hipEvent_t start, stop;
+};
+
+}  // namespace
+
+struct restir_frame {
+    std::atomic<int> refs{1};
+    int device = 0;
+    DevBuf a, b;
+    uint32_t W = 0, H = 0, vx0 = 0, vy0 = 0, vw = 0, vh = 0, N = 0;
+};
+
+struct restir_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+
+    // scene
+    DevBuf nodes, tri_v0, tri_e1, tri_e2, tri_n0, tri_n1, tri_n2, materials, lights;
+    SceneDev sdev{};
+    bool has_scene = false;
+
+    // work buffers for one view
+    uint32_t vw = 0, vh = 0, N = 0;
+    DevBuf n_t, p_mat, ra[2], rb[2], dbg[2], rgb;
+    int cur = 0;
+    uint32_t rgb_w = 0, rgb_h = 0;
+
+    // RNG
+    uint32_t seed = RESTIR_DEFAULT_SEED;
+    uint32_t frame_index = 0;
+
+    // stage API region
+    Region stage_rg{};
+    bool stage_ok = false;
+
+    // timing
+    bool timing = false;
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> free_events;
+    double ms[RESTIR_K_COUNT] = {0};
+    uint64_t launches[RESTIR_K_COUNT] = {0};
+};
+
+// ---------------------------------------------------------------------------------------------------------
+// pure host helpers
+extern "C" {
+
+const char* restir_last_error(void) { return g_err.c_str(); }
+int restir_abi_version(void) { return RESTIR_ABI_VERSION; }
+
+void restir_features_default(restir_features* out) {
+    if (!out) return;
+    std::memset(out, 0, sizeof(*out));
+    out->ray_trace_mode = RESTIR_MODE_RESTIR;
+    out->initial_light_samples = 32;
+    out->num_samples_in_reservoir = 2;
+    out->num_neighbours_to_sample = 5;
+    out->spatial_resample_radius = 10;
+    out->spatial_resampling_passes = 2;
+    out->temporal_clamp_m = 20;
+    out->initial_samples_visibility_check = 0;
+    out->unbiased_combination = 0;
+    out->spatial_reuse = 1;
+    out->spatial_reuse_visibility_check = 0;
+    out->temporal_reuse = 1;
+    out->enable_shading = 1;
+    out->enable_texture_mapping = 1;
+    out->enable_tone_mapping = 1;
+    out->gamma = 1.0f;
+    out->exposure = 1.5f;
+}
+
+uint32_t restir_rng_key(uint32_t seed, uint32_t frame, uint32_t stage, uint32_t pass) {
+    return mix32(mix32(mix32(seed ^ 0x9E3779B9u) + frame) ^ (stage * 0x01000193u + pass * 0x27D4EB2Fu));
+}
+
+uint32_t restir_rng_draw(uint32_t key, uint32_t global_pixel, uint32_t slot) {
+    return draw(pix_state(key, global_pixel), slot);
+}
+
+// Trackball (trackball.cpp:20-29, 75-78, 105-114) with glm::quat(euler) (type_quat.inl:208-217) and
+// quat * vec3 (type_quat.inl:347-354); plain float arithmetic, no contraction.
+void restir_camera_derive(const restir_camera* cam, restir_camera_frame* out) {
+    if (!cam || !out) return;
+    float hh = std::tan(cam->fovy / 2.0f);
+    float hw = cam->aspect * hh;
+    float hx = cam->rotation[0] * 0.5f, hy = cam->rotation[1] * 0.5f, hz = cam->rotation[2] * 0.5f;
+    float cx = std::cos(hx), cy = std::cos(hy), cz = std::cos(hz);
+    float sx = std::sin(hx), sy = std::sin(hy), sz = std::sin(hz);
+    float q[4];
+    q[3] = cx * cy * cz + sx * sy * sz;
+    q[0] = sx * cy * cz - cx * sy * sz;
+    q[1] = cx * sy * cz + sx * cy * sz;
+    q[2] = cx * cy * sz - sx * sy * cz;
+    // v = (0, 0, -distance): uv = cross(q.xyz, v), uuv = cross(q.xyz, uv), v + ((uv * w) + uuv) * 2
+    const float v[3] = {0.0f, 0.0f, -cam->distance};
+    float uv[3] = {q[1] * v[2] - v[1] * q[2], q[2] * v[0] - v[2] * q[0], q[0] * v[1] - v[0] * q[1]};
+    float uuv[3] = {q[1] * uv[2] - uv[1] * q[2], q[2] * uv[0] - uv[2] * q[0], q[0] * uv[1] - uv[0] * q[1]};
+    for (int a = 0; a < 3; a++) {
+        float r = v[a] + ((uv[a] * q[3]) + uuv[a]) * 2.0f;
+        out->origin[a] = cam->look_at[a] + r;
+    }
+    std::memcpy(out->quat, q, sizeof(q));
+    out->half_w = hw;
+    out->half_h = hh;
+}
+
+restir_status restir_tile_plan(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t tiles_y, uint32_t rank, uint32_t ghost,
+                               restir_tile* out) {
+    if (!out || W == 0 || H == 0 || tiles_x == 0 || tiles_y == 0 || rank >= tiles_x * tiles_y || tiles_x > W ||
+        tiles_y > H)
+        return fail(RESTIR_ERR_INVALID, "restir_tile_plan: bad arguments (W=%u H=%u tiles=%ux%u rank=%u)", W, H, tiles_x,
+                    tiles_y, rank);
+    const uint32_t tx = rank % tiles_x, ty = rank / tiles_x;
+    // even split, remainder to the first tiles (deterministic, every pixel owned exactly once)
+    auto span = [](uint32_t n, uint32_t parts, uint32_t i, uint32_t& s0, uint32_t& len) {
+        uint32_t base = n / parts, rem = n % parts;
+        s0 = i * base + std::min(i, rem);
+        len = base + (i < rem ? 1u : 0u);
+    };
+    restir_tile t{};
+    t.global_width = W;
+    t.global_height = H;
+    span(W, tiles_x, tx, t.x0, t.width);
+    span(H, tiles_y, ty, t.y0, t.height);
+    const uint32_t gx0 = t.x0 > ghost ? t.x0 - ghost : 0u;
+    const uint32_t gy0 = t.y0 > ghost ? t.y0 - ghost : 0u;
+    const uint32_t gx1 = std::min<uint64_t>((uint64_t)t.x0 + t.width + ghost, W);
+    const uint32_t gy1 = std::min<uint64_t>((uint64_t)t.y0 + t.height + ghost, H);
+    t.gx0 = gx0; t.gy0 = gy0; t.gwidth = gx1 - gx0; t.gheight = gy1 - gy0;
+    *out = t;
+    return RESTIR_OK;
+}
+
+restir_status restir_device_count(int* out) {
+    if (!out) return fail(RESTIR_ERR_INVALID, "restir_device_count: null");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) { *out = 0; return fail(RESTIR_ERR_NO_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e)); }
+    *out = n;
+    return RESTIR_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------------------
+// context helpers
+namespace {
+
+restir_status check_features(const restir_features* f) {
+    if (!f) return fail(RESTIR_ERR_INVALID, "features is NULL");
+    if (f->ray_trace_mode != RESTIR_MODE_RESTIR)
+        return fail(RESTIR_ERR_UNSUPPORTED, "rayTraceMode %u: only ReSTIR is implemented on this path (RMIS/ROMIS are out "
+                                            "of scope, SURVEY.md §2 #12)", f->ray_trace_mode);
+    if (f->num_samples_in_reservoir < 1 || f->num_samples_in_reservoir > RESTIR_MAX_N)
+        return fail(RESTIR_ERR_INVALID, "numSamplesInReservoir %u outside 1..%u", f->num_samples_in_reservoir, RESTIR_MAX_N);
+    if (f->spatial_resample_radius > 4096) return fail(RESTIR_ERR_INVALID, "spatialResampleRadius too large");
+    if (f->num_neighbours_to_sample > 4096) return fail(RESTIR_ERR_INVALID, "numNeighboursToSample too large");
+    if (f->gamma == 0.0f && f->enable_tone_mapping) { /* 1/gamma = inf, as in the reference */ }
+    return RESTIR_OK;
+}
+
+FeaturesDev to_dev(const restir_features* f) {
+    FeaturesDev d{};
+    d.M = f->initial_light_samples;
+    d.N = f->num_samples_in_reservoir;
+    d.K = f->num_neighbours_to_sample;
+    d.R = f->spatial_resample_radius;
+    d.clamp_m = f->temporal_clamp_m;
+    d.initial_vis = f->initial_samples_visibility_check;
+    d.unbiased = f->unbiased_combination;
+    d.spatial_vis = f->spatial_reuse_visibility_check;
+    d.shading = f->enable_shading;
+    d.tone_map = f->enable_tone_mapping;
+    d.gamma = f->gamma;
+    d.exposure = f->exposure;
+    return d;
+}
+
+restir_status ensure_work(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N, bool debug) {
+    const size_t npx = (size_t)vw * vh;
+    ST_TRY(c->n_t.ensure(npx * 16));
+    ST_TRY(c->p_mat.ensure(npx * 16));
+    for (int i = 0; i < 2; i++) {
+        ST_TRY(c->ra[i].ensure(npx * N * 16));
+        ST_TRY(c->rb[i].ensure(npx * N * 16));
+        if (debug) ST_TRY(c->dbg[i].ensure(npx * N * 8));
+    }
+    c->vw = vw; c->vh = vh; c->N = N;
+    return RESTIR_OK;
+}
+
+restir_status timed_begin(restir_ctx* c, int kernel, Pending& p) {
+    p.kernel = kernel;
+    p.start = p.stop = nullptr;
+    if (!c->timing) return RESTIR_OK;
+    for (hipEvent_t* e : {&p.start, &p.stop}) {
+        if (!c->free_events.empty()) { *e = c->free_events.back(); c->free_events.pop_back(); }
+        else HIP_TRY(hipEventCreate(e));
+    }
+    HIP_TRY(hipEventRecord(p.start, c->stream));
+    return RESTIR_OK;
+}
+
+restir_status timed_end(restir_ctx* c, Pending& p, hipError_t launch_err) {
+    if (launch_err != hipSuccess) return fail(RESTIR_ERR_HIP, "kernel launch: %s", hipGetErrorString(launch_err));
+    if (!c->timing) return RESTIR_OK;
+    HIP_TRY(hipEventRecord(p.stop, c->stream));
+    c->pending.push_back(p);
+    return RESTIR_OK;
+}
+
+restir_status collect_timings(restir_ctx* c) {
+    if (c->pending.empty()) return RESTIR_OK;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (Pending& p : c->pending) {
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, p.start, p.stop));
+        c->ms[p.kernel] += ms;
+        c->launches[p.kernel] += 1;
+        c->free_events.push_back(p.start);
+        c->free_events.push_back(p.stop);
+    }
+    c->pending.clear();
+    return RESTIR_OK;
+}
+
+#define TIMED(ctx, kid, call)                                   \
+    do {                                                        \
+        Pending p_;                                             \
+        ST_TRY(timed_begin((ctx), (kid), p_));                  \
+        ST_TRY(timed_end((ctx), p_, (call)));                   \
+    } while (0)
+
+CameraDev camera_dev(const restir_camera* cam) {
+    restir_camera_frame cf;
+    restir_camera_derive(cam, &cf);
+    CameraDev d{};
+    d.quat = make_float4(cf.quat[0], cf.quat[1], cf.quat[2], cf.quat[3]);
+    for (int a = 0; a < 3; a++) d.origin[a] = cf.origin[a];
+    d.half_w = cf.half_w;
+    d.half_h = cf.half_h;
+    return d;
+}
+
+Region make_region(uint32_t W, uint32_t H, uint32_t vx0, uint32_t vy0, uint32_t vw, uint32_t vh, uint32_t rx0,
+                   uint32_t ry0, uint32_t rw, uint32_t rh) {
+    Region r;
+    r.W = W; r.H = H;
+    r.vx0 = vx0; r.vy0 = vy0; r.vw = vw; r.vh = vh;
+    r.rx0 = rx0; r.ry0 = ry0; r.rw = rw; r.rh = rh;
+    return r;
+}
+
+// rect grown by g, clipped to the view
+Region grow_rect(const Region& base, uint32_t g) {
+    Region r = base;
+    uint32_t x0 = base.rx0 > base.vx0 + g ? base.rx0 - g : base.vx0;
+    uint32_t y0 = base.ry0 > base.vy0 + g ? base.ry0 - g : base.vy0;
+    uint64_t x1 = std::min<uint64_t>((uint64_t)base.rx0 + base.rw + g, (uint64_t)base.vx0 + base.vw);
+    uint64_t y1 = std::min<uint64_t>((uint64_t)base.ry0 + base.rh + g, (uint64_t)base.vy0 + base.vh);
+    r.rx0 = x0; r.ry0 = y0; r.rw = (uint32_t)(x1 - x0); r.rh = (uint32_t)(y1 - y0);
+    return r;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------------------
+extern "C" {
+
+restir_status restir_create(int device, restir_ctx** out) {
+    if (!out) return fail(RESTIR_ERR_INVALID, "restir_create: out is NULL");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return fail(RESTIR_ERR_NO_DEVICE, "no HIP device (%s)", hipGetErrorString(e));
+    if (device < 0) device = 0;
+    if (device >= n) return fail(RESTIR_ERR_NO_DEVICE, "device %d >= device count %d", device, n);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(RESTIR_ERR_NO_DEVICE, "device %d is %s; libromis_amd is built for gfx950 only", device, prop.gcnArchName);
+    HIP_TRY(hipSetDevice(device));
+    restir_ctx* c = new restir_ctx();
+    c->device = device;
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete c; return fail(RESTIR_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e)); }
+    *out = c;
+    return RESTIR_OK;
+}
+
+void restir_destroy(restir_ctx* c) {
+    if (!c) return;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        for (DevBuf* b : {&c->nodes, &c->tri_v0, &c->tri_e1, &c->tri_e2, &c->tri_n0, &c->tri_n1, &c->tri_n2,
+                          &c->materials, &c->lights, &c->n_t, &c->p_mat, &c->ra[0], &c->ra[1], &c->rb[0], &c->rb[1],
+                          &c->dbg[0], &c->dbg[1], &c->rgb})
+            b->release();
+        for (Pending& p : c->pending) { (void)hipEventDestroy(p.start); (void)hipEventDestroy(p.stop); }
+        for (hipEvent_t ev : c->free_events) (void)hipEventDestroy(ev);
+        (void)hipStreamDestroy(c->stream);
+    }
+    delete c;
+}
+
+restir_status restir_set_seed(restir_ctx* c, uint32_t seed, uint32_t frame_index) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->seed = seed;
+    c->frame_index = frame_index;
+    return RESTIR_OK;
+}
+
+restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_t num_meshes, const restir_light* lights,
+                               uint32_t num_lights) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    if (num_meshes && !meshes) return fail(RESTIR_ERR_INVALID, "meshes is NULL");
+    if (num_lights && !lights) return fail(RESTIR_ERR_INVALID, "lights is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+
+    // flatten triangles (mesh order = original index order, like the oracle)
+    std::vector<BvhTriangle> tris;
+    std::vector<float> n0, n1, n2;   // float4 records
+    for (uint32_t m = 0; m < num_meshes; m++) {
+        const restir_mesh& mesh = meshes[m];
+        if (mesh.num_triangles && (!mesh.positions || !mesh.normals || !mesh.triangles))
+            return fail(RESTIR_ERR_INVALID, "mesh %u: null arrays", m);
+        for (uint32_t i = 0; i < mesh.num_triangles; i++) {
+            const uint32_t* t = &mesh.triangles[3 * i];
+            if (t[0] >= mesh.num_vertices || t[1] >= mesh.num_vertices || t[2] >= mesh.num_vertices)
+                return fail(RESTIR_ERR_INVALID, "mesh %u triangle %u: vertex index out of range", m, i);
+            BvhTriangle bt;
+            std::memcpy(bt.v0, &mesh.positions[3 * t[0]], 12);
+            std::memcpy(bt.v1, &mesh.positions[3 * t[1]], 12);
+            std::memcpy(bt.v2, &mesh.positions[3 * t[2]], 12);
+            tris.push_back(bt);
+            for (int k = 0; k < 3; k++) {
+                std::vector<float>& dst = k == 0 ? n0 : (k == 1 ? n1 : n2);
+                dst.insert(dst.end(), &mesh.normals[3 * t[k]], &mesh.normals[3 * t[k]] + 3);
+                dst.push_back(k == 0 ? u2f(m) : 0.0f);
+            }
+        }
+    }
+    if (tris.size() >= (1u << 24)) return fail(RESTIR_ERR_INVALID, "too many triangles (%zu)", tris.size());
+    FlatBvh bvh = build_bvh(tris, 4);
+    const size_t T = tris.size();
+    std::vector<float> v0(4 * std::max<size_t>(T, 1)), e1(v0.size()), e2(v0.size());
+    for (size_t k = 0; k < T; k++) {
+        const BvhTriangle& t = tris[bvh.tri_order[k]];
+        for (int a = 0; a < 3; a++) {
+            v0[4 * k + a] = t.v0[a];
+            e1[4 * k + a] = t.v1[a] - t.v0[a];
+            e2[4 * k + a] = t.v2[a] - t.v0[a];
+        }
+        v0[4 * k + 3] = u2f(bvh.tri_order[k]);
+    }
+    // materials: one per mesh + the miss material (value-initialised HitInfo: kd 0, ks 0, shininess 1)
+    std::vector<float> mats(8 * (num_meshes + 1), 0.0f);
+    for (uint32_t m = 0; m < num_meshes; m++) {
+        const restir_material& mt = meshes[m].material;
+        mats[8 * m + 0] = mt.kd[0]; mats[8 * m + 1] = mt.kd[1]; mats[8 * m + 2] = mt.kd[2]; mats[8 * m + 3] = mt.shininess;
+        mats[8 * m + 4] = mt.ks[0]; mats[8 * m + 5] = mt.ks[1]; mats[8 * m + 6] = mt.ks[2]; mats[8 * m + 7] = mt.transparency;
+    }
+    mats[8 * num_meshes + 3] = 1.0f;
+    mats[8 * num_meshes + 7] = 1.0f;
+    // lights: 7 float4 records
+    std::vector<float> lt(28 * std::max<uint32_t>(num_lights, 1), 0.0f);
+    uint32_t types = 0;
+    for (uint32_t i = 0; i < num_lights; i++) {
+        const restir_light& l = lights[i];
+        if (l.type > RESTIR_LIGHT_PARALLELOGRAM) return fail(RESTIR_ERR_INVALID, "light %u: bad type %u", i, l.type);
+        types |= 1u << l.type;
+        float* o = &lt[28 * i];
+        const float* src[7] = {l.p0, l.p1, l.p2, l.c0, l.c1, l.c2, l.c3};
+        for (int r = 0; r < 7; r++) { std::memcpy(&o[4 * r], src[r], 12); o[4 * r + 3] = 0.0f; }
+        o[3] = u2f(l.type);
+    }
+    if (n0.empty()) { n0.assign(4, 0.0f); n1.assign(4, 0.0f); n2.assign(4, 0.0f); }
+    std::vector<float> nodes = bvh.nodes;
+    if (nodes.empty()) nodes.assign(8, 0.0f);
+
+    HIP_TRY(hipStreamSynchronize(c->stream));   // previous frames may still read the old scene
+    ST_TRY(c->nodes.upload(nodes.data(), nodes.size() * 4, c->stream));
+    ST_TRY(c->tri_v0.upload(v0.data(), v0.size() * 4, c->stream));
+    ST_TRY(c->tri_e1.upload(e1.data(), e1.size() * 4, c->stream));
+    ST_TRY(c->tri_e2.upload(e2.data(), e2.size() * 4, c->stream));
+    ST_TRY(c->tri_n0.upload(n0.data(), n0.size() * 4, c->stream));
+    ST_TRY(c->tri_n1.upload(n1.data(), n1.size() * 4, c->stream));
+    ST_TRY(c->tri_n2.upload(n2.data(), n2.size() * 4, c->stream));
+    ST_TRY(c->materials.upload(mats.data(), mats.size() * 4, c->stream));
+    ST_TRY(c->lights.upload(lt.data(), lt.size() * 4, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));   // host vectors go out of scope
+
+    SceneDev& s = c->sdev;
+    s.nodes = c->nodes.as<float4>();
+    s.num_nodes = bvh.num_nodes;
+    s.tri_v0 = c->tri_v0.as<float4>();
+    s.tri_e1 = c->tri_e1.as<float4>();
+    s.tri_e2 = c->tri_e2.as<float4>();
+    s.tri_n0 = c->tri_n0.as<float4>();
+    s.tri_n1 = c->tri_n1.as<float4>();
+    s.tri_n2 = c->tri_n2.as<float4>();
+    s.num_tris = (uint32_t)T;
+    s.materials = c->materials.as<float4>();
+    s.num_materials = num_meshes + 1;
+    s.lights = c->lights.as<float4>();
+    s.num_lights = num_lights;
+    s.light_types = types;
+    c->has_scene = true;
+    return RESTIR_OK;
+}
+
+// renderReSTIR (render.cpp:28-62)
+restir_status restir_render(restir_ctx* c, const restir_camera* cam, const restir_features* features, uint32_t width,
+                            uint32_t height, const restir_tile* tile, const restir_frame* prev, restir_frame** out_next,
+                            float* out_rgb) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    if (!cam) return fail(RESTIR_ERR_INVALID, "camera is NULL");
+    ST_TRY(check_features(features));
+    if (out_next) *out_next = nullptr;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->has_scene) return fail(RESTIR_ERR_STATE, "restir_render before restir_set_scene");
+    HIP_TRY(hipSetDevice(c->device));
+
+    restir_tile t{};
+    if (tile) {
+        t = *tile;
+        if (t.global_width != width || t.global_height != height)
+            return fail(RESTIR_ERR_INVALID, "tile global size %ux%u != %ux%u", t.global_width, t.global_height, width, height);
+        if (t.width == 0 || t.height == 0 || t.x0 + t.width > width || t.y0 + t.height > height || t.gx0 > t.x0 ||
+            t.gy0 > t.y0 || t.gx0 + t.gwidth < t.x0 + t.width || t.gy0 + t.gheight < t.y0 + t.height ||
+            t.gx0 + t.gwidth > width || t.gy0 + t.gheight > height)
+            return fail(RESTIR_ERR_INVALID, "inconsistent tile");
+    } else {
+        if (width == 0 || height == 0) return fail(RESTIR_ERR_INVALID, "empty image %ux%u", width, height);
+        t.global_width = width; t.global_height = height;
+        t.x0 = 0; t.y0 = 0; t.width = width; t.height = height;
+        t.gx0 = 0; t.gy0 = 0; t.gwidth = width; t.gheight = height;
+    }
+    const FeaturesDev f = to_dev(features);
+    const uint32_t N = f.N;
+    const uint32_t passes = features->spatial_reuse ? features->spatial_resampling_passes : 0u;
+    // the computed region must hold the ghost zone the spatial passes read (clipped at the image border)
+    {
+        restir_tile need{};
+        const uint64_t g = (uint64_t)passes * f.R;
+        uint32_t gx0 = t.x0 > g ? (uint32_t)(t.x0 - g) : 0u, gy0 = t.y0 > g ? (uint32_t)(t.y0 - g) : 0u;
+        uint64_t gx1 = std::min<uint64_t>((uint64_t)t.x0 + t.width + g, width);
+        uint64_t gy1 = std::min<uint64_t>((uint64_t)t.y0 + t.height + g, height);
+        if (t.gx0 > gx0 || t.gy0 > gy0 || (uint64_t)t.gx0 + t.gwidth < gx1 || (uint64_t)t.gy0 + t.gheight < gy1)
+            return fail(RESTIR_ERR_INVALID, "tile ghost zone narrower than passes * radius = %llu", (unsigned long long)g);
+        (void)need;
+    }
+    const bool temporal = features->temporal_reuse && prev != nullptr;
+    if (temporal) {
+        if (prev->N != N || prev->vw != t.gwidth || prev->vh != t.gheight || prev->vx0 != t.gx0 || prev->vy0 != t.gy0 ||
+            prev->W != width || prev->H != height)
+            return fail(RESTIR_ERR_INVALID, "temporal predecessor grid does not match this frame's region / N");
+        const bool has_ghost = t.gwidth != t.width || t.gheight != t.height;
+        if (has_ghost && passes > 0)
+            return fail(RESTIR_ERR_UNSUPPORTED, "temporal reuse on a ghost-zoned tile needs the predecessor's ghost zone "
+                                                "(halo exchange not implemented)");
+    }
+
+    ST_TRY(ensure_work(c, t.gwidth, t.gheight, N, false));
+    const size_t npx = (size_t)t.gwidth * t.gheight;
+    ST_TRY(c->rgb.ensure((size_t)t.width * t.height * 12));
+    c->rgb_w = t.width; c->rgb_h = t.height;
+
+    const CameraDev camd = camera_dev(cam);
+    const Region view = make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.gx0, t.gy0, t.gwidth, t.gheight);
+    const Region owned = make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.x0, t.y0, t.width, t.height);
+    const uint32_t frame = c->frame_index++;
+    const SceneDev& s = c->sdev;
+    float4* nt = c->n_t.as<float4>();
+    float4* pm = c->p_mat.as<float4>();
+    int cur = 0;
+
+    TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, nt, pm, c->stream));
+    TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, 0), camd.origin, nt, pm,
+                                      c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), nullptr, c->stream));
+    if (temporal) {
+        TIMED(c, RESTIR_K_TEMPORAL,
+              launch_temporal(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0), camd.origin, nt, pm,
+                              c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), prev->a.as<float4>(),
+                              prev->b.as<float4>(), c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), nullptr, c->stream));
+    }
+    for (uint32_t pass = 0; pass < passes; pass++) {
+        const Region pr = grow_rect(owned, (passes - 1u - pass) * f.R);
+        const int nxt = cur ^ 1;
+        TIMED(c, RESTIR_K_SPATIAL,
+              launch_spatial(s, pr, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_SPATIAL, pass), camd.origin, nt, pm,
+                             c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->ra[nxt].as<float4>(),
+                             c->rb[nxt].as<float4>(), nullptr, c->stream));
+        cur = nxt;
+    }
+    TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, nt, pm, c->ra[cur].as<float4>(), c->rb[cur].as<float4>(),
+                                          c->rgb.as<float>(), c->stream));
+    c->cur = cur;
+
+    if (out_next) {
+        restir_frame* fr = new restir_frame();
+        fr->device = c->device;
+        fr->W = width; fr->H = height; fr->vx0 = t.gx0; fr->vy0 = t.gy0; fr->vw = t.gwidth; fr->vh = t.gheight; fr->N = N;
+        // hand the final grid's buffers to the frame (no copy); the context re-allocates lazily
+        std::swap(fr->a, c->ra[cur]);
+        std::swap(fr->b, c->rb[cur]);
+        (void)npx;
+        *out_next = fr;
+    }
+    if (out_rgb) {
+        HIP_TRY(hipMemcpyAsync(out_rgb, c->rgb.p, (size_t)t.width * t.height * 12, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return RESTIR_OK;
+}
+
+restir_status restir_frame_retain(restir_frame* fr) {
+    if (!fr) return fail(RESTIR_ERR_INVALID, "frame is NULL");
+    fr->refs.fetch_add(1);
+    return RESTIR_OK;
+}
+
+void restir_frame_release(restir_frame* fr) {
+    if (!fr) return;
+    if (fr->refs.fetch_sub(1) == 1) {
+        (void)hipSetDevice(fr->device);
+        (void)hipDeviceSynchronize();
+        fr->a.release();
+        fr->b.release();
+        delete fr;
+    }
+}
+
+restir_status restir_synchronize(restir_ctx* c) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RESTIR_OK;
+}
+
+restir_status restir_download_rgb(restir_ctx* c, float* out_rgb, size_t count) {
+    if (!c || !out_rgb) return fail(RESTIR_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    const size_t need = (size_t)c->rgb_w * c->rgb_h * 3;
+    if (need == 0) return fail(RESTIR_ERR_STATE, "nothing rendered yet");
+    if (count < need) return fail(RESTIR_ERR_INVALID, "buffer holds %zu floats, need %zu", count, need);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(out_rgb, c->rgb.p, need * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RESTIR_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// stage API (parity tests): a whole width x height image, reservoir slot 0 = "current", slot 1 = "prev"
+restir_status restir_stage_configure(restir_ctx* c, uint32_t width, uint32_t height, uint32_t n) {
+    if (!c || width == 0 || height == 0 || n < 1 || n > RESTIR_MAX_N) return fail(RESTIR_ERR_INVALID, "bad stage size");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    ST_TRY(ensure_work(c, width, height, n, true));
+    ST_TRY(c->rgb.ensure((size_t)width * height * 12));
+    c->rgb_w = width; c->rgb_h = height;
+    c->stage_rg = make_region(width, height, 0, 0, width, height, 0, 0, width, height);
+    c->stage_ok = true;
+    c->cur = 0;
+    return RESTIR_OK;
+}
+
+static restir_status stage_buffer(restir_ctx* c, restir_buffer which, DevBuf** out, size_t* bytes) {
+    const size_t npx = (size_t)c->vw * c->vh;
+    const int cur = c->cur, prv = c->cur ^ 1;
+    switch (which) {
+        case RESTIR_BUF_GBUF_N_T: *out = &c->n_t; *bytes = npx * 16; break;
+        case RESTIR_BUF_GBUF_P_MAT: *out = &c->p_mat; *bytes = npx * 16; break;
+        case RESTIR_BUF_RES_A: *out = &c->ra[cur]; *bytes = npx * c->N * 16; break;
+        case RESTIR_BUF_RES_B: *out = &c->rb[cur]; *bytes = npx * c->N * 16; break;
+        case RESTIR_BUF_RES_DBG: *out = &c->dbg[cur]; *bytes = npx * c->N * 8; break;
+        case RESTIR_BUF_PREV_A: *out = &c->ra[prv]; *bytes = npx * c->N * 16; break;
+        case RESTIR_BUF_PREV_B: *out = &c->rb[prv]; *bytes = npx * c->N * 16; break;
+        case RESTIR_BUF_PREV_DBG: *out = &c->dbg[prv]; *bytes = npx * c->N * 8; break;
+        case RESTIR_BUF_RGB: *out = &c->rgb; *bytes = (size_t)c->rgb_w * c->rgb_h * 12; break;
+        default: return fail(RESTIR_ERR_INVALID, "unknown buffer %d", (int)which);
+    }
+    return RESTIR_OK;
+}
+
+restir_status restir_stage_upload(restir_ctx* c, restir_buffer which, const void* host, size_t bytes) {
+    if (!c || !host) return fail(RESTIR_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->stage_ok) return fail(RESTIR_ERR_STATE, "restir_stage_configure first");
+    DevBuf* b;
+    size_t need;
+    ST_TRY(stage_buffer(c, which, &b, &need));
+    if (bytes != need) return fail(RESTIR_ERR_INVALID, "buffer %d: %zu bytes given, %zu expected", (int)which, bytes, need);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(b->p, host, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RESTIR_OK;
+}
+
+restir_status restir_stage_download(restir_ctx* c, restir_buffer which, void* host, size_t bytes) {
+    if (!c || !host) return fail(RESTIR_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->stage_ok) return fail(RESTIR_ERR_STATE, "restir_stage_configure first");
+    DevBuf* b;
+    size_t need;
+    ST_TRY(stage_buffer(c, which, &b, &need));
+    if (bytes != need) return fail(RESTIR_ERR_INVALID, "buffer %d: %zu bytes given, %zu expected", (int)which, bytes, need);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(host, b->p, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RESTIR_OK;
+}
+
+#define STAGE_PRELUDE()                                                             \
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");                         \
+    std::lock_guard<std::mutex> lk(c->mu);                                          \
+    if (!c->stage_ok) return fail(RESTIR_ERR_STATE, "restir_stage_configure first"); \
+    if (!c->has_scene) return fail(RESTIR_ERR_STATE, "restir_set_scene first");      \
+    HIP_TRY(hipSetDevice(c->device))
+
+restir_status restir_stage_primary(restir_ctx* c, const restir_camera* cam) {
+    if (!cam) return fail(RESTIR_ERR_INVALID, "camera is NULL");
+    STAGE_PRELUDE();
+    const CameraDev camd = camera_dev(cam);
+    TIMED(c, RESTIR_K_PRIMARY, launch_primary(c->sdev, c->stage_rg, camd, c->n_t.as<float4>(), c->p_mat.as<float4>(), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RESTIR_OK;
+}
+
+static restir_status stage_features(restir_ctx* c, const restir_features* f, FeaturesDev& d) {
+    ST_TRY(check_features(f));
+    if (f->num_samples_in_reservoir != c->N)
+        return fail(RESTIR_ERR_INVALID, "N=%u but stage configured for N=%u", f->num_samples_in_reservoir, c->N);
+    d = to_dev(f);
+    return RESTIR_OK;
+}
+
+restir_status restir_stage_ris(restir_ctx* c, const restir_camera* cam, const restir_features* f, uint32_t key, int debug) {
+    if (!cam) return fail(RESTIR_ERR_INVALID, "camera is NULL");
+    STAGE_PRELUDE();
+    FeaturesDev d;
+    ST_TRY(stage_features(c, f, d));
+    const CameraDev camd = camera_dev(cam);
+    const int cur = c->cur;
+    TIMED(c, RESTIR_K_RIS, launch_ris(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
+                                      c->ra[cur].as<float4>(), c->rb[cur].as<float4>(),
+                                      debug ? c->dbg[cur].as<float2>() : nullptr, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RESTIR_OK;
+}
+
+restir_status restir_stage_temporal(restir_ctx* c, const restir_camera* cam, const restir_features* f, uint32_t key,
+                                    int debug) {
+    if (!cam) return fail(RESTIR_ERR_INVALID, "camera is NULL");
+    STAGE_PRELUDE();
+    FeaturesDev d;
+    ST_TRY(stage_features(c, f, d));
+    const CameraDev camd = camera_dev(cam);
+    const int cur = c->cur, prv = cur ^ 1;
+    TIMED(c, RESTIR_K_TEMPORAL,
+          launch_temporal(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
+                          c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->ra[prv].as<float4>(), c->rb[prv].as<float4>(),
+                          c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), debug ? c->dbg[cur].as<float2>() : nullptr,
+                          c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RESTIR_OK;
+}
+
+restir_status restir_stage_spatial(restir_ctx* c, const restir_camera* cam, const restir_features* f, uint32_t key,
+                                   int debug) {
+    if (!cam) return fail(RESTIR_ERR_INVALID, "camera is NULL");
+    STAGE_PRELUDE();
+    FeaturesDev d;
+    ST_TRY(stage_features(c, f, d));
+    const CameraDev camd = camera_dev(cam);
+    const int cur = c->cur, nxt = cur ^ 1;
+    TIMED(c, RESTIR_K_SPATIAL,
+          launch_spatial(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
+                         c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->ra[nxt].as<float4>(), c->rb[nxt].as<float4>(),
+                         debug ? c->dbg[nxt].as<float2>() : nullptr, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->cur = nxt;   // the pass output becomes "current" (RES_*), its input "prev" (PREV_*)
+    return RESTIR_OK;
+}
+
+restir_status restir_stage_final(restir_ctx* c, const restir_camera* cam, const restir_features* f) {
+    if (!cam) return fail(RESTIR_ERR_INVALID, "camera is NULL");
+    STAGE_PRELUDE();
+    FeaturesDev d;
+    ST_TRY(stage_features(c, f, d));
+    const CameraDev camd = camera_dev(cam);
+    const int cur = c->cur;
+    TIMED(c, RESTIR_K_FINAL, launch_final(c->sdev, c->stage_rg, d, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
+                                          c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->rgb.as<float>(), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RESTIR_OK;
+}
+
+restir_status restir_debug_math(restir_ctx* c, const float* x, const float* y, float* out_pow, float* out_exp, size_t n) {
+    if (!c || (n && (!x || !y || !out_pow || !out_exp))) return fail(RESTIR_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    DevBuf bx, by, bp, be;
+    ST_TRY(bx.upload(x, n * 4, c->stream));
+    ST_TRY(by.upload(y, n * 4, c->stream));
+    ST_TRY(bp.ensure(n * 4));
+    ST_TRY(be.ensure(n * 4));
+    hipError_t e = launch_debug_math(bx.as<float>(), by.as<float>(), bp.as<float>(), be.as<float>(), (uint32_t)n, c->stream);
+    if (e != hipSuccess) return fail(RESTIR_ERR_HIP, "debug math launch: %s", hipGetErrorString(e));
+    HIP_TRY(hipMemcpyAsync(out_pow, bp.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out_exp, be.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    bx.release(); by.release(); bp.release(); be.release();
+    return RESTIR_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// timing
+restir_status restir_enable_timing(restir_ctx* c, int enable) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->timing = enable != 0;
+    return RESTIR_OK;
+}
+
+restir_status restir_timings(restir_ctx* c, double* ms, uint64_t* launches) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    ST_TRY(collect_timings(c));
+    for (int k = 0; k < RESTIR_K_COUNT; k++) {
+        if (ms) ms[k] = c->ms[k];
+        if (launches) launches[k] = c->launches[k];
+    }
+    return RESTIR_OK;
+}
+
+restir_status restir_reset_timings(restir_ctx* c) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    ST_TRY(collect_timings(c));
+    for (int k = 0; k < RESTIR_K_COUNT; k++) { c->ms[k] = 0.0; c->launches[k] = 0; }
+    return RESTIR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,62 @@
+// restir_types.h -- device-side data layout shared by the kernels (kernels.hip) and the host launcher
+// (restir.cpp).  See DESIGN.md "Data layout in HBM".
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RESTIR_MAX_N_DEV 32u
+
+namespace romis {
+
+// Scene as the kernels see it.  All arrays are device pointers, 16-byte aligned float4 records.
+struct SceneDev {
+    // Threaded (stackless) BVH, depth-first order, 2 float4 per node:
+    //   nodes[2i]   = (lo.xyz, bits(miss link))       miss link = next node when the box is missed / leaf done
+    //   nodes[2i+1] = (hi.xyz, bits(leaf))            leaf = 0 for inner nodes (child = i + 1), else
+    //                                                  (count << 24) | first triangle (BVH order)
+    const float4* nodes;
+    uint32_t num_nodes;
+    // Triangles in BVH order (Moller-Trumbore operands, e1 = v1 - v0, e2 = v2 - v0 computed on the host):
+    //   tri_v0.w = bits(original triangle index) -- closest-hit ties resolve to the lowest original index
+    const float4* tri_v0;
+    const float4* tri_e1;
+    const float4* tri_e2;
+    // Shading attributes by ORIGINAL triangle index: vertex normals, n0.w = bits(material index)
+    const float4* tri_n0;
+    const float4* tri_n1;
+    const float4* tri_n2;
+    uint32_t num_tris;
+    // Materials: 2 float4 each: (kd.xyz, shininess), (ks.xyz, transparency).  Last entry = miss material.
+    const float4* materials;
+    uint32_t num_materials;
+    // Lights: 7 float4 each: (p0.xyz, bits(type)), (p1.xyz, 0), (p2.xyz, 0), c0, c1, c2, c3
+    const float4* lights;
+    uint32_t num_lights;
+    uint32_t light_types;      // bit t set <=> a light of type t is present
+    float box_pad;             // unused on device (bounds are padded on the host)
+};
+
+// Image region bookkeeping: global image W x H (y = 0 bottom), storage view (the computed region, row-major)
+// and the rectangle a pass writes.
+struct Region {
+    uint32_t W, H;
+    uint32_t vx0, vy0, vw, vh;
+    uint32_t rx0, ry0, rw, rh;
+};
+
+struct CameraDev {
+    float4 quat;      // x, y, z, w
+    float origin[3];
+    float half_w, half_h;
+};
+
+// The Features subset the kernels read.
+struct FeaturesDev {
+    uint32_t M, N, K, R;
+    uint32_t clamp_m;
+    uint32_t initial_vis, unbiased, spatial_vis, shading, tone_map;
+    float gamma, exposure;
+};
+
+}  // namespace romis

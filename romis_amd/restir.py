@@ -1,0 +1,170 @@
+"""Python host binding of the C ABI (include/restir_c.h) -- mirrors the reference's render surface.
+
+    renderer = Renderer(device=0)
+    renderer.set_scene(scene)                                  # EmbreeInterface(scene) (embree_interface.cpp:14-51)
+    rgb, grid = renderer.render_restir(prev_grid, camera, W, H, features)   # renderReSTIR (render.cpp:28-62)
+
+Errors raise RestirError (the reference throws std::runtime_error, render.cpp:99/278).  Everything runs in
+libromis_amd.so on the GPU; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from ._abi import RestirError, check  # noqa: F401
+
+
+class ReservoirGrid:
+    """Device-resident ReservoirGrid (reservoir.h:75) -- a reference-counted restir_frame handle."""
+
+    def __init__(self, lib, handle):
+        self._lib = lib
+        self.handle = handle
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            self._lib.restir_frame_release(self.handle)
+            self.handle = None
+
+
+class Renderer:
+    def __init__(self, device: int = 0):
+        self.lib = _abi.load_library()
+        h = C.c_void_p()
+        check(self.lib, self.lib.restir_create(device, C.byref(h)), "restir_create")
+        self.ctx = h
+        self._scene_keep = None
+        self.stage_shape = None
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.restir_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        self.close()
+
+    # ---- scene / seed -------------------------------------------------------------------------------
+    def set_scene(self, scene) -> None:
+        meshes, nm, lights, nl, keep = scene.to_abi()
+        check(self.lib, self.lib.restir_set_scene(self.ctx, meshes, nm, lights, nl), "restir_set_scene")
+        self._scene_keep = (meshes, lights, keep)
+
+    def set_seed(self, seed: int = _abi.RESTIR_DEFAULT_SEED, frame: int = 0) -> None:
+        check(self.lib, self.lib.restir_set_seed(self.ctx, seed, frame), "restir_set_seed")
+
+    # ---- frame ----------------------------------------------------------------------------------------
+    def render_restir(self, prev: ReservoirGrid | None, camera, width: int, height: int, features,
+                      tile=None, want_rgb: bool = True, want_grid: bool = True):
+        """renderReSTIR: returns (rgb [h][w][3] row 0 = top, or None; ReservoirGrid or None)."""
+        out = C.c_void_p()
+        rgb = None
+        rgb_ptr = None
+        if want_rgb:
+            h_ = tile.height if tile is not None else height
+            w_ = tile.width if tile is not None else width
+            rgb = np.zeros((h_, w_, 3), np.float32)
+            rgb_ptr = rgb.ctypes.data_as(C.POINTER(C.c_float))
+        st = self.lib.restir_render(self.ctx, C.byref(camera), C.byref(features), width, height,
+                                    C.byref(tile) if tile is not None else None,
+                                    prev.handle if prev is not None else None,
+                                    C.byref(out) if want_grid else None, rgb_ptr)
+        check(self.lib, st, "restir_render")
+        grid = ReservoirGrid(self.lib, out) if want_grid and out.value else None
+        return rgb, grid
+
+    def synchronize(self) -> None:
+        check(self.lib, self.lib.restir_synchronize(self.ctx), "restir_synchronize")
+
+    def download_rgb(self, width: int, height: int) -> np.ndarray:
+        rgb = np.zeros((height, width, 3), np.float32)
+        check(self.lib, self.lib.restir_download_rgb(self.ctx, rgb.ctypes.data_as(C.POINTER(C.c_float)), rgb.size),
+              "restir_download_rgb")
+        return rgb
+
+    # ---- timing ---------------------------------------------------------------------------------------
+    def enable_timing(self, on: bool = True) -> None:
+        check(self.lib, self.lib.restir_enable_timing(self.ctx, 1 if on else 0), "restir_enable_timing")
+
+    def timings(self):
+        ms = (C.c_double * _abi.K_COUNT)()
+        n = (C.c_uint64 * _abi.K_COUNT)()
+        check(self.lib, self.lib.restir_timings(self.ctx, ms, n), "restir_timings")
+        return {name: (ms[i], n[i]) for i, name in enumerate(_abi.KERNEL_NAMES)}
+
+    def reset_timings(self) -> None:
+        check(self.lib, self.lib.restir_reset_timings(self.ctx), "restir_reset_timings")
+
+    # ---- stage API (parity tests) ---------------------------------------------------------------------
+    def stage_configure(self, width: int, height: int, n: int) -> None:
+        check(self.lib, self.lib.restir_stage_configure(self.ctx, width, height, n), "restir_stage_configure")
+        self.stage_shape = (width, height, n)
+
+    def _shape(self, which):
+        w, h, n = self.stage_shape
+        npx = w * h
+        return {
+            _abi.BUF_GBUF_N_T: (npx, 4), _abi.BUF_GBUF_P_MAT: (npx, 4),
+            _abi.BUF_RES_A: (n, npx, 4), _abi.BUF_RES_B: (n, npx, 4), _abi.BUF_RES_DBG: (n, npx, 2),
+            _abi.BUF_PREV_A: (n, npx, 4), _abi.BUF_PREV_B: (n, npx, 4), _abi.BUF_PREV_DBG: (n, npx, 2),
+            _abi.BUF_RGB: (h, w, 3),
+        }[which]
+
+    def upload(self, which: int, arr: np.ndarray) -> None:
+        a = np.ascontiguousarray(arr, dtype=np.float32).reshape(self._shape(which))
+        check(self.lib, self.lib.restir_stage_upload(self.ctx, which, a.ctypes.data, a.nbytes), "restir_stage_upload")
+
+    def download(self, which: int) -> np.ndarray:
+        a = np.zeros(self._shape(which), np.float32)
+        check(self.lib, self.lib.restir_stage_download(self.ctx, which, a.ctypes.data, a.nbytes),
+              "restir_stage_download")
+        return a
+
+    def stage_primary(self, camera) -> None:
+        check(self.lib, self.lib.restir_stage_primary(self.ctx, C.byref(camera)), "restir_stage_primary")
+
+    def stage_ris(self, camera, features, key: int, debug: bool = True) -> None:
+        check(self.lib, self.lib.restir_stage_ris(self.ctx, C.byref(camera), C.byref(features), key, int(debug)),
+              "restir_stage_ris")
+
+    def stage_temporal(self, camera, features, key: int, debug: bool = True) -> None:
+        check(self.lib, self.lib.restir_stage_temporal(self.ctx, C.byref(camera), C.byref(features), key,
+                                                       int(debug)), "restir_stage_temporal")
+
+    def stage_spatial(self, camera, features, key: int, debug: bool = True) -> None:
+        check(self.lib, self.lib.restir_stage_spatial(self.ctx, C.byref(camera), C.byref(features), key,
+                                                      int(debug)), "restir_stage_spatial")
+
+    def stage_final(self, camera, features) -> None:
+        check(self.lib, self.lib.restir_stage_final(self.ctx, C.byref(camera), C.byref(features)),
+              "restir_stage_final")
+
+    def debug_math(self, x: np.ndarray, y: np.ndarray):
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.ascontiguousarray(y, np.float32)
+        pw = np.zeros_like(x)
+        ex = np.zeros_like(x)
+        FP = C.POINTER(C.c_float)
+        check(self.lib, self.lib.restir_debug_math(self.ctx, x.ctypes.data_as(FP), y.ctypes.data_as(FP),
+                                                   pw.ctypes.data_as(FP), ex.ctypes.data_as(FP), x.size),
+              "restir_debug_math")
+        return pw, ex
+
+
+def rng_key(seed: int, frame: int, stage: int, pass_: int = 0) -> int:
+    return _abi.load_library().restir_rng_key(seed, frame, stage, pass_)
+
+
+def tile_plan(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, ghost: int) -> _abi.Tile:
+    lib = _abi.load_library()
+    t = _abi.Tile()
+    check(lib, lib.restir_tile_plan(width, height, tiles_x, tiles_y, rank, ghost, C.byref(t)), "restir_tile_plan")
+    return t
+
+
+def tile_grid(n: int) -> tuple:
+    """Screen tiling for n ranks: 1x1, 2x1, 2x2, 4x2 (tiles_x, tiles_y)."""
+    return {1: (1, 1), 2: (2, 1), 4: (2, 2), 8: (4, 2)}.get(n) or (n, 1)

@@ -1,0 +1,353 @@
+"""GPU parity: every HIP kernel of libromis_amd.so against the CPU oracle (oracle/restir_oracle.c), through
+the C ABI.  Stage-isolated: each pass gets the ORACLE's inputs (G-buffer, reservoirs) uploaded, so a
+mismatch points at one kernel.  Bar: selected samples, M and every float bit-exact (the device reproduces
+the reference's float operation order; DESIGN.md "Floating point"); RGB within 1e-5 relative as north_star
+allows, checked bit-exact too where it holds.
+"""
+import numpy as np
+import pytest
+
+from romis_amd import _abi, scene
+
+pytestmark = pytest.mark.gpu
+
+W, H = 96, 64
+SEED = _abi.RESTIR_DEFAULT_SEED
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    from romis_amd import build, restir
+    build.build()
+    r = restir.Renderer(0)
+    yield r
+    r.close()
+
+
+_scenes = {}
+
+
+def get_scene(name):
+    if name not in _scenes:
+        _scenes[name] = scene.bench_scene(name) if name != "Cube" else scene.load_prebuilt("Cube")
+    return _scenes[name]
+
+
+def setup(gpu, oracle, name, N, w=W, h=H):
+    s = get_scene(name)
+    gpu.set_scene(s)
+    osc = oracle.OracleScene(s)
+    cam = scene.camera_for(name, w, h)
+    gpu.stage_configure(w, h, N)
+    return s, osc, cam
+
+
+def origin(oracle, cam):
+    return np.asarray(list(oracle.camera_frame(cam).origin), np.float32)
+
+
+def key(stage, p=0, frame=0):
+    from oracle import pyoracle
+    return pyoracle.lib().or_rng_key(SEED, frame, stage, p)
+
+
+def assert_bits(got, want, what):
+    g = np.ascontiguousarray(got, np.float32).reshape(-1)
+    w_ = np.ascontiguousarray(want, np.float32).reshape(-1)
+    assert g.shape == w_.shape, f"{what}: shape {g.shape} != {w_.shape}"
+    bad = np.flatnonzero(g.view(np.uint32) != w_.view(np.uint32))
+    assert bad.size == 0, f"{what}: {bad.size}/{g.size} words differ; first idx {bad[:4].tolist()} " \
+                          f"got {g[bad[:4]].tolist()} want {w_[bad[:4]].tolist()}"
+
+
+def oracle_ris(oracle, osc, f, cam, n_t, p_mat, frame=0, w=W, h=H):
+    return oracle.ris(osc, f, key(_abi.RESTIR_STAGE_RIS, 0, frame), origin(oracle, cam), w, h, n_t, p_mat)
+
+
+SCENES = ["nightclub_128pt", "nightclub_512", "cornell_parallelogram", "Cube"]
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_primary_gbuffer_bit_exact(gpu, oracle, name):
+    _, osc, cam = setup(gpu, oracle, name, 1)
+    gpu.stage_primary(cam)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    assert_bits(gpu.download(_abi.BUF_GBUF_N_T), n_t, "n_t")
+    assert_bits(gpu.download(_abi.BUF_GBUF_P_MAT), p_mat, "p_mat")
+    assert (n_t[:, 3] < 1e30).mean() > 0.3   # the camera sees geometry
+
+
+@pytest.mark.parametrize("name", SCENES)
+@pytest.mark.parametrize("N", [1, 2, 3])
+def test_ris_bit_exact(gpu, oracle, name, N):
+    _, osc, cam = setup(gpu, oracle, name, N)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    gpu.upload(_abi.BUF_GBUF_N_T, n_t)
+    gpu.upload(_abi.BUF_GBUF_P_MAT, p_mat)
+    f = _abi.default_features(num_samples_in_reservoir=N)
+    gpu.stage_ris(cam, f, key(_abi.RESTIR_STAGE_RIS))
+    a, b, d = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
+    assert_bits(gpu.download(_abi.BUF_RES_A), a, "res_a")
+    assert_bits(gpu.download(_abi.BUF_RES_B), b, "res_b")
+    assert_bits(gpu.download(_abi.BUF_RES_DBG), d, "wSum/chosen")
+
+
+@pytest.mark.parametrize("variant", ["visibility", "no_shading", "M1", "M64"])
+def test_ris_variants_bit_exact(gpu, oracle, variant):
+    N = 2
+    _, osc, cam = setup(gpu, oracle, "nightclub_512", N)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    gpu.upload(_abi.BUF_GBUF_N_T, n_t)
+    gpu.upload(_abi.BUF_GBUF_P_MAT, p_mat)
+    kw = {"visibility": dict(initial_samples_visibility_check=1), "no_shading": dict(enable_shading=0),
+          "M1": dict(initial_light_samples=1), "M64": dict(initial_light_samples=64)}[variant]
+    f = _abi.default_features(num_samples_in_reservoir=N, **kw)
+    gpu.stage_ris(cam, f, key(_abi.RESTIR_STAGE_RIS))
+    a, b, d = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
+    assert_bits(gpu.download(_abi.BUF_RES_A), a, "res_a")
+    assert_bits(gpu.download(_abi.BUF_RES_B), b, "res_b")
+
+
+def test_ris_no_lights(gpu, oracle):
+    s = get_scene("nightclub_128pt")
+    empty = scene.Scene(s.meshes, [], "dark")
+    gpu.set_scene(empty)
+    osc = oracle.OracleScene(empty)
+    cam = scene.nightclub_camera(W, H)
+    gpu.stage_configure(W, H, 2)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    gpu.upload(_abi.BUF_GBUF_N_T, n_t)
+    gpu.upload(_abi.BUF_GBUF_P_MAT, p_mat)
+    f = _abi.default_features()
+    gpu.stage_ris(cam, f, key(_abi.RESTIR_STAGE_RIS))
+    b = gpu.download(_abi.BUF_RES_B)
+    assert (b[..., 3].view(np.uint32) == 1).all()   # Reservoir(N) ctor M = 1 survives (light.cpp:46)
+    a, b2, _ = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
+    assert_bits(b, b2, "res_b")
+
+
+@pytest.mark.parametrize("N", [1, 2])
+@pytest.mark.parametrize("clamp", [20, 1])
+def test_temporal_bit_exact(gpu, oracle, N, clamp):
+    _, osc, cam = setup(gpu, oracle, "nightclub_128pt", N)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    f = _abi.default_features(num_samples_in_reservoir=N, temporal_clamp_m=clamp)
+    # predecessor = frame 0 after one spatial pass (so its M exceeds the clamp for clamp=1), current = frame 1 RIS
+    a0, b0, _ = oracle_ris(oracle, osc, f, cam, n_t, p_mat, frame=0)
+    pa, pb, _ = oracle.spatial_pass(osc, f, key(_abi.RESTIR_STAGE_SPATIAL, 0, 0), origin(oracle, cam), W, H, n_t,
+                                    p_mat, (a0, b0))
+    ca, cb, _ = oracle_ris(oracle, osc, f, cam, n_t, p_mat, frame=1)
+    for which, arr in [(_abi.BUF_GBUF_N_T, n_t), (_abi.BUF_GBUF_P_MAT, p_mat), (_abi.BUF_RES_A, ca),
+                       (_abi.BUF_RES_B, cb), (_abi.BUF_PREV_A, pa), (_abi.BUF_PREV_B, pb)]:
+        gpu.upload(which, arr)
+    kt = key(_abi.RESTIR_STAGE_TEMPORAL, 0, 1)
+    gpu.stage_temporal(cam, f, kt)
+    oa, ob, od = oracle.temporal(osc, f, kt, origin(oracle, cam), W, H, n_t, p_mat, (ca, cb), (pa, pb))
+    assert_bits(gpu.download(_abi.BUF_RES_A), oa, "res_a")
+    assert_bits(gpu.download(_abi.BUF_RES_B), ob, "res_b")
+    assert_bits(gpu.download(_abi.BUF_RES_DBG), od, "wSum/chosen")
+
+
+@pytest.mark.parametrize("name", ["nightclub_128pt", "cornell_parallelogram"])
+@pytest.mark.parametrize("N", [1, 2, 3])
+@pytest.mark.parametrize("mode", ["biased", "unbiased", "unbiased_vis"])
+def test_spatial_pass_bit_exact(gpu, oracle, name, N, mode):
+    _, osc, cam = setup(gpu, oracle, name, N)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    f = _abi.default_features(num_samples_in_reservoir=N, unbiased_combination=int(mode != "biased"),
+                              spatial_reuse_visibility_check=int(mode == "unbiased_vis"))
+    a, b, _ = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
+    for which, arr in [(_abi.BUF_GBUF_N_T, n_t), (_abi.BUF_GBUF_P_MAT, p_mat), (_abi.BUF_RES_A, a), (_abi.BUF_RES_B, b)]:
+        gpu.upload(which, arr)
+    for p in range(2):
+        kp = key(_abi.RESTIR_STAGE_SPATIAL, p)
+        gpu.stage_spatial(cam, f, kp)
+        a, b, d = oracle.spatial_pass(osc, f, kp, origin(oracle, cam), W, H, n_t, p_mat, (a, b))
+        assert_bits(gpu.download(_abi.BUF_RES_A), a, f"pass {p} res_a")
+        assert_bits(gpu.download(_abi.BUF_RES_B), b, f"pass {p} res_b")
+        assert_bits(gpu.download(_abi.BUF_RES_DBG), d, f"pass {p} wSum/chosen")
+
+
+@pytest.mark.parametrize("k,r", [(0, 10), (10, 30), (5, 1)])
+def test_spatial_neighbour_ranges(gpu, oracle, k, r):
+    N = 1
+    _, osc, cam = setup(gpu, oracle, "nightclub_128pt", N)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    f = _abi.default_features(num_samples_in_reservoir=N, num_neighbours_to_sample=k, spatial_resample_radius=r)
+    a, b, _ = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
+    for which, arr in [(_abi.BUF_GBUF_N_T, n_t), (_abi.BUF_GBUF_P_MAT, p_mat), (_abi.BUF_RES_A, a), (_abi.BUF_RES_B, b)]:
+        gpu.upload(which, arr)
+    kp = key(_abi.RESTIR_STAGE_SPATIAL, 0)
+    gpu.stage_spatial(cam, f, kp)
+    a2, b2, _ = oracle.spatial_pass(osc, f, kp, origin(oracle, cam), W, H, n_t, p_mat, (a, b))
+    assert_bits(gpu.download(_abi.BUF_RES_A), a2, "res_a")
+    assert_bits(gpu.download(_abi.BUF_RES_B), b2, "res_b")
+
+
+@pytest.mark.parametrize("N", [1, 2])
+@pytest.mark.parametrize("tonemap", [1, 0])
+def test_final_shading(gpu, oracle, N, tonemap):
+    _, osc, cam = setup(gpu, oracle, "nightclub_512", N)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    f = _abi.default_features(num_samples_in_reservoir=N, enable_tone_mapping=tonemap, gamma=2.2)
+    a, b, _ = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
+    for which, arr in [(_abi.BUF_GBUF_N_T, n_t), (_abi.BUF_GBUF_P_MAT, p_mat), (_abi.BUF_RES_A, a), (_abi.BUF_RES_B, b)]:
+        gpu.upload(which, arr)
+    gpu.stage_final(cam, f)
+    got = gpu.download(_abi.BUF_RGB)
+    want = oracle.final(osc, f, origin(oracle, cam), W, H, n_t, p_mat, (a, b))
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-7)
+    assert_bits(got, want, "rgb")
+
+
+def test_device_math_matches_oracle(gpu, oracle):
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(-1, 1, 4096), rng.uniform(0, 50, 4096), [0.0, -0.0, 1.0, -1.0, np.inf, -np.inf,
+                        np.nan, 1e-40, -3.0, 2.0]]).astype(np.float32)
+    y = np.concatenate([np.full(4096, 250.0), rng.uniform(-3, 3, 4096), [2.0, 3.0, np.nan, np.inf, -1.0, 3.0, 0.0,
+                        5.0, 0.5, -np.inf]]).astype(np.float32)
+    pw, ex = gpu.debug_math(x, y)
+    lib = oracle.lib()
+    want_pw = np.array([lib.or_powf(float(a), float(b)) for a, b in zip(x, y)], np.float32)
+    want_ex = np.array([lib.or_expf(float(a)) for a in x], np.float32)
+    assert_bits(pw, want_pw, "powf")
+    assert_bits(ex, want_ex, "expf")
+
+
+# --------------------------------------------------------------------------------------------------------
+# whole frames through restir_render (renderReSTIR)
+@pytest.mark.parametrize("name,N,passes,unbiased", [("nightclub_128pt", 1, 1, 0), ("nightclub_512", 2, 2, 0),
+                                                    ("cornell_parallelogram", 1, 2, 1)])
+def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased):
+    s = get_scene(name)
+    gpu.set_scene(s)
+    osc = oracle.OracleScene(s)
+    cam = scene.camera_for(name, W, H)
+    f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=passes, unbiased_combination=unbiased,
+                              temporal_reuse=0)
+    gpu.set_seed(SEED, 0)
+    rgb, grid = gpu.render_restir(None, cam, W, H, f)
+    want, _, _ = oracle.render_frame(osc, cam, f, W, H, SEED, 0)
+    np.testing.assert_allclose(rgb, want, rtol=1e-5, atol=1e-7)
+    assert_bits(rgb, want, "rgb")
+
+
+def test_temporal_sequence_matches_oracle(gpu, oracle):
+    """C3-style: 4 static frames, temporal reuse threading the previous frame's grid (main.cpp:165)."""
+    name = "nightclub_128pt"
+    s = get_scene(name)
+    gpu.set_scene(s)
+    osc = oracle.OracleScene(s)
+    cam = scene.camera_for(name, W, H)
+    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=2, temporal_reuse=1)
+    gpu.set_seed(SEED, 0)
+    prev_gpu, prev_or = None, None
+    for frame in range(4):
+        rgb, grid = gpu.render_restir(prev_gpu, cam, W, H, f)
+        want, res, _ = oracle.render_frame(osc, cam, f, W, H, SEED, frame, prev=prev_or)
+        assert_bits(rgb, want, f"frame {frame} rgb")
+        prev_gpu, prev_or = grid, res
+
+
+@pytest.mark.parametrize("tiles", [(2, 1), (2, 2), (4, 2)])
+def test_tiles_stitch_to_full_frame(gpu, oracle, tiles):
+    """Screen tiles with ghost zones (the multi-GPU decomposition) reproduce the single-GPU frame bit-exactly."""
+    from romis_amd import restir
+    name = "nightclub_128pt"
+    s = get_scene(name)
+    gpu.set_scene(s)
+    cam = scene.camera_for(name, W, H)
+    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=2, temporal_reuse=0)
+    gpu.set_seed(SEED, 0)
+    full, _ = gpu.render_restir(None, cam, W, H, f, want_grid=False)
+    stitched = np.zeros_like(full)
+    tx, ty = tiles
+    for rank in range(tx * ty):
+        t = restir.tile_plan(W, H, tx, ty, rank, f.spatial_resampling_passes * f.spatial_resample_radius)
+        gpu.set_seed(SEED, 0)
+        rgb, _ = gpu.render_restir(None, cam, W, H, f, tile=t, want_grid=False)
+        # rgb rows: row 0 = top of the tile; the full image's row 0 = top (global y = H - 1)
+        r0 = H - (t.y0 + t.height)
+        stitched[r0:r0 + t.height, t.x0:t.x0 + t.width] = rgb
+    assert_bits(stitched, full, "stitched tiles")
+
+
+# --------------------------------------------------------------------------------------------------------
+# full-size (BASELINE configs) checks: size-independent properties + oracle on sampled row bands
+def test_full_1080p_spatial_properties_and_sampled_parity(gpu, oracle):
+    Wf, Hf, N = 1920, 1080, 1
+    name = "nightclub_128pt"
+    s = get_scene(name)
+    gpu.set_scene(s)
+    osc = oracle.OracleScene(s)
+    cam = scene.camera_for(name, Wf, Hf)
+    gpu.stage_configure(Wf, Hf, N)
+    f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=1)
+    gpu.stage_primary(cam)
+    gpu.stage_ris(cam, f, key(_abi.RESTIR_STAGE_RIS))
+    n_t = gpu.download(_abi.BUF_GBUF_N_T)
+    p_mat = gpu.download(_abi.BUF_GBUF_P_MAT)
+    a0 = gpu.download(_abi.BUF_RES_A)
+    b0 = gpu.download(_abi.BUF_RES_B)
+    kp = key(_abi.RESTIR_STAGE_SPATIAL, 0)
+    gpu.stage_spatial(cam, f, kp)
+    a1 = gpu.download(_abi.BUF_RES_A)
+    b1 = gpu.download(_abi.BUF_RES_B)
+    M0 = b0[0, :, 3].view(np.uint32).astype(np.int64)
+    M1 = b1[0, :, 3].view(np.uint32).astype(np.int64)
+    # properties: M only grows, by whole input Ms, bounded by (k+1) * max input M; W finite, non-negative
+    assert (M1 >= M0).all() and (M1 <= (f.num_neighbours_to_sample + 1) * M0.max()).all()
+    assert np.isfinite(a1[0, :, 3]).all() and (a1[0, :, 3] >= 0).all()
+    # the selected light sample of every pixel is the sample of a pixel inside its (2r+1)^2 window
+    pos0 = a0[0, :, :3].reshape(Hf, Wf, 3)
+    pos1 = a1[0, :, :3].reshape(Hf, Wf, 3)
+    rng = np.random.default_rng(0)
+    r = f.spatial_resample_radius
+    for _ in range(200):
+        y, x = int(rng.integers(0, Hf)), int(rng.integers(0, Wf))
+        win = pos0[max(0, y - r):y + r + 1, max(0, x - r):x + r + 1].reshape(-1, 3)
+        assert (win == pos1[y, x]).all(axis=1).any()
+    # oracle parity on sampled row bands of the full-size frame
+    o = origin(oracle, cam)
+    for y0 in (0, 517, Hf - 8):
+        rect = oracle.Rect(0, y0, Wf, 8)
+        view = oracle.Rect(0, 0, Wf, Hf)
+        a2, b2, _ = oracle.spatial_pass(osc, f, kp, o, Wf, Hf, n_t, p_mat, (a0, b0), view=view, rect=rect)
+        sl = slice(y0 * Wf, (y0 + 8) * Wf)
+        assert_bits(a1[:, sl], a2[:, sl], f"band {y0} res_a")
+        assert_bits(b1[:, sl], b2[:, sl], f"band {y0} res_b")
+    # G-buffer + RIS on sampled bands too
+    n_t_or = np.zeros_like(n_t)
+    p_mat_or = np.zeros_like(p_mat)
+    from oracle import pyoracle
+    import ctypes as C
+    cf = pyoracle.camera_frame(cam)
+    for y0 in (3, 700):
+        rect = oracle.Rect(0, y0, Wf, 4)
+        view = oracle.Rect(0, 0, Wf, Hf)
+        pyoracle.lib().or_primary(osc.handle, C.byref(cf), Wf, Hf, view, rect, pyoracle.fp(n_t_or), pyoracle.fp(p_mat_or))
+        sl = slice(y0 * Wf, (y0 + 4) * Wf)
+        assert_bits(n_t[sl], n_t_or[sl], f"band {y0} n_t")
+        assert_bits(p_mat[sl], p_mat_or[sl], f"band {y0} p_mat")
+
+
+def test_full_1080p_render_deterministic(gpu):
+    name = "nightclub_128pt"
+    gpu.set_scene(get_scene(name))
+    cam = scene.camera_for(name, 1920, 1080)
+    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=1, temporal_reuse=0)
+    gpu.set_seed(SEED, 0)
+    a, _ = gpu.render_restir(None, cam, 1920, 1080, f, want_grid=False)
+    gpu.set_seed(SEED, 0)
+    b, _ = gpu.render_restir(None, cam, 1920, 1080, f, want_grid=False)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert np.isfinite(a).all() and (a >= 0).all() and a.mean() > 0.01
+
+
+def test_errors_are_reported(gpu):
+    from romis_amd._abi import RestirError
+    cam = scene.nightclub_camera(W, H)
+    with pytest.raises(RestirError, match="UNSUPPORTED"):
+        gpu.render_restir(None, cam, W, H, _abi.default_features(ray_trace_mode=_abi.MODE_ROMIS))
+    with pytest.raises(RestirError, match="INVALID"):
+        gpu.render_restir(None, cam, W, H, _abi.default_features(num_samples_in_reservoir=0))

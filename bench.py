@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mpixel-reservoirs/s of the ReSTIR frame (BASELINE.json metric) on 1..8 MI355X.
+
+One step = one renderReSTIR frame (render.cpp:28-62) of configs[1] of BASELINE.json: cornell-nightclub
+geometry, 128 point lights, 1920x1080 per GPU, M = 32 initial candidates, N = 1 reservoir, spatial reuse
+k = 5, r = 10, one pass (biased), no temporal reuse, shading + tone mapping on -- primary rays, initial RIS,
+spatial pass and final shading (shadow rays) all run on the GPU inside the timed region; inputs (scene, BVH)
+are resident in HBM before it starts and no host transfer happens inside it.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): weak scaling over screen
+tiles -- each rank owns a 1920x1080 tile of a (tx*1920) x (ty*1080) image (2x1, 2x2, 4x2) and computes its
+tile plus a ghost zone of passes*r pixels, so no data-path collective is needed (DESIGN.md "Multi-GPU");
+the barrier / max-over-ranks timing uses torch.distributed (RCCL).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md "Chip-level parameters")
+TILE_W, TILE_H = 1920, 1080
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--scene", default="nightclub_128pt")
+    ap.add_argument("--M", type=int, default=32)
+    ap.add_argument("--N", type=int, default=1)
+    ap.add_argument("--k", type=int, default=5)
+    ap.add_argument("--r", type=int, default=10)
+    ap.add_argument("--passes", type=int, default=1)
+    ap.add_argument("--tile-width", type=int, default=TILE_W)
+    ap.add_argument("--tile-height", type=int, default=TILE_H)
+    ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
+    ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
+    ap.add_argument("--cpu-rows", type=int, default=96, help="rows of the workload the CPU baseline renders")
+    ap.add_argument("--traffic-csv", default=None,
+                    help="rocprofv3 --pmc CSV (FETCH_SIZE / WRITE_SIZE) of this command for roofline.traffic")
+    return ap.parse_args()
+
+
+def dist_setup(n_gpus):
+    """(rank, world, local_rank, torch or None).  torch is imported before libromis_amd so both share one HIP runtime."""
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if world != n_gpus and rank == 0:
+        print(f"warning: --gpus {n_gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    return rank, world, local, torch
+
+
+def barrier_sync(torch, world, renderer):
+    renderer.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+
+def max_over_ranks(torch, world, value, local):
+    if world == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=torch.device("cuda", local))
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def pmc_traffic(path, kernel_prefix="k_spatial"):
+    """Per-launch HBM bytes of the spatial kernel from a rocprofv3 --pmc CSV (counter_collection.csv).
+    FETCH_SIZE / WRITE_SIZE are KB; FETCH_SIZE is doubled for wide coalesced streams on gfx950
+    (MI355X_MICROARCH.md "HBM")."""
+    import csv
+    fetch, write = {}, {}
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            if not row.get("Kernel_Name", "").startswith(kernel_prefix):
+                continue
+            d = row.get("Dispatch_Id")
+            name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
+            if name == "FETCH_SIZE":
+                fetch[d] = val
+            elif name == "WRITE_SIZE":
+                write[d] = val
+    if not fetch and not write:
+        return None
+    f = sum(fetch.values()) / max(1, len(fetch)) * 1024.0 * 2.0
+    w = sum(write.values()) / max(1, len(write)) * 1024.0
+    return f + w
+
+
+def cpu_baseline(sc, cam_fn, features, rows, W, H):
+    """The oracle (C restatement, OpenMP over rows) on a band of `rows` rows of the same workload."""
+    from oracle import pyoracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    osc = pyoracle.OracleScene(sc)
+    cam = cam_fn(W, H)
+    y0 = (H - rows) // 2
+    view = pyoracle.Rect(0, y0, W, rows)
+    pyoracle.render_frame(osc, cam, features, W, H, view=pyoracle.Rect(0, y0, W, 4), threads=threads)   # warm
+    t0 = time.perf_counter()
+    pyoracle.render_frame(osc, cam, features, W, H, view=view, threads=threads)
+    dt = time.perf_counter() - t0
+    px = W * rows * features.num_samples_in_reservoir
+    return {"value": round(px / dt / 1e6, 6), "unit": "Mpixel-reservoirs/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/restir_oracle.c frame (primary+RIS+spatial+final) on rows {y0}..{y0 + rows - 1} of the "
+                      f"{W}x{H} workload ({W * rows} px, {dt:.2f} s, OpenMP {threads} threads)"}
+
+
+def main():
+    args = parse()
+    rank, world, local, torch = dist_setup(args.gpus)
+    from romis_amd import _abi, restir, scene
+
+    tx, ty = restir.tile_grid(world)
+    GW, GH = tx * args.tile_width, ty * args.tile_height
+    sc = scene.bench_scene(args.scene)
+    cam = scene.camera_for(args.scene, GW, GH)
+    f = _abi.default_features(initial_light_samples=args.M, num_samples_in_reservoir=args.N,
+                              num_neighbours_to_sample=args.k, spatial_resample_radius=args.r,
+                              spatial_resampling_passes=args.passes, spatial_reuse=1 if args.passes > 0 else 0,
+                              temporal_reuse=0, unbiased_combination=0)
+    ghost = args.passes * args.r
+    tile = restir.tile_plan(GW, GH, tx, ty, rank, ghost)
+
+    r = restir.Renderer(local)
+    r.set_scene(sc)
+    r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
+
+    def step():
+        r.render_restir(None, cam, GW, GH, f, tile=tile, want_rgb=False, want_grid=False)
+
+    for _ in range(args.warmup):
+        step()
+    r.reset_timings()
+    r.enable_timing(True)
+    barrier_sync(torch, world, r)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier_sync(torch, world, r)
+    t1 = time.perf_counter()
+    r.enable_timing(False)
+    elapsed = max_over_ranks(torch, world, t1 - t0, local)
+    kt = r.timings()
+
+    ms_per_step = elapsed / args.steps * 1e3
+    owned_px = tile.width * tile.height            # identical on every rank (even split)
+    total = GW * GH * args.N
+    value = total / (elapsed / args.steps) / 1e6
+
+    # roofline of the spatial pass: algorithmic bytes = 64 B read (own G 32 B + own reservoir 32 B) +
+    # 32 B written per pixel per sub-reservoir ... N=1: read 32 + 32N, write 32N
+    sp_ms, sp_n = kt["spatial"]
+    roofline = None
+    if sp_n:
+        sp_px = (tile.width + 2 * 0) * tile.height   # pass p computes the tile grown by (P-1-p) r; P=1 -> tile
+        bytes_per_launch = sp_px * (32 + 32 * args.N + 32 * args.N)
+        avg_s = sp_ms / sp_n / 1e3
+        achieved = bytes_per_launch / avg_s / 1e9
+        traffic = pmc_traffic(args.traffic_csv) if args.traffic_csv else None
+        roofline = {"kernel": "k_spatial", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": traffic, "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(avg_s * 1e6, 2),
+                    "read_only_frac": round(sp_px * (32 + 32 * args.N) / avg_s / 1e9 / HBM_PEAK_GBS, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        cpu = cpu_baseline(sc, lambda w, h: scene.camera_for(args.scene, w, h), f, args.cpu_rows, GW, GH)
+
+    kernels = {k: {"ms_total": round(v[0], 4), "launches": int(v[1]),
+                   "us_per_launch": round(v[0] / v[1] * 1e3, 2) if v[1] else None} for k, v in kt.items()}
+    if rank == 0:
+        out = {
+            "metric": "Mpixel-reservoirs/s at 1080p, M=32, k=5 spatial; 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "Mpixel-reservoirs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (prebuilt cornell-nightclub geometry, 128 point lights, keyed RNG seed 0x5EED0001)",
+            "config": {"workload": "C2: cornell-nightclub 1080p per GPU, 128 point lights, M=32, N=1, spatial k=5 r=10 "
+                                   "x1 biased, no temporal, frame = primary+RIS+spatial+final",
+                       "scene": args.scene, "tile": [args.tile_width, args.tile_height], "image": [GW, GH],
+                       "tiles": [tx, ty], "M": args.M, "N": args.N, "k": args.k, "r": args.r, "passes": args.passes,
+                       "parallelism": f"screen tiles {tx}x{ty}, ghost {ghost}px"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernels": kernels,
+        }
+        print(json.dumps(out), flush=True)
+    r.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

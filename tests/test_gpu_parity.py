@@ -74,7 +74,7 @@ def test_primary_gbuffer_bit_exact(gpu, oracle, name):
     n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
     assert_bits(gpu.download(_abi.BUF_GBUF_N_T), n_t, "n_t")
     assert_bits(gpu.download(_abi.BUF_GBUF_P_MAT), p_mat, "p_mat")
-    assert (n_t[:, 3] < 1e30).mean() > 0.3   # the camera sees geometry
+    assert (n_t[:, 3] < 1e30).mean() > 0.05   # the camera sees geometry
 
 
 @pytest.mark.parametrize("name", SCENES)

@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--tile-height", type=int, default=TILE_H)
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    ap.add_argument("--cpu-rows", type=int, default=96, help="rows of the workload the CPU baseline renders")
+    ap.add_argument("--cpu-rows", type=int, default=540, help="rows of the workload the CPU baseline renders")
     ap.add_argument("--traffic-csv", default=None,
                     help="rocprofv3 --pmc CSV (FETCH_SIZE / WRITE_SIZE) of this command for roofline.traffic")
     return ap.parse_args()
@@ -110,16 +110,23 @@ def cpu_baseline(sc, cam_fn, features, rows, W, H):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     osc = pyoracle.OracleScene(sc)
     cam = cam_fn(W, H)
+    g = features.spatial_resampling_passes * features.spatial_resample_radius
     y0 = (H - rows) // 2
-    view = pyoracle.Rect(0, y0, W, rows)
-    pyoracle.render_frame(osc, cam, features, W, H, view=pyoracle.Rect(0, y0, W, 4), threads=threads)   # warm
+
+    def band(n):   # owned rows [y0, y0+n) plus the ghost rows the spatial passes read
+        return pyoracle.Rect(0, y0 - g, W, n + 2 * g), pyoracle.Rect(0, y0, W, n)
+
+    v, rc = band(2)
+    pyoracle.render_frame(osc, cam, features, W, H, view=v, rect=rc, threads=threads)   # warm
+    v, rc = band(rows)
     t0 = time.perf_counter()
-    pyoracle.render_frame(osc, cam, features, W, H, view=view, threads=threads)
+    pyoracle.render_frame(osc, cam, features, W, H, view=v, rect=rc, threads=threads)
     dt = time.perf_counter() - t0
     px = W * rows * features.num_samples_in_reservoir
     return {"value": round(px / dt / 1e6, 6), "unit": "Mpixel-reservoirs/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/restir_oracle.c frame (primary+RIS+spatial+final) on rows {y0}..{y0 + rows - 1} of the "
-                      f"{W}x{H} workload ({W * rows} px, {dt:.2f} s, OpenMP {threads} threads)"}
+            "sample": f"oracle/restir_oracle.c frame (primary+RIS+spatial+final) owning rows {y0}..{y0 + rows - 1} "
+                      f"of the {W}x{H} workload ({W * rows} px counted, +{2 * g} ghost rows computed, {dt:.2f} s, "
+                      f"OpenMP {threads} threads)"}
 
 
 def main():

@@ -137,7 +137,8 @@ struct Px {
     v3 P, N, V;
     float t;
     float4 kd_sh;   // kd.xyz, shininess
-    float4 ks_tr;   // ks.xyz, transparency
+    float4 ks_pm;   // ks.xyz, bits(pow mode)
+    float4 pw;      // (underflow threshold, bits(integer exponent), transparency, 0)
 };
 
 __device__ __forceinline__ Px load_px(const SceneDev& s, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
@@ -148,10 +149,36 @@ __device__ __forceinline__ Px load_px(const SceneDev& s, const float4* __restric
     r.P = xyz(b);
     uint32_t m = __float_as_uint(b.w);
     if (m >= s.num_materials) m = s.num_materials - 1;
-    r.kd_sh = s.materials[2 * m];
-    r.ks_tr = s.materials[2 * m + 1];
+    r.kd_sh = s.materials[3 * m];
+    r.ks_pm = s.materials[3 * m + 1];
+    r.pw = s.materials[3 * m + 2];
     r.V = vnormalize(vsub(origin, r.P));
     return r;
+}
+
+// std::pow(cosTheta, shininess) (shading.cpp:26) specialised per material; every branch returns exactly what
+// pm_powf(x, shininess) returns (or, for ks == 0, a value whose product with ks is the same +-0 the reference
+// gets after its NaN clean-up -- see DESIGN.md "Floating point").
+__device__ __forceinline__ float material_pow(float x, const Px& px) {
+    const uint32_t mode = __float_as_uint(px.ks_pm.w);
+    if (mode == ROMIS_POW_SKIP) return 1.0f;
+    if (mode == ROMIS_POW_INT) {
+        const uint32_t n = __float_as_uint(px.pw.y);
+        const float ax = fabsf(x);
+        if (ax < px.pw.x) return (__builtin_signbit(x) && (n & 1u)) ? -0.0f : 0.0f;   // |x|^n < 2^-151: underflow
+        if (ax <= 3.402823466e+38F) {
+            double base = (double)ax, acc = 1.0;
+            uint32_t k = n;
+            while (k) {
+                if (k & 1u) acc = acc * base;
+                k >>= 1;
+                if (k) base = base * base;
+            }
+            const double sign = (x < 0.0f && (n & 1u)) ? -1.0 : 1.0;
+            return (float)(sign * acc);
+        }
+    }
+    return pm_powf_general(x, px.kd_sh.w);
 }
 
 // computeShading (shading.cpp:7-34)
@@ -164,7 +191,7 @@ __device__ __forceinline__ v3 shade(const FeaturesDev& f, const Px& px, v3 lpos,
     v3 R = vnormalize(vsub(vscale(px.N, 2.0f * dotNL), L));
     float cosTheta = vdot(R, px.V);
     v3 diffuse = vscale(vmul(lcol, kd), dotNL);
-    v3 specular = vscale(vmul(lcol, xyz(px.ks_tr)), pm_powf(cosTheta, px.kd_sh.w));
+    v3 specular = vscale(vmul(lcol, xyz(px.ks_pm)), material_pow(cosTheta, px));
     if (vany_nan(diffuse)) diffuse = mk(0.0f, 0.0f, 0.0f);
     if (vany_nan(specular)) specular = mk(0.0f, 0.0f, 0.0f);
     float d = vdistance(px.P, lpos);
@@ -262,6 +289,26 @@ __device__ __forceinline__ size_t neighbour_index(const Region& rg, uint32_t x, 
     return (size_t)(ny - (int)rg.vy0) * rg.vw + (size_t)(nx - (int)rg.vx0);
 }
 
+// 2D launch: 32x8-pixel tiles, one 256-lane block each (a wave = 32x2 pixels).  Blocks are dealt
+// round-robin over the 8 XCDs (blocks b and b+8 share one -- MI355X_MICROARCH.md "Workgroup dispatch"), so
+// block b is remapped to give each XCD one contiguous run of tiles, i.e. a horizontal band of the image:
+// the rows a neighbourhood gathers then sit in that XCD's L2 instead of being fetched by all eight.
+constexpr uint32_t kTileW = 32, kTileH = 8;
+
+__device__ __forceinline__ bool tile_pixel(const Region& rg, uint32_t& x, uint32_t& y, size_t& p) {
+    const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
+    const uint32_t nb = gridDim.x;
+    const uint32_t b = blockIdx.x;
+    const uint32_t xcd = b % 8u, q = nb / 8u, rem = nb % 8u;
+    const uint32_t logical = xcd * q + min(xcd, rem) + b / 8u;
+    const uint32_t tx = logical % ntx, ty = logical / ntx;
+    x = rg.rx0 + tx * kTileW + threadIdx.x % kTileW;
+    y = rg.ry0 + ty * kTileH + threadIdx.x / kTileW;
+    if (x >= rg.rx0 + rg.rw || y >= rg.ry0 + rg.rh) return false;
+    p = (size_t)(y - rg.vy0) * rg.vw + (x - rg.vx0);
+    return true;
+}
+
 __device__ __forceinline__ bool region_pixel(const Region& rg, uint32_t idx, uint32_t& x, uint32_t& y, size_t& p) {
     if (idx >= rg.rw * rg.rh) return false;
     x = rg.rx0 + idx % rg.rw;
@@ -280,7 +327,7 @@ extern "C" __global__ __launch_bounds__(256) void k_primary(SceneDev s, Region r
                                                            float4* __restrict__ p_mat) {
     uint32_t x, y;
     size_t p;
-    if (!region_pixel(rg, blockIdx.x * blockDim.x + threadIdx.x, x, y, p)) return;
+    if (!tile_pixel(rg, x, y, p)) return;
     float nx = (float)x / (float)rg.W * 2.0f - 1.0f;
     float ny = (float)y / (float)rg.H * 2.0f - 1.0f;
     v3 csd = vnormalize(mk(-nx * cam.half_w, ny * cam.half_h, 1.0f));
@@ -342,7 +389,8 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
                 v3 l23 = vmix(xyz(lt[5]), xyz(lt[6]), a);
                 col = vmix(l01, l23, b);
             }
-            float w = target_pdf(f, px, pos, col) / invL;
+            const float pd = target_pdf(f, px, pos, col);
+            const float w = s.light_scale != 0.0f ? pd * s.light_scale : pd / invL;
             res_update<NT>(r, N, pos, col, w, rand01(draw(ps, 4u * c + 3u)));
         }
         for (uint32_t j = 0; j < N; j++) {
@@ -447,7 +495,7 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
                                              float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg) {
     uint32_t x, y;
     size_t p;
-    if (!region_pixel(rg, blockIdx.x * blockDim.x + threadIdx.x, x, y, p)) return;
+    if (!tile_pixel(rg, x, y, p)) return;
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
     const uint32_t K = f.K;
@@ -530,8 +578,7 @@ __device__ __forceinline__ void final_body(const SceneDev& s, const Region& rg, 
                                            float* __restrict__ rgb) {
     uint32_t x, y;
     size_t p;
-    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (!region_pixel(rg, idx, x, y, p)) return;
+    if (!tile_pixel(rg, x, y, p)) return;
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
     Px px = load_px(s, n_t, p_mat, p, origin);
@@ -586,12 +633,16 @@ namespace romis {
 namespace {
 constexpr uint32_t kBlock = 256;
 inline dim3 grid_for(const Region& rg) { return dim3((rg.rw * rg.rh + kBlock - 1) / kBlock); }
+inline dim3 grid_tiles(const Region& rg) {
+    return dim3(((rg.rw + kTileW - 1) / kTileW) * ((rg.rh + kTileH - 1) / kTileH));
+}
+static_assert(kTileW * kTileH == kBlock, "one lane per tile pixel");
 }  // namespace
 
 hipError_t launch_primary(const SceneDev& s, const Region& rg, const CameraDev& cam, float4* n_t, float4* p_mat,
                           hipStream_t stream) {
     if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_primary, grid_for(rg), dim3(kBlock), 0, stream, s, rg, cam, n_t, p_mat);
+    hipLaunchKernelGGL(k_primary, grid_tiles(rg), dim3(kBlock), 0, stream, s, rg, cam, n_t, p_mat);
     return hipGetLastError();
 }
 
@@ -621,7 +672,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg, const FeaturesDev
     if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
     auto k = f.unbiased ? (f.N == 1 ? k_spatial_n1_unbiased : (f.N == 2 ? k_spatial_n2_unbiased : k_spatial_n0_unbiased))
                         : (f.N == 1 ? k_spatial_n1_biased : (f.N == 2 ? k_spatial_n2_biased : k_spatial_n0_biased));
-    hipLaunchKernelGGL(k, grid_for(rg), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib,
+    hipLaunchKernelGGL(k, grid_tiles(rg), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib,
                        oa, ob, odbg);
     return hipGetLastError();
 }
@@ -630,7 +681,7 @@ hipError_t launch_final(const SceneDev& s, const Region& rg, const FeaturesDev& 
                         const float4* p_mat, const float4* ra, const float4* rb, float* rgb, hipStream_t stream) {
     if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
     auto k = f.N == 1 ? k_final_n1 : (f.N == 2 ? k_final_n2 : k_final_n0);
-    hipLaunchKernelGGL(k, grid_for(rg), dim3(kBlock), 0, stream, s, rg, f, o[0], o[1], o[2], n_t, p_mat, ra, rb, rgb);
+    hipLaunchKernelGGL(k, grid_tiles(rg), dim3(kBlock), 0, stream, s, rg, f, o[0], o[1], o[2], n_t, p_mat, ra, rb, rgb);
     return hipGetLastError();
 }
 

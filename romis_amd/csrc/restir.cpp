@@ -444,14 +444,33 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
         v0[4 * k + 3] = u2f(bvh.tri_order[k]);
     }
     // materials: one per mesh + the miss material (value-initialised HitInfo: kd 0, ks 0, shininess 1)
-    std::vector<float> mats(8 * (num_meshes + 1), 0.0f);
-    for (uint32_t m = 0; m < num_meshes; m++) {
-        const restir_material& mt = meshes[m].material;
-        mats[8 * m + 0] = mt.kd[0]; mats[8 * m + 1] = mt.kd[1]; mats[8 * m + 2] = mt.kd[2]; mats[8 * m + 3] = mt.shininess;
-        mats[8 * m + 4] = mt.ks[0]; mats[8 * m + 5] = mt.ks[1]; mats[8 * m + 6] = mt.ks[2]; mats[8 * m + 7] = mt.transparency;
+    // 3 float4 per material: (kd, shininess), (ks, pow mode), (underflow threshold, exponent, transparency, 0)
+    std::vector<float> mats(12 * (num_meshes + 1), 0.0f);
+    auto put_material = [&](uint32_t m, const restir_material& mt) {
+        float* o = &mats[12 * m];
+        o[0] = mt.kd[0]; o[1] = mt.kd[1]; o[2] = mt.kd[2]; o[3] = mt.shininess;
+        o[4] = mt.ks[0]; o[5] = mt.ks[1]; o[6] = mt.ks[2];
+        uint32_t mode = ROMIS_POW_GENERAL, n = 0;
+        float thr = 0.0f;
+        const float y = mt.shininess;
+        if (mt.ks[0] == 0.0f && mt.ks[1] == 0.0f && mt.ks[2] == 0.0f) {
+            mode = ROMIS_POW_SKIP;
+        } else if (y == std::trunc(y) && y >= 1.0f && y <= 1048576.0f) {
+            mode = ROMIS_POW_INT;
+            n = (uint32_t)y;
+            // |x| < thr  =>  |x|^n <= 2^-152, which the double powering rounds to a float +-0
+            thr = std::nextafter((float)std::exp2(-152.0 / (double)n), 0.0f);
+        }
+        o[7] = u2f(mode);
+        o[8] = thr; o[9] = u2f(n); o[10] = mt.transparency; o[11] = 0.0f;
+    };
+    for (uint32_t m = 0; m < num_meshes; m++) put_material(m, meshes[m].material);
+    {
+        restir_material miss{};   // value-initialised HitInfo material: kd 0, ks 0, shininess 1, transparency 1
+        miss.shininess = 1.0f;
+        miss.transparency = 1.0f;
+        put_material(num_meshes, miss);
     }
-    mats[8 * num_meshes + 3] = 1.0f;
-    mats[8 * num_meshes + 7] = 1.0f;
     // lights: 7 float4 records
     std::vector<float> lt(28 * std::max<uint32_t>(num_lights, 1), 0.0f);
     uint32_t types = 0;
@@ -495,6 +514,8 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
     s.lights = c->lights.as<float4>();
     s.num_lights = num_lights;
     s.light_types = types;
+    // w = p / (1/L) (light.cpp:80) equals p * L exactly when 1/L is a power of two
+    s.light_scale = (num_lights && (num_lights & (num_lights - 1)) == 0) ? (float)num_lights : 0.0f;
     c->has_scene = true;
     return RESTIR_OK;
 }

@@ -7,6 +7,11 @@
 
 #define RESTIR_MAX_N_DEV 32u
 
+// material pow modes (std::pow(cosTheta, shininess), shading.cpp:26)
+#define ROMIS_POW_SKIP 0u      // ks == 0: the specular term is +-0 whatever pow returns
+#define ROMIS_POW_INT 1u       // shininess is an integer in [1, 2^20]: binary powering in double
+#define ROMIS_POW_GENERAL 2u   // anything else: pm_powf_general
+
 namespace romis {
 
 // Scene as the kernels see it.  All arrays are device pointers, 16-byte aligned float4 records.
@@ -27,14 +32,15 @@ struct SceneDev {
     const float4* tri_n1;
     const float4* tri_n2;
     uint32_t num_tris;
-    // Materials: 2 float4 each: (kd.xyz, shininess), (ks.xyz, transparency).  Last entry = miss material.
+    // Materials: 3 float4 each: (kd.xyz, shininess), (ks.xyz, bits(pow mode)),
+    // (pow underflow threshold, bits(integer exponent), transparency, 0).  Last entry = miss material.
     const float4* materials;
     uint32_t num_materials;
     // Lights: 7 float4 each: (p0.xyz, bits(type)), (p1.xyz, 0), (p2.xyz, 0), c0, c1, c2, c3
     const float4* lights;
     uint32_t num_lights;
     uint32_t light_types;      // bit t set <=> a light of type t is present
-    float box_pad;             // unused on device (bounds are padded on the host)
+    float light_scale;         // L when 1/L is a power of two (then p / (1/L) == p * L exactly), else 0
 };
 
 // Image region bookkeeping: global image W x H (y = 0 bottom), storage view (the computed region, row-major)

@@ -10,8 +10,9 @@
 //
 // One lane per pixel throughout: the reservoir update (Reservoir::update, reservoir.cpp:10-32) is a serial
 // prefix over the candidate stream whose float rounding must match the reference order exactly, so it stays
-// a per-lane loop; the wave's 64 lanes work on 64 pixels.  Reservoirs and the G-buffer are SoA float4 planes
-// read with 16-byte coalesced loads.  Visibility uses a stackless threaded BVH (no scratch stack).
+// a per-lane loop; a wave's 64 lanes work on 64 pixels.  Reservoirs and the G-buffer are SoA float4 planes
+// read with 16-byte coalesced loads.  Visibility uses a stackless threaded BVH (no scratch stack) that the
+// ray kernels stage once per (persistent) workgroup into LDS; the light table is staged into LDS for RIS.
 #include "device_math.h"
 #include "restir_types.h"
 
@@ -62,21 +63,50 @@ __device__ __forceinline__ v3 safe_inv(v3 d) {
 
 __device__ __forceinline__ float widen(float t) { return t * 1.0001f + 1e-4f; }
 
+// The traversal arrays, either the global copies or the workgroup's LDS copy.
+struct Bvh {
+    const float4* nodes;
+    const float4* v0;
+    const float4* e1;
+    const float4* e2;
+    uint32_t num_nodes;
+};
+
+__device__ __forceinline__ Bvh global_bvh(const SceneDev& s) {
+    Bvh b;
+    b.nodes = s.nodes; b.v0 = s.tri_v0; b.e1 = s.tri_e1; b.e2 = s.tri_e2; b.num_nodes = s.num_nodes;
+    return b;
+}
+
+// Copy nodes + triangles into LDS (every thread of the block participates; ends with a barrier).
+__device__ __forceinline__ Bvh stage_bvh(const SceneDev& s, float4* lds) {
+    const uint32_t nn = 2u * s.num_nodes, nt = s.num_tris;
+    for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = s.nodes[i];
+    for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) {
+        lds[nn + i] = s.tri_v0[i];
+        lds[nn + nt + i] = s.tri_e1[i];
+        lds[nn + 2 * nt + i] = s.tri_e2[i];
+    }
+    __syncthreads();
+    Bvh b;
+    b.nodes = lds; b.v0 = lds + nn; b.e1 = lds + nn + nt; b.e2 = lds + nn + 2 * nt; b.num_nodes = s.num_nodes;
+    return b;
+}
+
 // any hit in (0, tfar] -- EmbreeInterface::anyHit (embree_interface.cpp:58-62)
-__device__ bool occluded(const SceneDev& s, v3 o, v3 d, float tfar) {
+__device__ __forceinline__ bool occluded(const Bvh& b, v3 o, v3 d, float tfar) {
     v3 invd = safe_inv(d);
     float tb = widen(tfar);
     uint32_t i = 0;
-    while (i < s.num_nodes) {
-        float4 lo = s.nodes[2 * i], hi = s.nodes[2 * i + 1];
+    while (i < b.num_nodes) {
+        float4 lo = b.nodes[2 * i], hi = b.nodes[2 * i + 1];
         uint32_t miss = __float_as_uint(lo.w), leaf = __float_as_uint(hi.w);
         if (box_hit(lo, hi, o, invd, tb)) {
             if (leaf) {
                 uint32_t first = leaf & 0xFFFFFFu, cnt = leaf >> 24;
                 for (uint32_t k = 0; k < cnt; k++) {
                     float t, u, v;
-                    if (tri_hit(s.tri_v0[first + k], s.tri_e1[first + k], s.tri_e2[first + k], o, d, tfar, t, u, v))
-                        return true;
+                    if (tri_hit(b.v0[first + k], b.e1[first + k], b.e2[first + k], o, d, tfar, t, u, v)) return true;
                 }
                 i = miss;
             } else {
@@ -90,22 +120,23 @@ __device__ bool occluded(const SceneDev& s, v3 o, v3 d, float tfar) {
 }
 
 // closest hit: minimal t, lowest original triangle index on ties
-__device__ bool closest(const SceneDev& s, v3 o, v3 d, float& t_best, float& u_best, float& v_best, uint32_t& tri_best) {
+__device__ __forceinline__ bool closest(const Bvh& b, v3 o, v3 d, float& t_best, float& u_best, float& v_best,
+                                        uint32_t& tri_best) {
     v3 invd = safe_inv(d);
     bool found = false;
     t_best = ROMIS_FLT_MAX;
     tri_best = 0xFFFFFFFFu;
     uint32_t i = 0;
-    while (i < s.num_nodes) {
-        float4 lo = s.nodes[2 * i], hi = s.nodes[2 * i + 1];
+    while (i < b.num_nodes) {
+        float4 lo = b.nodes[2 * i], hi = b.nodes[2 * i + 1];
         uint32_t miss = __float_as_uint(lo.w), leaf = __float_as_uint(hi.w);
         if (box_hit(lo, hi, o, invd, widen(t_best))) {
             if (leaf) {
                 uint32_t first = leaf & 0xFFFFFFu, cnt = leaf >> 24;
                 for (uint32_t k = 0; k < cnt; k++) {
-                    float4 v0 = s.tri_v0[first + k];
+                    float4 v0 = b.v0[first + k];
                     float t, u, v;
-                    if (tri_hit(v0, s.tri_e1[first + k], s.tri_e2[first + k], o, d, ROMIS_FLT_MAX, t, u, v)) {
+                    if (tri_hit(v0, b.e1[first + k], b.e2[first + k], o, d, ROMIS_FLT_MAX, t, u, v)) {
                         uint32_t orig = __float_as_uint(v0.w);
                         if (!found || t < t_best || (t == t_best && orig < tri_best)) {
                             found = true; t_best = t; u_best = u; v_best = v; tri_best = orig;
@@ -124,11 +155,11 @@ __device__ bool closest(const SceneDev& s, v3 o, v3 d, float& t_best, float& u_b
 }
 
 // testVisibilityLightSample (utils.cpp:41-56)
-__device__ __forceinline__ bool visible(const SceneDev& s, v3 P, v3 y) {
+__device__ __forceinline__ bool visible(const Bvh& b, v3 P, v3 y) {
     v3 dir = vnormalize(vsub(y, P));
     v3 P2 = vadd(P, vscale(dir, 1e-3f));
     float tfar = vdistance(P2, y);
-    return !occluded(s, P2, dir, tfar);
+    return !occluded(b, P2, dir, tfar);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -141,10 +172,8 @@ struct Px {
     float4 pw;      // (underflow threshold, bits(integer exponent), transparency, 0)
 };
 
-__device__ __forceinline__ Px load_px(const SceneDev& s, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
-                                      size_t p, v3 origin) {
+__device__ __forceinline__ Px make_px(const SceneDev& s, float4 a, float4 b, v3 origin) {
     Px r;
-    float4 a = n_t[p], b = p_mat[p];
     r.N = xyz(a); r.t = a.w;
     r.P = xyz(b);
     uint32_t m = __float_as_uint(b.w);
@@ -154,6 +183,11 @@ __device__ __forceinline__ Px load_px(const SceneDev& s, const float4* __restric
     r.pw = s.materials[3 * m + 2];
     r.V = vnormalize(vsub(origin, r.P));
     return r;
+}
+
+__device__ __forceinline__ Px load_px(const SceneDev& s, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                      size_t p, v3 origin) {
+    return make_px(s, n_t[p], p_mat[p], origin);
 }
 
 // std::pow(cosTheta, shininess) (shading.cpp:26) specialised per material; every branch returns exactly what
@@ -265,11 +299,16 @@ __device__ __forceinline__ float contribution_weight(float p, uint32_t M, float 
     return ((1.0f / p) * (1.0f / (float)M)) * wsum;
 }
 
-__device__ __forceinline__ void sub_load(Sub& r, const float4* __restrict__ a, const float4* __restrict__ b, size_t i) {
-    float4 fa = a[i], fb = b[i];
+__device__ __forceinline__ Sub sub_from(float4 fa, float4 fb) {
+    Sub r;
     r.pos = xyz(fa); r.W = fa.w;
     r.col = xyz(fb); r.M = __float_as_uint(fb.w);
     r.wsum = 0.0f; r.chosen = 0.0f;
+    return r;
+}
+
+__device__ __forceinline__ void sub_load(Sub& r, const float4* __restrict__ a, const float4* __restrict__ b, size_t i) {
+    r = sub_from(a[i], b[i]);
 }
 
 __device__ __forceinline__ void sub_store(const Sub& r, float4* __restrict__ a, float4* __restrict__ b,
@@ -289,24 +328,32 @@ __device__ __forceinline__ size_t neighbour_index(const Region& rg, uint32_t x, 
     return (size_t)(ny - (int)rg.vy0) * rg.vw + (size_t)(nx - (int)rg.vx0);
 }
 
-// 2D launch: 32x8-pixel tiles, one 256-lane block each (a wave = 32x2 pixels).  Blocks are dealt
-// round-robin over the 8 XCDs (blocks b and b+8 share one -- MI355X_MICROARCH.md "Workgroup dispatch"), so
-// block b is remapped to give each XCD one contiguous run of tiles, i.e. a horizontal band of the image:
-// the rows a neighbourhood gathers then sit in that XCD's L2 instead of being fetched by all eight.
+// ---------------------------------------------------------------------------------------------------------
+// Work mapping.  Tiles of 32x8 pixels, one 256-lane block each (a wave = 32x2 pixels).
 constexpr uint32_t kTileW = 32, kTileH = 8;
 
-__device__ __forceinline__ bool tile_pixel(const Region& rg, uint32_t& x, uint32_t& y, size_t& p) {
+__device__ __forceinline__ uint32_t num_tiles(const Region& rg) {
+    return ((rg.rw + kTileW - 1) / kTileW) * ((rg.rh + kTileH - 1) / kTileH);
+}
+
+__device__ __forceinline__ bool tile_pixel_of(const Region& rg, uint32_t tile, uint32_t& x, uint32_t& y, size_t& p) {
     const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
-    const uint32_t nb = gridDim.x;
-    const uint32_t b = blockIdx.x;
-    const uint32_t xcd = b % 8u, q = nb / 8u, rem = nb % 8u;
-    const uint32_t logical = xcd * q + min(xcd, rem) + b / 8u;
-    const uint32_t tx = logical % ntx, ty = logical / ntx;
+    const uint32_t tx = tile % ntx, ty = tile / ntx;
     x = rg.rx0 + tx * kTileW + threadIdx.x % kTileW;
     y = rg.ry0 + ty * kTileH + threadIdx.x / kTileW;
     if (x >= rg.rx0 + rg.rw || y >= rg.ry0 + rg.rh) return false;
     p = (size_t)(y - rg.vy0) * rg.vw + (x - rg.vx0);
     return true;
+}
+
+// Spatial pass: blocks are dealt round-robin over the 8 XCDs (blocks b and b+8 share one --
+// MI355X_MICROARCH.md "Workgroup dispatch"), so block b is remapped to give each XCD one contiguous run of
+// tiles, i.e. a horizontal band of the image: the rows a neighbourhood gathers then sit in that XCD's L2
+// instead of being fetched by all eight (FETCH_SIZE 0.95 GB -> 0.15 GB per 1080p pass, profiles/).
+__device__ __forceinline__ uint32_t xcd_banded_tile() {
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    const uint32_t xcd = b % 8u, q = nb / 8u, rem = nb % 8u;
+    return xcd * q + min(xcd, rem) + b / 8u;
 }
 
 __device__ __forceinline__ bool region_pixel(const Region& rg, uint32_t idx, uint32_t& x, uint32_t& y, size_t& p) {
@@ -321,96 +368,125 @@ __device__ __forceinline__ bool region_pixel(const Region& rg, uint32_t idx, uin
 
 using namespace romis;
 
+extern __shared__ __attribute__((aligned(16))) float4 g_lds[];
+
 // ---------------------------------------------------------------------------------------------------------
-// k_primary: one lane per pixel of rg's rect; writes n_t / p_mat.
-extern "C" __global__ __launch_bounds__(256) void k_primary(SceneDev s, Region rg, CameraDev cam, float4* __restrict__ n_t,
-                                                           float4* __restrict__ p_mat) {
-    uint32_t x, y;
-    size_t p;
-    if (!tile_pixel(rg, x, y, p)) return;
-    float nx = (float)x / (float)rg.W * 2.0f - 1.0f;
-    float ny = (float)y / (float)rg.H * 2.0f - 1.0f;
-    v3 csd = vnormalize(mk(-nx * cam.half_w, ny * cam.half_h, 1.0f));
-    v3 d = qrotate(cam.quat, csd);
-    v3 o = mk(cam.origin[0], cam.origin[1], cam.origin[2]);
-    float t, u = 0.0f, v = 0.0f;
-    uint32_t tri;
-    v3 n = mk(0.0f, 0.0f, 0.0f);
-    uint32_t m = s.num_materials - 1;
-    if (closest(s, o, d, t, u, v, tri)) {
-        float w0 = (1.0f - u) - v;
-        float4 a = s.tri_n0[tri], b = s.tri_n1[tri], c = s.tri_n2[tri];
-        n = vadd(vadd(vscale(xyz(a), w0), vscale(xyz(b), u)), vscale(xyz(c), v));
-        m = __float_as_uint(a.w);
-    } else {
-        t = ROMIS_FLT_MAX;
+// k_primary: persistent blocks stage the BVH into LDS once, then sweep 32x8 tiles; writes n_t / p_mat.
+template <bool LDS_BVH>
+__device__ __forceinline__ void primary_body(const SceneDev& s, const Region& rg, const CameraDev& cam,
+                                             float4* __restrict__ n_t, float4* __restrict__ p_mat) {
+    const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
+    const uint32_t nt = num_tiles(rg);
+    const v3 o = mk(cam.origin[0], cam.origin[1], cam.origin[2]);
+    for (uint32_t tile = blockIdx.x; tile < nt; tile += gridDim.x) {
+        uint32_t x, y;
+        size_t p;
+        if (!tile_pixel_of(rg, tile, x, y, p)) continue;
+        float nx = (float)x / (float)rg.W * 2.0f - 1.0f;
+        float ny = (float)y / (float)rg.H * 2.0f - 1.0f;
+        v3 csd = vnormalize(mk(-nx * cam.half_w, ny * cam.half_h, 1.0f));
+        v3 d = qrotate(cam.quat, csd);
+        float t, u = 0.0f, v = 0.0f;
+        uint32_t tri;
+        v3 n = mk(0.0f, 0.0f, 0.0f);
+        uint32_t m = s.num_materials - 1;
+        if (closest(bvh, o, d, t, u, v, tri)) {
+            float w0 = (1.0f - u) - v;
+            float4 a = s.tri_n0[tri], b = s.tri_n1[tri], c = s.tri_n2[tri];
+            n = vadd(vadd(vscale(xyz(a), w0), vscale(xyz(b), u)), vscale(xyz(c), v));
+            m = __float_as_uint(a.w);
+        } else {
+            t = ROMIS_FLT_MAX;
+        }
+        v3 P = vadd(o, vscale(d, t));
+        n_t[p] = make_float4(n.x, n.y, n.z, t);
+        p_mat[p] = make_float4(P.x, P.y, P.z, __uint_as_float(m));
     }
-    v3 P = vadd(o, vscale(d, t));
-    n_t[p] = make_float4(n.x, n.y, n.z, t);
-    p_mat[p] = make_float4(P.x, P.y, P.z, __uint_as_float(m));
+}
+
+extern "C" __global__ __launch_bounds__(256) void k_primary(SceneDev s, Region rg, CameraDev cam, float4* n_t, float4* p_mat) {
+    primary_body<false>(s, rg, cam, n_t, p_mat);
+}
+extern "C" __global__ __launch_bounds__(256) void k_primary_lds(SceneDev s, Region rg, CameraDev cam, float4* n_t,
+                                                               float4* p_mat) {
+    primary_body<true>(s, rg, cam, n_t, p_mat);
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// k_ris: genCanonicalSamples per pixel.  Lane-serial candidate loop (M iterations) -- VALU bound.
-template <int NT>
+// k_ris: genCanonicalSamples per pixel.  Lane-serial candidate loop (M iterations) -- VALU bound.  The light
+// table is staged into LDS once per persistent block when it fits (LDS_LIGHTS), so the per-candidate random
+// light fetch is an LDS read instead of a dependent global load.
+template <int NT, bool LDS_LIGHTS>
 __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                          const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                          float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg) {
-    uint32_t x, y;
-    size_t p;
-    if (!region_pixel(rg, blockIdx.x * blockDim.x + threadIdx.x, x, y, p)) return;
+    const uint32_t L = s.num_lights;
+    const float4* lights = s.lights;
+    if (LDS_LIGHTS) {
+        for (uint32_t i = threadIdx.x; i < 7u * L; i += blockDim.x) g_lds[i] = s.lights[i];
+        __syncthreads();
+        lights = g_lds;
+    }
+    const Bvh bvh = global_bvh(s);
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
-    Sub r[NT > 0 ? NT : RESTIR_MAX_N_DEV];
-    for (uint32_t j = 0; j < N; j++) sub_init(r[j]);
-    const uint32_t L = s.num_lights;
-    if (L != 0) {
-        Px px = load_px(s, n_t, p_mat, p, origin);
-        const uint32_t ps = pix_state(key, y * rg.W + x);
-        for (uint32_t j = 0; j < N; j++) r[j].M = 0u;
-        const float invL = 1.0f / (float)L;
-        for (uint32_t c = 0; c < f.M; c++) {
-            const float4* lt = s.lights + 7u * uniform_index(draw(ps, 4u * c), L);
-            float4 l0 = lt[0];
-            uint32_t type = __float_as_uint(l0.w);
-            v3 pos, col;
-            if (type == 0u) {
-                pos = xyz(l0);
-                col = xyz(lt[3]);
-            } else if (type == 1u) {
-                float fr = rand01(draw(ps, 4u * c + 1u));
-                pos = vmix(xyz(l0), xyz(lt[1]), fr);
-                col = vmix(xyz(lt[3]), xyz(lt[4]), fr);
-            } else {
-                float a = rand01(draw(ps, 4u * c + 1u));
-                float b = rand01(draw(ps, 4u * c + 2u));
-                pos = vadd(vadd(xyz(l0), vscale(xyz(lt[1]), a)), vscale(xyz(lt[2]), b));
-                v3 l01 = vmix(xyz(lt[3]), xyz(lt[4]), a);
-                v3 l23 = vmix(xyz(lt[5]), xyz(lt[6]), a);
-                col = vmix(l01, l23, b);
+    const uint32_t total = rg.rw * rg.rh;
+    const float invL = 1.0f / (float)L;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
+        uint32_t x, y;
+        size_t p;
+        if (!region_pixel(rg, base + threadIdx.x, x, y, p)) continue;
+        Sub r[NT > 0 ? NT : RESTIR_MAX_N_DEV];
+        for (uint32_t j = 0; j < N; j++) sub_init(r[j]);
+        if (L != 0) {
+            Px px = load_px(s, n_t, p_mat, p, origin);
+            const uint32_t ps = pix_state(key, y * rg.W + x);
+            for (uint32_t j = 0; j < N; j++) r[j].M = 0u;
+            for (uint32_t c = 0; c < f.M; c++) {
+                const float4* lt = lights + 7u * uniform_index(draw(ps, 4u * c), L);
+                float4 l0 = lt[0];
+                uint32_t type = __float_as_uint(l0.w);
+                v3 pos, col;
+                if (type == 0u) {
+                    pos = xyz(l0);
+                    col = xyz(lt[3]);
+                } else if (type == 1u) {
+                    float fr = rand01(draw(ps, 4u * c + 1u));
+                    pos = vmix(xyz(l0), xyz(lt[1]), fr);
+                    col = vmix(xyz(lt[3]), xyz(lt[4]), fr);
+                } else {
+                    float a = rand01(draw(ps, 4u * c + 1u));
+                    float b = rand01(draw(ps, 4u * c + 2u));
+                    pos = vadd(vadd(xyz(l0), vscale(xyz(lt[1]), a)), vscale(xyz(lt[2]), b));
+                    v3 l01 = vmix(xyz(lt[3]), xyz(lt[4]), a);
+                    v3 l23 = vmix(xyz(lt[5]), xyz(lt[6]), a);
+                    col = vmix(l01, l23, b);
+                }
+                const float pd = target_pdf(f, px, pos, col);
+                const float w = s.light_scale != 0.0f ? pd * s.light_scale : pd / invL;   // light.cpp:80
+                res_update<NT>(r, N, pos, col, w, rand01(draw(ps, 4u * c + 3u)));
             }
-            const float pd = target_pdf(f, px, pos, col);
-            const float w = s.light_scale != 0.0f ? pd * s.light_scale : pd / invL;
-            res_update<NT>(r, N, pos, col, w, rand01(draw(ps, 4u * c + 3u)));
+            for (uint32_t j = 0; j < N; j++) {
+                if (f.initial_vis && !visible(bvh, px.P, r[j].pos)) r[j].W = 0.0f;
+                else r[j].W = contribution_weight(target_pdf(f, px, r[j].pos, r[j].col), r[j].M, r[j].wsum);
+            }
         }
-        for (uint32_t j = 0; j < N; j++) {
-            if (f.initial_vis && !visible(s, px.P, r[j].pos)) r[j].W = 0.0f;
-            else r[j].W = contribution_weight(target_pdf(f, px, r[j].pos, r[j].col), r[j].M, r[j].wsum);
-        }
+        for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, j * npx + p);
     }
-    for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, j * npx + p);
 }
 
-#define ROMIS_RIS_KERNEL(NT)                                                                                          \
-    extern "C" __global__ __launch_bounds__(256) void k_ris_n##NT(SceneDev s, Region rg, FeaturesDev f, uint32_t key,  \
-                                                                 float ox, float oy, float oz, const float4* n_t,     \
-                                                                 const float4* p_mat, float4* ra, float4* rb,         \
-                                                                 float2* rdbg) {                                      \
-        ris_body<NT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg);                                        \
+#define ROMIS_RIS_KERNEL(NT, LDS, NAME)                                                                               \
+    extern "C" __global__ __launch_bounds__(256) void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
+                                                          float oy, float oz, const float4* n_t, const float4* p_mat,   \
+                                                          float4* ra, float4* rb, float2* rdbg) {                       \
+        ris_body<NT, LDS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg);                                     \
     }
-ROMIS_RIS_KERNEL(1)
-ROMIS_RIS_KERNEL(2)
-ROMIS_RIS_KERNEL(0)
+ROMIS_RIS_KERNEL(1, false, k_ris_n1)
+ROMIS_RIS_KERNEL(2, false, k_ris_n2)
+ROMIS_RIS_KERNEL(0, false, k_ris_n0)
+ROMIS_RIS_KERNEL(1, true, k_ris_n1_lds)
+ROMIS_RIS_KERNEL(2, true, k_ris_n2_lds)
+ROMIS_RIS_KERNEL(0, true, k_ris_n0_lds)
 
 // ---------------------------------------------------------------------------------------------------------
 // Combine state shared by temporal and spatial: out[] (Reservoir(N) of the current pixel) + routed M sums.
@@ -418,24 +494,26 @@ template <int NT>
 struct Combiner {
     Sub out[NT > 0 ? NT : RESTIR_MAX_N_DEV];
     uint32_t macc[NT > 0 ? NT : RESTIR_MAX_N_DEV];
-    uint32_t N;
+    uint32_t N_;
     uint32_t t;      // update counter (RNG slot offset)
-    __device__ __forceinline__ void init(uint32_t n) {
-        N = NT > 0 ? (uint32_t)NT : n;
-        for (uint32_t j = 0; j < N; j++) { sub_init(out[j]); macc[j] = 0u; }
+    // compile-time trip count when N is a template constant (keeps out[] / macc[] in registers)
+    __device__ __forceinline__ uint32_t n() const { return NT > 0 ? (uint32_t)NT : N_; }
+    __device__ __forceinline__ void init(uint32_t nn) {
+        N_ = nn;
+        for (uint32_t j = 0; j < n(); j++) { sub_init(out[j]); macc[j] = 0u; }
         t = 0;
     }
     // combine one input sub-reservoir (reservoir.cpp:47-54 / :75-82)
     __device__ __forceinline__ void consume(const FeaturesDev& f, const Px& cur, const Sub& in, uint32_t ps, uint32_t slot0) {
         float pd = target_pdf(f, cur, in.pos, in.col);
         float w = (pd * in.W) * (float)in.M;
-        uint32_t k = res_update<NT>(out, N, in.pos, in.col, w, rand01(draw(ps, slot0 + t)));
+        uint32_t k = res_update<NT>(out, n(), in.pos, in.col, w, rand01(draw(ps, slot0 + t)));
         t++;
         macc_add<NT>(macc, k, in.M);
     }
     __device__ __forceinline__ void finish_biased(const FeaturesDev& f, const Px& cur) {
-        for (uint32_t j = 0; j < N; j++) out[j].M = macc[j];
-        for (uint32_t j = 0; j < N; j++)
+        for (uint32_t j = 0; j < n(); j++) out[j].M = macc[j];
+        for (uint32_t j = 0; j < n(); j++)
             out[j].W = contribution_weight(target_pdf(f, cur, out[j].pos, out[j].col), out[j].M, out[j].wsum);
     }
 };
@@ -487,7 +565,11 @@ ROMIS_TEMPORAL_KERNEL(0)
 
 // ---------------------------------------------------------------------------------------------------------
 // k_spatial: one spatialReuse pass.  Neighbours stream straight into the combine (accepted neighbours in draw
-// order, current last -- render_utils.cpp:108-124), so no per-lane candidate list is kept.
+// order, current last -- render_utils.cpp:108-124), so no per-lane candidate list is kept.  The neighbour
+// draws do not depend on data, so the loads of a batch of kBatch neighbours are all issued before the first
+// is consumed (one memory latency per batch instead of a dependent chain per neighbour).
+constexpr uint32_t kBatch = 5;
+
 template <int NT, bool UNBIASED>
 __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
                                              v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
@@ -495,7 +577,7 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
                                              float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg) {
     uint32_t x, y;
     size_t p;
-    if (!tile_pixel(rg, x, y, p)) return;
+    if (!tile_pixel_of(rg, xcd_banded_tile(), x, y, p)) return;
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
     const uint32_t K = f.K;
@@ -504,20 +586,55 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
     const uint32_t slot0 = 2u * K;
     Combiner<NT> cmb;
     cmb.init(N);
-    for (uint32_t n = 0; n < K; n++) {
-        const int dx = uniform_offset(draw(ps, 2u * n), f.R);
-        const int dy = uniform_offset(draw(ps, 2u * n + 1u), f.R);
-        const size_t q = neighbour_index(rg, x, y, dx, dy);
-        if (!UNBIASED) {
-            float4 g = n_t[q];
-            float depthFracDiff = fabsf(1.0f - (g.w / cur.t));
-            float normalsDotProd = vdot(xyz(g), cur.N);
-            if (depthFracDiff > 0.1f || normalsDotProd < 0.90630778703f) continue;
+    for (uint32_t n0 = 0; n0 < K; n0 += kBatch) {
+        uint32_t q[kBatch];
+        float4 g[kBatch];
+        bool ok[kBatch];
+#pragma unroll
+        for (uint32_t i = 0; i < kBatch; i++) {
+            const uint32_t n = n0 + i;
+            q[i] = (uint32_t)p;
+            if (n < K)
+                q[i] = (uint32_t)neighbour_index(rg, x, y, uniform_offset(draw(ps, 2u * n), f.R),
+                                       uniform_offset(draw(ps, 2u * n + 1u), f.R));
         }
-        for (uint32_t j = 0; j < N; j++) {
-            Sub in;
-            sub_load(in, ia, ib, j * npx + q);
-            cmb.consume(f, cur, in, ps, slot0);
+        if constexpr (!UNBIASED) {
+#pragma unroll
+            for (uint32_t i = 0; i < kBatch; i++) g[i] = n_t[q[i]];
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kBatch; i++) {
+            ok[i] = n0 + i < K;
+            if (!UNBIASED && ok[i]) {   // render_utils.cpp:114-118
+                float depthFracDiff = fabsf(1.0f - (g[i].w / cur.t));
+                float normalsDotProd = vdot(xyz(g[i]), cur.N);
+                if (depthFracDiff > 0.1f || normalsDotProd < 0.90630778703f) ok[i] = false;
+            }
+        }
+        if constexpr (NT == 1) {
+            float4 a[kBatch], b[kBatch];
+#pragma unroll
+            for (uint32_t i = 0; i < kBatch; i++) {
+                if (ok[i]) { a[i] = ia[q[i]]; b[i] = ib[q[i]]; }
+            }
+            // consume in draw order with ONE inlined combine body: the batch is shifted down a register per
+            // step (static indices only; a rolled loop over a[i] would spill the batch to memory)
+#pragma unroll 1
+            for (uint32_t i = 0; i < kBatch; i++) {
+                if (ok[0]) cmb.consume(f, cur, sub_from(a[0], b[0]), ps, slot0);
+#pragma unroll
+                for (uint32_t j = 0; j + 1 < kBatch; j++) { a[j] = a[j + 1]; b[j] = b[j + 1]; ok[j] = ok[j + 1]; }
+            }
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < kBatch; i++) {
+                if (!ok[i]) continue;
+                for (uint32_t j = 0; j < N; j++) {
+                    Sub in;
+                    sub_load(in, ia, ib, j * npx + q[i]);
+                    cmb.consume(f, cur, in, ps, slot0);
+                }
+            }
         }
     }
     for (uint32_t j = 0; j < N; j++) {
@@ -530,6 +647,7 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
     } else {
         // combineUnbiased (reservoir.cpp:84-103): Z_j = sum over the stream of the input's total M where
         // p_r(y_j) [* vis_r(y_j)] > 0.  The stream is re-derived from the same draws (no rejection here).
+        const Bvh bvh = global_bvh(s);
         for (uint32_t j = 0; j < N; j++) cmb.out[j].M = cmb.macc[j];
         unsigned long long Z[NT > 0 ? NT : RESTIR_MAX_N_DEV];
         for (uint32_t j = 0; j < N; j++) Z[j] = 0ull;
@@ -542,7 +660,7 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
             for (uint32_t j = 0; j < N; j++) tot += __float_as_uint(ib[j * npx + q].w);
             for (uint32_t j = 0; j < N; j++) {
                 float pd = target_pdf(f, rp, cmb.out[j].pos, cmb.out[j].col);
-                if (f.spatial_vis) pd *= visible(s, rp.P, cmb.out[j].pos) ? 1.0f : 0.0f;
+                if (f.spatial_vis) pd *= visible(bvh, rp.P, cmb.out[j].pos) ? 1.0f : 0.0f;
                 if (pd > 0.0f) Z[j] += tot;
             }
         }
@@ -571,50 +689,58 @@ ROMIS_SPATIAL_KERNEL(0, true, k_spatial_n0_unbiased)
 
 // ---------------------------------------------------------------------------------------------------------
 // k_final: finalShading + exposureToneMapping + Screen::setPixel y-flip.  rgb rows: row 0 = top of rect.
-template <int NT>
+// Persistent blocks stage the BVH into LDS once (shadow rays are the kernel's main cost).
+template <int NT, bool LDS_BVH>
 __device__ __forceinline__ void final_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, v3 origin,
                                            const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                            const float4* __restrict__ ra, const float4* __restrict__ rb,
                                            float* __restrict__ rgb) {
-    uint32_t x, y;
-    size_t p;
-    if (!tile_pixel(rg, x, y, p)) return;
+    const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
-    Px px = load_px(s, n_t, p_mat, p, origin);
-    v3 color = mk(0.0f, 0.0f, 0.0f);
-    for (uint32_t j = 0; j < N; j++) {
-        Sub r;
-        sub_load(r, ra, rb, j * npx + p);
-        v3 sc = shade(f, px, r.pos, r.col);
-        // The visibility test can only matter when the shaded value is non-zero: (vis ? sc : 0) * W equals
-        // sc * W when sc == 0 (both are 0 * W), so the shadow ray is skipped exactly then.
-        if ((sc.x != 0.0f || sc.y != 0.0f || sc.z != 0.0f) && !visible(s, px.P, r.pos)) sc = mk(0.0f, 0.0f, 0.0f);
-        sc = vscale(sc, r.W);
-        color = vadd(color, sc);
+    const uint32_t nt = num_tiles(rg);
+    const float g = 1.0f / f.gamma;
+    for (uint32_t tile = blockIdx.x; tile < nt; tile += gridDim.x) {
+        uint32_t x, y;
+        size_t p;
+        if (!tile_pixel_of(rg, tile, x, y, p)) continue;
+        Px px = load_px(s, n_t, p_mat, p, origin);
+        v3 color = mk(0.0f, 0.0f, 0.0f);
+        for (uint32_t j = 0; j < N; j++) {
+            Sub r;
+            sub_load(r, ra, rb, j * npx + p);
+            v3 sc = shade(f, px, r.pos, r.col);
+            // The visibility test can only matter when the shaded value is non-zero: (vis ? sc : 0) * W equals
+            // sc * W when sc == 0 (both are 0 * W), so the shadow ray is skipped exactly then.
+            if ((sc.x != 0.0f || sc.y != 0.0f || sc.z != 0.0f) && !visible(bvh, px.P, r.pos)) sc = mk(0.0f, 0.0f, 0.0f);
+            sc = vscale(sc, r.W);
+            color = vadd(color, sc);
+        }
+        color = vdivs(color, (float)N);
+        if (f.tone_map) {
+            v3 e = vscale(mk(-color.x, -color.y, -color.z), f.exposure);
+            v3 mapped = mk(1.0f - pm_expf(e.x), 1.0f - pm_expf(e.y), 1.0f - pm_expf(e.z));
+            // pm_powf(x, 1) == x for every x (gamma = 1, the Features default): skip the call
+            color = g == 1.0f ? mapped : mk(pm_powf(mapped.x, g), pm_powf(mapped.y, g), pm_powf(mapped.z, g));
+        }
+        const uint32_t row = rg.rh - 1u - (y - rg.ry0);
+        float* o = rgb + 3 * ((size_t)row * rg.rw + (x - rg.rx0));
+        o[0] = color.x; o[1] = color.y; o[2] = color.z;
     }
-    color = vdivs(color, (float)N);
-    if (f.tone_map) {
-        v3 e = vscale(mk(-color.x, -color.y, -color.z), f.exposure);
-        v3 mapped = mk(1.0f - pm_expf(e.x), 1.0f - pm_expf(e.y), 1.0f - pm_expf(e.z));
-        float g = 1.0f / f.gamma;
-        color = mk(pm_powf(mapped.x, g), pm_powf(mapped.y, g), pm_powf(mapped.z, g));
-    }
-    const uint32_t row = rg.rh - 1u - (y - rg.ry0);
-    float* o = rgb + 3 * ((size_t)row * rg.rw + (x - rg.rx0));
-    o[0] = color.x; o[1] = color.y; o[2] = color.z;
 }
 
-#define ROMIS_FINAL_KERNEL(NT)                                                                                         \
-    extern "C" __global__ __launch_bounds__(256) void k_final_n##NT(SceneDev s, Region rg, FeaturesDev f, float ox,      \
-                                                                   float oy, float oz, const float4* n_t,               \
-                                                                   const float4* p_mat, const float4* ra,               \
-                                                                   const float4* rb, float* rgb) {                      \
-        final_body<NT>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb);                                              \
+#define ROMIS_FINAL_KERNEL(NT, LDS, NAME)                                                                              \
+    extern "C" __global__ __launch_bounds__(256) void NAME(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,     \
+                                                          float oz, const float4* n_t, const float4* p_mat,             \
+                                                          const float4* ra, const float4* rb, float* rgb) {             \
+        final_body<NT, LDS>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb);                                         \
     }
-ROMIS_FINAL_KERNEL(1)
-ROMIS_FINAL_KERNEL(2)
-ROMIS_FINAL_KERNEL(0)
+ROMIS_FINAL_KERNEL(1, false, k_final_n1)
+ROMIS_FINAL_KERNEL(2, false, k_final_n2)
+ROMIS_FINAL_KERNEL(0, false, k_final_n0)
+ROMIS_FINAL_KERNEL(1, true, k_final_n1_lds)
+ROMIS_FINAL_KERNEL(2, true, k_final_n2_lds)
+ROMIS_FINAL_KERNEL(0, true, k_final_n0_lds)
 
 // ---------------------------------------------------------------------------------------------------------
 // Test hooks: device powf / expf on arrays (parity of the portable math with the oracle).
@@ -632,26 +758,42 @@ extern "C" __global__ void k_debug_math(const float* x, const float* y, float* p
 namespace romis {
 namespace {
 constexpr uint32_t kBlock = 256;
-inline dim3 grid_for(const Region& rg) { return dim3((rg.rw * rg.rh + kBlock - 1) / kBlock); }
-inline dim3 grid_tiles(const Region& rg) {
-    return dim3(((rg.rw + kTileW - 1) / kTileW) * ((rg.rh + kTileH - 1) / kTileH));
-}
 static_assert(kTileW * kTileH == kBlock, "one lane per tile pixel");
+// persistent grids: 256 CUs x 4 blocks of 256 lanes
+constexpr uint32_t kPersistentBlocks = 1024;
+constexpr size_t kLdsBudget = 64 * 1024;
+
+inline uint32_t tiles_of(const Region& rg) {
+    return ((rg.rw + kTileW - 1) / kTileW) * ((rg.rh + kTileH - 1) / kTileH);
+}
+inline dim3 grid_for(const Region& rg) { return dim3((rg.rw * rg.rh + kBlock - 1) / kBlock); }
+inline dim3 grid_tiles(const Region& rg) { return dim3(tiles_of(rg)); }
+inline dim3 grid_persistent(uint32_t work_items) { return dim3(work_items < kPersistentBlocks ? work_items : kPersistentBlocks); }
+inline size_t bvh_lds_bytes(const SceneDev& s) { return ((size_t)2 * s.num_nodes + (size_t)3 * s.num_tris) * 16; }
+inline size_t lights_lds_bytes(const SceneDev& s) { return (size_t)7 * s.num_lights * 16; }
 }  // namespace
 
 hipError_t launch_primary(const SceneDev& s, const Region& rg, const CameraDev& cam, float4* n_t, float4* p_mat,
                           hipStream_t stream) {
     if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_primary, grid_tiles(rg), dim3(kBlock), 0, stream, s, rg, cam, n_t, p_mat);
+    const size_t lds = bvh_lds_bytes(s);
+    if (lds <= kLdsBudget)
+        hipLaunchKernelGGL(k_primary_lds, grid_persistent(tiles_of(rg)), dim3(kBlock), lds, stream, s, rg, cam, n_t, p_mat);
+    else
+        hipLaunchKernelGGL(k_primary, grid_persistent(tiles_of(rg)), dim3(kBlock), 0, stream, s, rg, cam, n_t, p_mat);
     return hipGetLastError();
 }
 
 hipError_t launch_ris(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* o,
                       const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, hipStream_t stream) {
     if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
-    auto k = f.N == 1 ? k_ris_n1 : (f.N == 2 ? k_ris_n2 : k_ris_n0);
-    hipLaunchKernelGGL(k, grid_for(rg), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ra, rb,
-                       rdbg);
+    const size_t lds = lights_lds_bytes(s);
+    const bool use_lds = s.num_lights > 0 && lds <= kLdsBudget;
+    auto k = use_lds ? (f.N == 1 ? k_ris_n1_lds : (f.N == 2 ? k_ris_n2_lds : k_ris_n0_lds))
+                     : (f.N == 1 ? k_ris_n1 : (f.N == 2 ? k_ris_n2 : k_ris_n0));
+    const uint32_t items = (rg.rw * rg.rh + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k, grid_persistent(items), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f, key, o[0], o[1],
+                       o[2], n_t, p_mat, ra, rb, rdbg);
     return hipGetLastError();
 }
 
@@ -680,8 +822,12 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg, const FeaturesDev
 hipError_t launch_final(const SceneDev& s, const Region& rg, const FeaturesDev& f, const float* o, const float4* n_t,
                         const float4* p_mat, const float4* ra, const float4* rb, float* rgb, hipStream_t stream) {
     if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
-    auto k = f.N == 1 ? k_final_n1 : (f.N == 2 ? k_final_n2 : k_final_n0);
-    hipLaunchKernelGGL(k, grid_tiles(rg), dim3(kBlock), 0, stream, s, rg, f, o[0], o[1], o[2], n_t, p_mat, ra, rb, rgb);
+    const size_t lds = bvh_lds_bytes(s);
+    const bool use_lds = lds <= kLdsBudget;
+    auto k = use_lds ? (f.N == 1 ? k_final_n1_lds : (f.N == 2 ? k_final_n2_lds : k_final_n0_lds))
+                     : (f.N == 1 ? k_final_n1 : (f.N == 2 ? k_final_n2 : k_final_n0));
+    hipLaunchKernelGGL(k, grid_persistent(tiles_of(rg)), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f, o[0], o[1],
+                       o[2], n_t, p_mat, ra, rb, rgb);
     return hipGetLastError();
 }
 

@@ -125,6 +125,7 @@ SIGNATURES = {
     "restir_debug_math": (C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                     C.POINTER(C.c_float), C.c_size_t]),
     "restir_enable_timing": (C.c_int, [_P, C.c_int]),
+    "restir_set_tuning": (C.c_int, [_P, C.c_char_p, C.c_int]),
     "restir_timings": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "restir_reset_timings": (C.c_int, [_P]),
 }

@@ -364,6 +364,14 @@ __device__ __forceinline__ bool region_pixel(const Region& rg, uint32_t idx, uin
     return true;
 }
 
+// Work items of a launch: 32x8 tiles (map2d) or runs of 256 row-major pixels.
+__device__ __forceinline__ uint32_t work_items(const Region& rg) {
+    return rg.map2d ? num_tiles(rg) : (rg.rw * rg.rh + 255u) / 256u;
+}
+__device__ __forceinline__ bool work_pixel(const Region& rg, uint32_t item, uint32_t& x, uint32_t& y, size_t& p) {
+    return rg.map2d ? tile_pixel_of(rg, item, x, y, p) : region_pixel(rg, item * 256u + threadIdx.x, x, y, p);
+}
+
 }  // namespace romis
 
 using namespace romis;
@@ -376,12 +384,12 @@ template <bool LDS_BVH>
 __device__ __forceinline__ void primary_body(const SceneDev& s, const Region& rg, const CameraDev& cam,
                                              float4* __restrict__ n_t, float4* __restrict__ p_mat) {
     const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
-    const uint32_t nt = num_tiles(rg);
+    const uint32_t nt = work_items(rg);
     const v3 o = mk(cam.origin[0], cam.origin[1], cam.origin[2]);
     for (uint32_t tile = blockIdx.x; tile < nt; tile += gridDim.x) {
         uint32_t x, y;
         size_t p;
-        if (!tile_pixel_of(rg, tile, x, y, p)) continue;
+        if (!work_pixel(rg, tile, x, y, p)) continue;
         float nx = (float)x / (float)rg.W * 2.0f - 1.0f;
         float ny = (float)y / (float)rg.H * 2.0f - 1.0f;
         v3 csd = vnormalize(mk(-nx * cam.half_w, ny * cam.half_h, 1.0f));
@@ -430,12 +438,12 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
     const Bvh bvh = global_bvh(s);
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
-    const uint32_t total = rg.rw * rg.rh;
+    const uint32_t items = work_items(rg);
     const float invL = 1.0f / (float)L;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
+    for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {
         uint32_t x, y;
         size_t p;
-        if (!region_pixel(rg, base + threadIdx.x, x, y, p)) continue;
+        if (!work_pixel(rg, item, x, y, p)) continue;
         Sub r[NT > 0 ? NT : RESTIR_MAX_N_DEV];
         for (uint32_t j = 0; j < N; j++) sub_init(r[j]);
         if (L != 0) {
@@ -577,7 +585,7 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
                                              float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg) {
     uint32_t x, y;
     size_t p;
-    if (!tile_pixel_of(rg, xcd_banded_tile(), x, y, p)) return;
+    if (!work_pixel(rg, rg.map2d ? xcd_banded_tile() : blockIdx.x, x, y, p)) return;
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
     const uint32_t K = f.K;
@@ -698,12 +706,12 @@ __device__ __forceinline__ void final_body(const SceneDev& s, const Region& rg, 
     const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
-    const uint32_t nt = num_tiles(rg);
+    const uint32_t nt = work_items(rg);
     const float g = 1.0f / f.gamma;
     for (uint32_t tile = blockIdx.x; tile < nt; tile += gridDim.x) {
         uint32_t x, y;
         size_t p;
-        if (!tile_pixel_of(rg, tile, x, y, p)) continue;
+        if (!work_pixel(rg, tile, x, y, p)) continue;
         Px px = load_px(s, n_t, p_mat, p, origin);
         v3 color = mk(0.0f, 0.0f, 0.0f);
         for (uint32_t j = 0; j < N; j++) {
@@ -759,75 +767,81 @@ namespace romis {
 namespace {
 constexpr uint32_t kBlock = 256;
 static_assert(kTileW * kTileH == kBlock, "one lane per tile pixel");
-// persistent grids: 256 CUs x 4 blocks of 256 lanes
-constexpr uint32_t kPersistentBlocks = 1024;
 constexpr size_t kLdsBudget = 64 * 1024;
 
-inline uint32_t tiles_of(const Region& rg) {
-    return ((rg.rw + kTileW - 1) / kTileW) * ((rg.rh + kTileH - 1) / kTileH);
+inline uint32_t items_of(const Region& rg) {
+    return rg.map2d ? ((rg.rw + kTileW - 1) / kTileW) * ((rg.rh + kTileH - 1) / kTileH) : (rg.rw * rg.rh + kBlock - 1) / kBlock;
 }
-inline dim3 grid_for(const Region& rg) { return dim3((rg.rw * rg.rh + kBlock - 1) / kBlock); }
-inline dim3 grid_tiles(const Region& rg) { return dim3(tiles_of(rg)); }
-inline dim3 grid_persistent(uint32_t work_items) { return dim3(work_items < kPersistentBlocks ? work_items : kPersistentBlocks); }
+// cap = 0: one block per work item; else a persistent grid of at most `cap` blocks
+inline dim3 grid_capped(uint32_t items, uint32_t cap) { return dim3(cap && items > cap ? cap : items); }
 inline size_t bvh_lds_bytes(const SceneDev& s) { return ((size_t)2 * s.num_nodes + (size_t)3 * s.num_tris) * 16; }
 inline size_t lights_lds_bytes(const SceneDev& s) { return (size_t)7 * s.num_lights * 16; }
+inline Region with_map(Region rg, uint32_t map2d) { rg.map2d = map2d; return rg; }
 }  // namespace
 
-hipError_t launch_primary(const SceneDev& s, const Region& rg, const CameraDev& cam, float4* n_t, float4* p_mat,
-                          hipStream_t stream) {
-    if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
+hipError_t launch_primary(const SceneDev& s, const Region& rg0, const CameraDev& cam, float4* n_t, float4* p_mat,
+                          const Tuning& tu, hipStream_t stream) {
+    if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
+    const Region rg = with_map(rg0, tu.primary_2d);
     const size_t lds = bvh_lds_bytes(s);
-    if (lds <= kLdsBudget)
-        hipLaunchKernelGGL(k_primary_lds, grid_persistent(tiles_of(rg)), dim3(kBlock), lds, stream, s, rg, cam, n_t, p_mat);
+    const dim3 grid = grid_capped(items_of(rg), tu.primary_blocks);
+    if (tu.primary_lds && lds <= kLdsBudget)
+        hipLaunchKernelGGL(k_primary_lds, grid, dim3(kBlock), lds, stream, s, rg, cam, n_t, p_mat);
     else
-        hipLaunchKernelGGL(k_primary, grid_persistent(tiles_of(rg)), dim3(kBlock), 0, stream, s, rg, cam, n_t, p_mat);
+        hipLaunchKernelGGL(k_primary, grid, dim3(kBlock), 0, stream, s, rg, cam, n_t, p_mat);
     return hipGetLastError();
 }
 
-hipError_t launch_ris(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* o,
-                      const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, hipStream_t stream) {
-    if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
+hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
+                      const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, const Tuning& tu,
+                      hipStream_t stream) {
+    if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
+    const Region rg = with_map(rg0, 0);
     const size_t lds = lights_lds_bytes(s);
-    const bool use_lds = s.num_lights > 0 && lds <= kLdsBudget;
+    const bool use_lds = tu.ris_lds && s.num_lights > 0 && lds <= kLdsBudget;
     auto k = use_lds ? (f.N == 1 ? k_ris_n1_lds : (f.N == 2 ? k_ris_n2_lds : k_ris_n0_lds))
                      : (f.N == 1 ? k_ris_n1 : (f.N == 2 ? k_ris_n2 : k_ris_n0));
-    const uint32_t items = (rg.rw * rg.rh + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k, grid_persistent(items), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f, key, o[0], o[1],
-                       o[2], n_t, p_mat, ra, rb, rdbg);
+    hipLaunchKernelGGL(k, grid_capped(items_of(rg), tu.ris_blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,
+                       key, o[0], o[1], o[2], n_t, p_mat, ra, rb, rdbg);
     return hipGetLastError();
 }
 
-hipError_t launch_temporal(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* o,
+hipError_t launch_temporal(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
                            const float4* n_t, const float4* p_mat, const float4* ca, const float4* cb,
                            const float4* pa, const float4* pb, float4* oa, float4* ob, float2* odbg,
-                           hipStream_t stream) {
-    if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
+                           const Tuning& tu, hipStream_t stream) {
+    (void)tu;
+    if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
+    const Region rg = with_map(rg0, 0);
     auto k = f.N == 1 ? k_temporal_n1 : (f.N == 2 ? k_temporal_n2 : k_temporal_n0);
-    hipLaunchKernelGGL(k, grid_for(rg), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ca, cb,
+    hipLaunchKernelGGL(k, dim3(items_of(rg)), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ca, cb,
                        pa, pb, oa, ob, odbg);
     return hipGetLastError();
 }
 
-hipError_t launch_spatial(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* o,
+hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
                           const float4* n_t, const float4* p_mat, const float4* ia, const float4* ib, float4* oa,
-                          float4* ob, float2* odbg, hipStream_t stream) {
-    if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
+                          float4* ob, float2* odbg, const Tuning& tu, hipStream_t stream) {
+    if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
+    const Region rg = with_map(rg0, tu.spatial_xcd);   // XCD-banded order works on 2D tiles
     auto k = f.unbiased ? (f.N == 1 ? k_spatial_n1_unbiased : (f.N == 2 ? k_spatial_n2_unbiased : k_spatial_n0_unbiased))
                         : (f.N == 1 ? k_spatial_n1_biased : (f.N == 2 ? k_spatial_n2_biased : k_spatial_n0_biased));
-    hipLaunchKernelGGL(k, grid_tiles(rg), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib,
+    hipLaunchKernelGGL(k, dim3(items_of(rg)), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib,
                        oa, ob, odbg);
     return hipGetLastError();
 }
 
-hipError_t launch_final(const SceneDev& s, const Region& rg, const FeaturesDev& f, const float* o, const float4* n_t,
-                        const float4* p_mat, const float4* ra, const float4* rb, float* rgb, hipStream_t stream) {
-    if (rg.rw == 0 || rg.rh == 0) return hipSuccess;
+hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev& f, const float* o, const float4* n_t,
+                        const float4* p_mat, const float4* ra, const float4* rb, float* rgb, const Tuning& tu,
+                        hipStream_t stream) {
+    if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
+    const Region rg = with_map(rg0, tu.final_2d);
     const size_t lds = bvh_lds_bytes(s);
-    const bool use_lds = lds <= kLdsBudget;
+    const bool use_lds = tu.final_lds && lds <= kLdsBudget;
     auto k = use_lds ? (f.N == 1 ? k_final_n1_lds : (f.N == 2 ? k_final_n2_lds : k_final_n0_lds))
                      : (f.N == 1 ? k_final_n1 : (f.N == 2 ? k_final_n2 : k_final_n0));
-    hipLaunchKernelGGL(k, grid_persistent(tiles_of(rg)), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f, o[0], o[1],
-                       o[2], n_t, p_mat, ra, rb, rgb);
+    hipLaunchKernelGGL(k, grid_capped(items_of(rg), tu.final_blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,
+                       o[0], o[1], o[2], n_t, p_mat, ra, rb, rgb);
     return hipGetLastError();
 }
 

@@ -6,19 +6,20 @@
 namespace romis {
 
 hipError_t launch_primary(const SceneDev& s, const Region& rg, const CameraDev& cam, float4* n_t, float4* p_mat,
-                          hipStream_t stream);
+                          const Tuning& tu, hipStream_t stream);
 hipError_t launch_ris(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
-                      const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, hipStream_t stream);
+                      const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, const Tuning& tu,
+                      hipStream_t stream);
 hipError_t launch_temporal(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
                            const float4* n_t, const float4* p_mat, const float4* ca, const float4* cb,
                            const float4* pa, const float4* pb, float4* oa, float4* ob, float2* odbg,
-                           hipStream_t stream);
+                           const Tuning& tu, hipStream_t stream);
 hipError_t launch_spatial(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
                           const float4* n_t, const float4* p_mat, const float4* ia, const float4* ib, float4* oa,
-                          float4* ob, float2* odbg, hipStream_t stream);
+                          float4* ob, float2* odbg, const Tuning& tu, hipStream_t stream);
 hipError_t launch_final(const SceneDev& s, const Region& rg, const FeaturesDev& f, const float* origin,
                         const float4* n_t, const float4* p_mat, const float4* ra, const float4* rb, float* rgb,
-                        hipStream_t stream);
+                        const Tuning& tu, hipStream_t stream);
 hipError_t launch_debug_math(const float* x, const float* y, float* pw, float* ex, uint32_t n, hipStream_t stream);
 
 }  // namespace romis

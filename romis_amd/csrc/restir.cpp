@@ -110,6 +110,9 @@ struct restir_ctx {
     int cur = 0;
     uint32_t rgb_w = 0, rgb_h = 0;
 
+    // launch-shape knobs (restir_set_tuning)
+    Tuning tuning{};
+
     // RNG
     uint32_t seed = RESTIR_DEFAULT_SEED;
     uint32_t frame_index = 0;
@@ -330,7 +333,7 @@ CameraDev camera_dev(const restir_camera* cam) {
 
 Region make_region(uint32_t W, uint32_t H, uint32_t vx0, uint32_t vy0, uint32_t vw, uint32_t vh, uint32_t rx0,
                    uint32_t ry0, uint32_t rw, uint32_t rh) {
-    Region r;
+    Region r{};
     r.W = W; r.H = H;
     r.vx0 = vx0; r.vy0 = vy0; r.vw = vw; r.vh = vh;
     r.rx0 = rx0; r.ry0 = ry0; r.rw = rw; r.rh = rh;
@@ -586,14 +589,14 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     float4* pm = c->p_mat.as<float4>();
     int cur = 0;
 
-    TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, nt, pm, c->stream));
+    TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, nt, pm, c->tuning, c->stream));
     TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, 0), camd.origin, nt, pm,
-                                      c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), nullptr, c->stream));
+                                      c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), nullptr, c->tuning, c->stream));
     if (temporal) {
         TIMED(c, RESTIR_K_TEMPORAL,
               launch_temporal(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0), camd.origin, nt, pm,
                               c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), prev->a.as<float4>(),
-                              prev->b.as<float4>(), c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), nullptr, c->stream));
+                              prev->b.as<float4>(), c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), nullptr, c->tuning, c->stream));
     }
     for (uint32_t pass = 0; pass < passes; pass++) {
         const Region pr = grow_rect(owned, (passes - 1u - pass) * f.R);
@@ -601,11 +604,11 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
         TIMED(c, RESTIR_K_SPATIAL,
               launch_spatial(s, pr, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_SPATIAL, pass), camd.origin, nt, pm,
                              c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->ra[nxt].as<float4>(),
-                             c->rb[nxt].as<float4>(), nullptr, c->stream));
+                             c->rb[nxt].as<float4>(), nullptr, c->tuning, c->stream));
         cur = nxt;
     }
     TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, nt, pm, c->ra[cur].as<float4>(), c->rb[cur].as<float4>(),
-                                          c->rgb.as<float>(), c->stream));
+                                          c->rgb.as<float>(), c->tuning, c->stream));
     c->cur = cur;
 
     if (out_next) {
@@ -734,7 +737,7 @@ restir_status restir_stage_primary(restir_ctx* c, const restir_camera* cam) {
     if (!cam) return fail(RESTIR_ERR_INVALID, "camera is NULL");
     STAGE_PRELUDE();
     const CameraDev camd = camera_dev(cam);
-    TIMED(c, RESTIR_K_PRIMARY, launch_primary(c->sdev, c->stage_rg, camd, c->n_t.as<float4>(), c->p_mat.as<float4>(), c->stream));
+    TIMED(c, RESTIR_K_PRIMARY, launch_primary(c->sdev, c->stage_rg, camd, c->n_t.as<float4>(), c->p_mat.as<float4>(), c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
@@ -756,7 +759,7 @@ restir_status restir_stage_ris(restir_ctx* c, const restir_camera* cam, const re
     const int cur = c->cur;
     TIMED(c, RESTIR_K_RIS, launch_ris(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                                       c->ra[cur].as<float4>(), c->rb[cur].as<float4>(),
-                                      debug ? c->dbg[cur].as<float2>() : nullptr, c->stream));
+                                      debug ? c->dbg[cur].as<float2>() : nullptr, c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
@@ -773,7 +776,7 @@ restir_status restir_stage_temporal(restir_ctx* c, const restir_camera* cam, con
           launch_temporal(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                           c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->ra[prv].as<float4>(), c->rb[prv].as<float4>(),
                           c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), debug ? c->dbg[cur].as<float2>() : nullptr,
-                          c->stream));
+                          c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
@@ -789,7 +792,7 @@ restir_status restir_stage_spatial(restir_ctx* c, const restir_camera* cam, cons
     TIMED(c, RESTIR_K_SPATIAL,
           launch_spatial(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                          c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->ra[nxt].as<float4>(), c->rb[nxt].as<float4>(),
-                         debug ? c->dbg[nxt].as<float2>() : nullptr, c->stream));
+                         debug ? c->dbg[nxt].as<float2>() : nullptr, c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->cur = nxt;   // the pass output becomes "current" (RES_*), its input "prev" (PREV_*)
     return RESTIR_OK;
@@ -803,7 +806,7 @@ restir_status restir_stage_final(restir_ctx* c, const restir_camera* cam, const 
     const CameraDev camd = camera_dev(cam);
     const int cur = c->cur;
     TIMED(c, RESTIR_K_FINAL, launch_final(c->sdev, c->stage_rg, d, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
-                                          c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->rgb.as<float>(), c->stream));
+                                          c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->rgb.as<float>(), c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
@@ -844,6 +847,24 @@ restir_status restir_timings(restir_ctx* c, double* ms, uint64_t* launches) {
         if (ms) ms[k] = c->ms[k];
         if (launches) launches[k] = c->launches[k];
     }
+    return RESTIR_OK;
+}
+
+restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
+    if (!c || !key) return fail(RESTIR_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    Tuning& t = c->tuning;
+    const uint32_t v = (uint32_t)value;
+    if (!std::strcmp(key, "primary.blocks")) t.primary_blocks = v;
+    else if (!std::strcmp(key, "primary.lds")) t.primary_lds = v;
+    else if (!std::strcmp(key, "primary.2d")) t.primary_2d = v;
+    else if (!std::strcmp(key, "ris.blocks")) t.ris_blocks = v;
+    else if (!std::strcmp(key, "ris.lds")) t.ris_lds = v;
+    else if (!std::strcmp(key, "spatial.xcd")) t.spatial_xcd = v;
+    else if (!std::strcmp(key, "final.blocks")) t.final_blocks = v;
+    else if (!std::strcmp(key, "final.lds")) t.final_lds = v;
+    else if (!std::strcmp(key, "final.2d")) t.final_2d = v;
+    else return fail(RESTIR_ERR_INVALID, "unknown tuning key '%s'", key);
     return RESTIR_OK;
 }
 

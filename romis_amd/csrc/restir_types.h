@@ -49,6 +49,20 @@ struct Region {
     uint32_t W, H;
     uint32_t vx0, vy0, vw, vh;
     uint32_t rx0, ry0, rw, rh;
+    uint32_t map2d;   // work item = a 32x8 tile (1) or 256 consecutive row-major pixels (0)
+};
+
+// Launch-shape knobs (restir_set_tuning); they never change results, only speed.
+struct Tuning {
+    uint32_t primary_blocks = 0;   // grid cap (persistent blocks); 0 = one block per work item
+    uint32_t primary_lds = 1;      // stage the BVH in LDS when it fits
+    uint32_t primary_2d = 1;
+    uint32_t ris_blocks = 0;
+    uint32_t ris_lds = 0;          // stage the light table in LDS when it fits
+    uint32_t spatial_xcd = 1;      // XCD-banded tile order
+    uint32_t final_blocks = 0;
+    uint32_t final_lds = 1;
+    uint32_t final_2d = 1;
 };
 
 struct CameraDev {

@@ -95,6 +95,9 @@ class Renderer:
         check(self.lib, self.lib.restir_timings(self.ctx, ms, n), "restir_timings")
         return {name: (ms[i], n[i]) for i, name in enumerate(_abi.KERNEL_NAMES)}
 
+    def set_tuning(self, key: str, value: int) -> None:
+        check(self.lib, self.lib.restir_set_tuning(self.ctx, key.encode(), int(value)), "restir_set_tuning")
+
     def reset_timings(self) -> None:
         check(self.lib, self.lib.restir_reset_timings(self.ctx), "restir_reset_timings")
 

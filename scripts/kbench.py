@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Interleaved in-process A/B of launch-shape knobs (restir_set_tuning) on the headline 1080p frame.
+
+    python scripts/kbench.py [--rounds 5] [--frames 10]
+
+Every variant renders the same frames; per-kernel times come from HIP events on the context's stream.
+Prints one JSON object: {variant: {kernel: median us per launch}}.  Knobs never change results (the GPU
+parity suite checks that under the defaults; this script also checks the RGB of every variant is identical).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+from romis_amd import _abi, restir, scene  # noqa: E402
+
+DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 0,
+            "spatial.xcd": 1, "final.blocks": 0, "final.lds": 1, "final.2d": 1}
+
+VARIANTS = {
+    "default": {},
+    "primary_1d_global": {"primary.2d": 0, "primary.lds": 0},
+    "primary_1d_lds": {"primary.2d": 0},
+    "primary_2d_global": {"primary.lds": 0},
+    "primary_2d_lds_p1024": {"primary.blocks": 1024},
+    "primary_2d_lds_p2048": {"primary.blocks": 2048},
+    "ris_lds": {"ris.lds": 1},
+    "ris_p2048": {"ris.blocks": 2048},
+    "ris_lds_p2048": {"ris.lds": 1, "ris.blocks": 2048},
+    "spatial_noxcd": {"spatial.xcd": 0},
+    "final_1d_global": {"final.2d": 0, "final.lds": 0},
+    "final_1d_lds": {"final.2d": 0},
+    "final_2d_global": {"final.lds": 0},
+    "final_2d_lds_p1024": {"final.blocks": 1024},
+    "final_2d_lds_p2048": {"final.blocks": 2048},
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--scene", default="nightclub_128pt")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    args = ap.parse_args()
+    W, H = args.width, args.height
+    r = restir.Renderer(0)
+    r.set_scene(scene.bench_scene(args.scene))
+    cam = scene.camera_for(args.scene, W, H)
+    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=1, temporal_reuse=0)
+    ref_rgb = None
+    samples = {v: {k: [] for k in _abi.KERNEL_NAMES} for v in VARIANTS}
+    for rnd in range(args.rounds):
+        for name, knobs in VARIANTS.items():
+            for k, v in {**DEFAULTS, **knobs}.items():
+                r.set_tuning(k, v)
+            r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
+            rgb, _ = r.render_restir(None, cam, W, H, f, want_grid=False)   # warm + result check
+            if ref_rgb is None:
+                ref_rgb = rgb
+            elif not np.array_equal(rgb.view(np.uint32), ref_rgb.view(np.uint32)):
+                raise SystemExit(f"variant {name} changed the image")
+            r.reset_timings()
+            r.enable_timing(True)
+            for _ in range(args.frames):
+                r.render_restir(None, cam, W, H, f, want_rgb=False, want_grid=False)
+            r.synchronize()
+            r.enable_timing(False)
+            for k, (ms, n) in r.timings().items():
+                if n:
+                    samples[name][k].append(ms / n * 1e3)
+    out = {name: {k: round(statistics.median(v), 2) for k, v in ks.items() if v} for name, ks in samples.items()}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

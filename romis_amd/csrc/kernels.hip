@@ -244,24 +244,29 @@ struct Sub {
     float W;
     uint32_t M;
     float wsum, chosen;
+    // target pdf of the held sample at the combining pixel, cached when the sample was accepted: the
+    // final W (reservoir.cpp:61-64, light.cpp:90-93) re-evaluates exactly that value, so it is reused
+    float pd;
+    bool has_pd;
 };
 
 __device__ __forceinline__ void sub_init(Sub& r) {
     r.pos = mk(0.0f, 0.0f, 0.0f); r.col = mk(0.0f, 0.0f, 0.0f);
     r.W = 0.0f; r.M = 1u; r.wsum = ROMIS_FLT_MIN; r.chosen = 0.0f;
+    r.pd = 0.0f; r.has_pd = false;
 }
 
 // Reservoir::update (reservoir.cpp:10-32)
-__device__ __forceinline__ void sub_take(Sub& r, v3 pos, v3 col, float w, float u) {
+__device__ __forceinline__ void sub_take(Sub& r, v3 pos, v3 col, float w, float u, float pd) {
     r.M += 1u;
     r.wsum += w;
-    if (u < (w / r.wsum)) { r.pos = pos; r.col = col; r.chosen = w; }
+    if (u < (w / r.wsum)) { r.pos = pos; r.col = col; r.chosen = w; r.pd = pd; r.has_pd = true; }
 }
 
 template <int NT>
-__device__ __forceinline__ uint32_t res_update(Sub* r, uint32_t N, v3 pos, v3 col, float w, float u) {
+__device__ __forceinline__ uint32_t res_update(Sub* r, uint32_t N, v3 pos, v3 col, float w, float u, float pd) {
     if (NT == 1) {
-        sub_take(r[0], pos, col, w, u);
+        sub_take(r[0], pos, col, w, u, pd);
         return 0;
     }
     uint32_t k = 0;
@@ -274,11 +279,11 @@ __device__ __forceinline__ uint32_t res_update(Sub* r, uint32_t N, v3 pos, v3 co
             if (r[j].wsum < best) { k = j; best = r[j].wsum; }
 #pragma unroll
         for (uint32_t j = 0; j < (uint32_t)(NT > 0 ? NT : 1); j++)
-            if (j == k) sub_take(r[j], pos, col, w, u);
+            if (j == k) sub_take(r[j], pos, col, w, u, pd);
     } else {
         for (uint32_t j = 0; j < n; j++)
             if (r[j].wsum < best) { k = j; best = r[j].wsum; }
-        sub_take(r[k], pos, col, w, u);
+        sub_take(r[k], pos, col, w, u, pd);
     }
     return k;
 }
@@ -304,6 +309,7 @@ __device__ __forceinline__ Sub sub_from(float4 fa, float4 fb) {
     r.pos = xyz(fa); r.W = fa.w;
     r.col = xyz(fb); r.M = __float_as_uint(fb.w);
     r.wsum = 0.0f; r.chosen = 0.0f;
+    r.pd = 0.0f; r.has_pd = false;
     return r;
 }
 
@@ -472,11 +478,12 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
                 }
                 const float pd = target_pdf(f, px, pos, col);
                 const float w = s.light_scale != 0.0f ? pd * s.light_scale : pd / invL;   // light.cpp:80
-                res_update<NT>(r, N, pos, col, w, rand01(draw(ps, 4u * c + 3u)));
+                res_update<NT>(r, N, pos, col, w, rand01(draw(ps, 4u * c + 3u)), pd);
             }
             for (uint32_t j = 0; j < N; j++) {
                 if (f.initial_vis && !visible(bvh, px.P, r[j].pos)) r[j].W = 0.0f;
-                else r[j].W = contribution_weight(target_pdf(f, px, r[j].pos, r[j].col), r[j].M, r[j].wsum);
+                else r[j].W = contribution_weight(r[j].has_pd ? r[j].pd : target_pdf(f, px, r[j].pos, r[j].col), r[j].M,
+                                                  r[j].wsum);
             }
         }
         for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, j * npx + p);
@@ -515,14 +522,15 @@ struct Combiner {
     __device__ __forceinline__ void consume(const FeaturesDev& f, const Px& cur, const Sub& in, uint32_t ps, uint32_t slot0) {
         float pd = target_pdf(f, cur, in.pos, in.col);
         float w = (pd * in.W) * (float)in.M;
-        uint32_t k = res_update<NT>(out, n(), in.pos, in.col, w, rand01(draw(ps, slot0 + t)));
+        uint32_t k = res_update<NT>(out, n(), in.pos, in.col, w, rand01(draw(ps, slot0 + t)), pd);
         t++;
         macc_add<NT>(macc, k, in.M);
     }
     __device__ __forceinline__ void finish_biased(const FeaturesDev& f, const Px& cur) {
         for (uint32_t j = 0; j < n(); j++) out[j].M = macc[j];
         for (uint32_t j = 0; j < n(); j++)
-            out[j].W = contribution_weight(target_pdf(f, cur, out[j].pos, out[j].col), out[j].M, out[j].wsum);
+            out[j].W = contribution_weight(out[j].has_pd ? out[j].pd : target_pdf(f, cur, out[j].pos, out[j].col),
+                                           out[j].M, out[j].wsum);
     }
 };
 
@@ -673,7 +681,7 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
             }
         }
         for (uint32_t j = 0; j < N; j++) {
-            float pc = target_pdf(f, cur, cmb.out[j].pos, cmb.out[j].col);
+            float pc = cmb.out[j].has_pd ? cmb.out[j].pd : target_pdf(f, cur, cmb.out[j].pos, cmb.out[j].col);
             if (pc == 0.0f || Z[j] == 0ull) cmb.out[j].W = 0.0f;
             else cmb.out[j].W = ((1.0f / pc) * (1.0f / (float)Z[j])) * cmb.out[j].wsum;
         }

@@ -58,7 +58,7 @@ struct Tuning {
     uint32_t primary_lds = 1;      // stage the BVH in LDS when it fits
     uint32_t primary_2d = 1;
     uint32_t ris_blocks = 0;
-    uint32_t ris_lds = 0;          // stage the light table in LDS when it fits
+    uint32_t ris_lds = 1;          // stage the light table in LDS when it fits
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
     uint32_t final_blocks = 0;
     uint32_t final_lds = 1;

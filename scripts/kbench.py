@@ -20,7 +20,7 @@ import numpy as np  # noqa: E402
 
 from romis_amd import _abi, restir, scene  # noqa: E402
 
-DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 0,
+DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 1,
             "spatial.xcd": 1, "final.blocks": 0, "final.lds": 1, "final.2d": 1}
 
 VARIANTS = {
@@ -30,7 +30,7 @@ VARIANTS = {
     "primary_2d_global": {"primary.lds": 0},
     "primary_2d_lds_p1024": {"primary.blocks": 1024},
     "primary_2d_lds_p2048": {"primary.blocks": 2048},
-    "ris_lds": {"ris.lds": 1},
+    "ris_nolds": {"ris.lds": 0},
     "ris_p2048": {"ris.blocks": 2048},
     "ris_lds_p2048": {"ris.lds": 1, "ris.blocks": 2048},
     "spatial_noxcd": {"spatial.xcd": 0},

@@ -1,0 +1,92 @@
+// Drives the C++ wrapper (include/romis_amd/restir.hpp) the way the reference's CLI drives renderRayTraced
+// (src/main.cpp:213-230): load a scene, render `frames` frames threading the previous grid, write the last
+// frame's RGB.  Used by tests/test_cpp_wrapper.py (compiled on CPU; run on the GPU box).
+//
+//   render_scene <scene.bin> <out.rgb> <width> <height> <frames> <N> <passes> <temporal>
+//
+// scene.bin (little endian): u32 num_meshes; per mesh: u32 V, u32 T, f32[3V] positions, f32[3V] normals,
+// u32[3T] triangles, f32[8] material (kd3 ks3 shininess transparency); u32 num_lights, restir_light[L];
+// f32[10] camera (fovy aspect lookAt3 distance rotation3).
+#include <romis_amd/restir.hpp>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+template <class T>
+static void rd(FILE* f, T* p, size_t n) {
+    if (n && std::fread(p, sizeof(T), n, f) != n) { std::fprintf(stderr, "short read\n"); std::exit(2); }
+}
+
+int main(int argc, char** argv) {
+    if (argc < 9) { std::fprintf(stderr, "usage: %s scene.bin out.rgb W H frames N passes temporal\n", argv[0]); return 2; }
+    const int W = std::atoi(argv[3]), H = std::atoi(argv[4]), frames = std::atoi(argv[5]);
+    FILE* f = std::fopen(argv[1], "rb");
+    if (!f) { std::perror("scene"); return 2; }
+    romis::Scene scene;
+    uint32_t nm = 0;
+    rd(f, &nm, 1);
+    scene.meshes.resize(nm);
+    for (auto& m : scene.meshes) {
+        uint32_t V = 0, T = 0;
+        rd(f, &V, 1);
+        rd(f, &T, 1);
+        m.positions.resize(3 * size_t(V));
+        m.normals.resize(3 * size_t(V));
+        m.triangles.resize(3 * size_t(T));
+        rd(f, m.positions.data(), m.positions.size());
+        rd(f, m.normals.data(), m.normals.size());
+        rd(f, m.triangles.data(), m.triangles.size());
+        float mat[8];
+        rd(f, mat, 8);
+        std::memcpy(m.material.kd, mat, 12);
+        std::memcpy(m.material.ks, mat + 3, 12);
+        m.material.shininess = mat[6];
+        m.material.transparency = mat[7];
+    }
+    uint32_t nl = 0;
+    rd(f, &nl, 1);
+    scene.lights.resize(nl);
+    rd(f, scene.lights.data(), nl);
+    float cam[10];
+    rd(f, cam, 10);
+    std::fclose(f);
+
+    romis::Camera camera;
+    camera.fovy = cam[0];
+    camera.aspect = cam[1];
+    std::memcpy(camera.look_at, cam + 2, 12);
+    camera.distance = cam[5];
+    std::memcpy(camera.rotation, cam + 6, 12);
+
+    romis::Features features;
+    features.num_samples_in_reservoir = uint32_t(std::atoi(argv[6]));
+    features.spatial_resampling_passes = uint32_t(std::atoi(argv[7]));
+    features.temporal_reuse = uint8_t(std::atoi(argv[8]));
+
+    try {
+        romis::Renderer renderer(0);
+        renderer.setScene(scene);
+        renderer.setSeed(RESTIR_DEFAULT_SEED, 0);
+        romis::Screen screen(W, H);
+        std::shared_ptr<romis::ReservoirGrid> prev;
+        for (int i = 0; i < frames; i++) prev = romis::renderRayTraced(renderer, prev, camera, screen, features);
+        FILE* o = std::fopen(argv[2], "wb");
+        std::fwrite(screen.rgb.data(), sizeof(float), screen.rgb.size(), o);
+        std::fclose(o);
+        // the reference's error convention: unsupported modes throw
+        romis::Features bad = features;
+        bad.ray_trace_mode = RESTIR_MODE_ROMIS;
+        try {
+            romis::renderRayTraced(renderer, prev, camera, screen, bad);
+            std::fprintf(stderr, "expected an exception\n");
+            return 1;
+        } catch (const std::runtime_error&) {
+        }
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "error: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

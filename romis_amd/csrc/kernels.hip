@@ -167,6 +167,7 @@ __device__ __forceinline__ bool visible(const Bvh& b, v3 P, v3 y) {
 struct Px {
     v3 P, N, V;
     float t;
+    uint32_t mat;
     float4 kd_sh;   // kd.xyz, shininess
     float4 ks_pm;   // ks.xyz, bits(pow mode)
     float4 pw;      // (underflow threshold, bits(integer exponent), transparency, 0)
@@ -178,6 +179,7 @@ __device__ __forceinline__ Px make_px(const SceneDev& s, float4 a, float4 b, v3 
     r.P = xyz(b);
     uint32_t m = __float_as_uint(b.w);
     if (m >= s.num_materials) m = s.num_materials - 1;
+    r.mat = m;
     r.kd_sh = s.materials[3 * m];
     r.ks_pm = s.materials[3 * m + 1];
     r.pw = s.materials[3 * m + 2];
@@ -456,7 +458,13 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
             Px px = load_px(s, n_t, p_mat, p, origin);
             const uint32_t ps = pix_state(key, y * rg.W + x);
             for (uint32_t j = 0; j < N; j++) r[j].M = 0u;
-            for (uint32_t c = 0; c < f.M; c++) {
+            // A primary-ray miss carries the value-initialised HitInfo (kd = ks = 0, N = 0): its target pdf is
+            // exactly 0 for every finite light sample, so all M updates add w = 0 to sub-reservoir
+            // 0 (the argmin over equal wSums), none is accepted and W = 0 -- the loop's result is known.
+            const uint32_t c_end = (px.mat == s.num_materials - 1 && s.lights_finite && !__builtin_isnan(px.P.x + px.P.y + px.P.z))
+                                       ? 0u : f.M;
+            if (c_end == 0u) r[0].M = f.M;
+            for (uint32_t c = 0; c < c_end; c++) {
                 const float4* lt = lights + 7u * uniform_index(draw(ps, 4u * c), L);
                 float4 l0 = lt[0];
                 uint32_t type = __float_as_uint(l0.w);

@@ -519,6 +519,9 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
     s.light_types = types;
     // w = p / (1/L) (light.cpp:80) equals p * L exactly when 1/L is a power of two
     s.light_scale = (num_lights && (num_lights & (num_lights - 1)) == 0) ? (float)num_lights : 0.0f;
+    s.lights_finite = 1u;
+    for (uint32_t i = 0; i < 28 * num_lights; i++)
+        if (!std::isfinite(lt[i]) && (i % 4) != 3) s.lights_finite = 0u;
     c->has_scene = true;
     return RESTIR_OK;
 }

@@ -25,6 +25,7 @@ DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks"
 
 VARIANTS = {
     "default": {},
+    "feat_no_tonemap": {"@enable_tone_mapping": 0},
     "primary_1d_global": {"primary.2d": 0, "primary.lds": 0},
     "primary_1d_lds": {"primary.2d": 0},
     "primary_2d_global": {"primary.lds": 0},
@@ -59,18 +60,23 @@ def main():
     samples = {v: {k: [] for k in _abi.KERNEL_NAMES} for v in VARIANTS}
     for rnd in range(args.rounds):
         for name, knobs in VARIANTS.items():
+            fv = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=1, temporal_reuse=0)
             for k, v in {**DEFAULTS, **knobs}.items():
-                r.set_tuning(k, v)
+                if k.startswith("@"):          # a Features override (changes results: not image-checked)
+                    setattr(fv, k[1:], v)
+                else:
+                    r.set_tuning(k, v)
             r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
-            rgb, _ = r.render_restir(None, cam, W, H, f, want_grid=False)   # warm + result check
+            rgb, _ = r.render_restir(None, cam, W, H, fv, want_grid=False)   # warm + result check
             if ref_rgb is None:
                 ref_rgb = rgb
-            elif not np.array_equal(rgb.view(np.uint32), ref_rgb.view(np.uint32)):
+            elif not any(k.startswith("@") for k in knobs) and not np.array_equal(rgb.view(np.uint32),
+                                                                                ref_rgb.view(np.uint32)):
                 raise SystemExit(f"variant {name} changed the image")
             r.reset_timings()
             r.enable_timing(True)
             for _ in range(args.frames):
-                r.render_restir(None, cam, W, H, f, want_rgb=False, want_grid=False)
+                r.render_restir(None, cam, W, H, fv, want_rgb=False, want_grid=False)
             r.synchronize()
             r.enable_timing(False)
             for k, (ms, n) in r.timings().items():

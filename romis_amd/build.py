@@ -58,9 +58,29 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if force or _stale(LIB, objs):
         cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fno-gpu-rdc", "-o", LIB] + objs
         subprocess.check_call(cmd)
+    tool = os.path.join(OUT, "tools", "fastmath_check")
+    src = os.path.join(ROOT, "tests", "hip", "fastmath_check.hip")
+    if os.path.exists(src) and (force or _stale(tool, [src, os.path.join(CSRC, "device_math.h"), __file__])):
+        os.makedirs(os.path.dirname(tool), exist_ok=True)
+        subprocess.check_call([HIPCC] + COMMON + DEVICE + ["-x", "hip", src, "-o", tool])
     if verbose:
         print(LIB)
     return LIB
+
+
+def build_variant(name: str, defines: list[str]) -> str:
+    """Build _build/variants/<name>/libromis_amd.so with kernels.hip compiled under extra -D defines (the
+    ablation study, scripts/ablate.py).  The host objects are the shipped ones."""
+    build()
+    vdir = os.path.join(OUT, "variants", name)
+    os.makedirs(vdir, exist_ok=True)
+    obj = os.path.join(vdir, "kernels.hip.o")
+    subprocess.check_call([HIPCC] + COMMON + SOURCES[0][1] + [f"-D{d}" for d in defines] +
+                          ["-c", os.path.join(CSRC, "kernels.hip"), "-o", obj])
+    lib = os.path.join(vdir, "libromis_amd.so")
+    objs = [obj] + [os.path.join(OUT, s + ".o") for s, _ in SOURCES[1:]]
+    subprocess.check_call([HIPCC, "-shared", f"--offload-arch={ARCH}", "-fno-gpu-rdc", "-o", lib] + objs)
+    return lib
 
 
 def main(argv=None) -> int:

@@ -12,18 +12,80 @@ namespace romis {
 
 struct v3 { float x, y, z; };
 
+// ---- exact fast forms of the correctly rounded f32 sqrt / reciprocal / division ---------------------------
+// Each returns bit for bit what the IEEE operation returns, on the input range its guard states; callers take
+// the library expansion for lanes outside it.  tests/hip/fastmath_check.hip checks them exhaustively (sqrt,
+// reciprocal: every float) and on 2^32 random + edge operand pairs (division); DESIGN.md §4 has the proofs.
+//
+// sqrt: the compiler's own correctly rounded expansion for -fhip-fp32-correctly-rounded-divide-sqrt
+// (v_sqrt_f32, then pick s-1ulp / s / s+1ulp by the sign of the fma residuals) without its denormal rescaling
+// and +-0 / inf fix-ups, which are identities for q in [2^-96, FLT_MAX].
+__device__ __forceinline__ bool sqrt_fast_ok(float q) { return q >= 0x1p-96f && q <= 3.402823466e+38F; }
+__device__ __forceinline__ float sqrt_rn_core(float q) {
+    const float s = __builtin_amdgcn_sqrtf(q);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rm = __builtin_fmaf(-sm, s, q), rp = __builtin_fmaf(-sp, s, q);
+    float r = (rm <= 0.0f) ? sm : s;
+    return (rp > 0.0f) ? sp : r;
+}
+// reciprocal: v_rcp_f32 (< 1 ulp) + one Newton step with exact fma residual (Markstein); the exhaustive check
+// pins it to 1.0f / b for every |b| in [2^-125, 2^125].
+__device__ __forceinline__ bool rcp_fast_ok(float b) { const float a = fabsf(b); return a >= 0x1p-125f && a <= 0x1p125f; }
+__device__ __forceinline__ float rcp_rn_core(float b) {
+    const float y = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, y, 1.0f), y, y);
+}
+// division by a shared denominator: RN32(a / b) == RN32(a * R) with R ~ 1/b in double to 2^-51 relative,
+// because a/b of two floats stays >= 2^-49 relative away from every f32 rounding boundary (proof in DESIGN.md).
+__device__ __forceinline__ bool div_fast_ok(float b) { const float a = fabsf(b); return a >= 0x1p-120f && a <= 0x1p120f; }
+__device__ __forceinline__ double rcp_d(float b) {
+    const double d = (double)b;
+    double y = __builtin_amdgcn_rcp(d);
+    y = __builtin_fma(__builtin_fma(-d, y, 1.0), y, y);
+    return __builtin_fma(__builtin_fma(-d, y, 1.0), y, y);
+}
+__device__ __forceinline__ float div_by_rcp_d(float a, double r) { return (float)((double)a * r); }
+
+__device__ __forceinline__ float sqrt_rn(float q) {
+    float s = sqrt_rn_core(q);
+    if (__builtin_expect(!sqrt_fast_ok(q), 0)) s = sqrtf(q);
+    return s;
+}
+__device__ __forceinline__ float rcp_rn(float b) {
+    float y = rcp_rn_core(b);
+    if (__builtin_expect(!rcp_fast_ok(b), 0)) y = 1.0f / b;
+    return y;
+}
+
 __device__ __host__ __forceinline__ v3 mk(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
 __device__ __forceinline__ v3 vadd(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ v3 vsub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ v3 vmul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ v3 vscale(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
-__device__ __forceinline__ v3 vdivs(v3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+// v / s componentwise: one double reciprocal shared by the three quotients (exact, see div_by_rcp_d)
+__device__ __forceinline__ v3 vdivs(v3 a, float s) {
+    if (__builtin_expect(div_fast_ok(s), 1)) {
+        const double r = rcp_d(s);
+        return mk(div_by_rcp_d(a.x, r), div_by_rcp_d(a.y, r), div_by_rcp_d(a.z, r));
+    }
+    return mk(a.x / s, a.y / s, a.z / s);
+}
+
 // glm compute_dot<vec3> (func_geometric.inl:48-54): (x*x' + y*y') + z*z'
 __device__ __forceinline__ float vdot(v3 a, v3 b) { v3 t = vmul(a, b); return (t.x + t.y) + t.z; }
-__device__ __forceinline__ float vlength(v3 a) { return sqrtf(vdot(a, a)); }
+__device__ __forceinline__ float vlength(v3 a) { return sqrt_rn(vdot(a, a)); }
 __device__ __forceinline__ float vdistance(v3 p0, v3 p1) { return vlength(vsub(p1, p0)); }
-// glm normalize = v * (1 / sqrt(dot(v, v))) (func_geometric.inl:82-88)
-__device__ __forceinline__ v3 vnormalize(v3 a) { return vscale(a, 1.0f / sqrtf(vdot(a, a))); }
+// glm normalize = v * (1 / sqrt(dot(v, v))) (func_geometric.inl:82-88); also hands back sqrt(dot(v, v)),
+// which is glm::length(v) / glm::distance bit for bit.  One guard covers both fast forms: q in the sqrt range
+// puts sqrt(q) in [2^-48, 2^64], inside the reciprocal's.
+__device__ __forceinline__ v3 vnormalize_len(v3 a, float& len) {
+    const float q = vdot(a, a);
+    float s = sqrt_rn_core(q), y = rcp_rn_core(s);
+    if (__builtin_expect(!sqrt_fast_ok(q), 0)) { s = sqrtf(q); y = 1.0f / s; }
+    len = s;
+    return vscale(a, y);
+}
+__device__ __forceinline__ v3 vnormalize(v3 a) { float l; return vnormalize_len(a, l); }
 // glm mix = x * (1 - a) + y * a (func_common.inl:104-111)
 __device__ __forceinline__ v3 vmix(v3 x, v3 y, float a) { return vadd(vscale(x, 1.0f - a), vscale(y, a)); }
 __device__ __forceinline__ v3 vcross(v3 x, v3 y) {
@@ -47,7 +109,11 @@ __device__ __host__ __forceinline__ uint32_t mix32(uint32_t h) {
 __device__ __host__ __forceinline__ uint32_t pix_state(uint32_t key, uint32_t g) {
     return mix32(key ^ mix32(g * 0x9E3779B1u + 0x7F4A7C15u));
 }
+#if defined(ROMIS_ABL_RNG)
+__device__ __host__ __forceinline__ uint32_t draw(uint32_t ps, uint32_t slot) { uint32_t h = ps + slot * 0x9E3779B9u; return h ^ (h >> 15); }
+#else
 __device__ __host__ __forceinline__ uint32_t draw(uint32_t ps, uint32_t slot) { return mix32(ps + slot * 0x9E3779B9u); }
+#endif
 // rand() + linearMap(float(rand()), 0, RAND_MAX, 0, 1) (utils.cpp:26-31): exact (power-of-two scale)
 __device__ __forceinline__ float rand01(uint32_t d) {
     float val = (float)(d >> 1);

@@ -192,10 +192,34 @@ __device__ __forceinline__ Px load_px(const SceneDev& s, const float4* __restric
     return make_px(s, n_t[p], p_mat[p], origin);
 }
 
+// |x|^n (n >= 1) by binary powering in double: exactly the product sequence of pm_powf's integer branch
+// (oracle/portable_math.h: acc = 1, acc *= base at each set bit, base squared between bits), started at the
+// lowest set bit since 1 * base == base.  With a wave-uniform n the bit tests are scalar branches (the empty
+// volatile asm keeps the compiler from turning them into per-lane selects), leaving only the f64 multiplies.
+template <bool UNIFORM>
+__device__ __forceinline__ double pow_int_chain(double base, uint32_t k) {
+    if (k == 0u) return 1.0;
+    while (!(k & 1u)) { base = base * base; k >>= 1; }
+    double acc = base;
+    k >>= 1;
+    while (k) {
+        base = base * base;
+        if (k & 1u) {
+            if (UNIFORM) asm volatile("");
+            acc = acc * base;
+        }
+        k >>= 1;
+    }
+    return acc;
+}
+
 // std::pow(cosTheta, shininess) (shading.cpp:26) specialised per material; every branch returns exactly what
 // pm_powf(x, shininess) returns (or, for ks == 0, a value whose product with ks is the same +-0 the reference
 // gets after its NaN clean-up -- see DESIGN.md "Floating point").
 __device__ __forceinline__ float material_pow(float x, const Px& px) {
+#if defined(ROMIS_ABL_POW)
+    return x * px.kd_sh.w;
+#endif
     const uint32_t mode = __float_as_uint(px.ks_pm.w);
     if (mode == ROMIS_POW_SKIP) return 1.0f;
     if (mode == ROMIS_POW_INT) {
@@ -203,13 +227,10 @@ __device__ __forceinline__ float material_pow(float x, const Px& px) {
         const float ax = fabsf(x);
         if (ax < px.pw.x) return (__builtin_signbit(x) && (n & 1u)) ? -0.0f : 0.0f;   // |x|^n < 2^-151: underflow
         if (ax <= 3.402823466e+38F) {
-            double base = (double)ax, acc = 1.0;
-            uint32_t k = n;
-            while (k) {
-                if (k & 1u) acc = acc * base;
-                k >>= 1;
-                if (k) base = base * base;
-            }
+            // the same multiplication chain either way; a wave whose lanes share the exponent (one material)
+            // runs it under scalar loop control instead of a per-lane divergent loop
+            const uint32_t n0 = __builtin_amdgcn_readfirstlane(n);
+            const double acc = __all(n == n0) ? pow_int_chain<true>((double)ax, n0) : pow_int_chain<false>((double)ax, n);
             const double sign = (x < 0.0f && (n & 1u)) ? -1.0 : 1.0;
             return (float)(sign * acc);
         }
@@ -218,25 +239,34 @@ __device__ __forceinline__ float material_pow(float x, const Px& px) {
 }
 
 // computeShading (shading.cpp:7-34)
-__device__ __forceinline__ v3 shade(const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
+__device__ __forceinline__ v3 shade(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
     v3 kd = xyz(px.kd_sh);
     if (!f.shading) return kd;
-    v3 L = vnormalize(vsub(lpos, px.P));
+    float d;   // glm::distance(hitPos, lightPos) == |lightPos - hitPos|, the length normalize() takes
+    v3 L = vnormalize_len(vsub(lpos, px.P), d);
     float dotNL = vdot(px.N, L);
     if (dotNL < 0.0f) return mk(0.0f, 0.0f, 0.0f);
     v3 R = vnormalize(vsub(vscale(px.N, 2.0f * dotNL), L));
     float cosTheta = vdot(R, px.V);
+    const float pw = material_pow(cosTheta, px);
     v3 diffuse = vscale(vmul(lcol, kd), dotNL);
-    v3 specular = vscale(vmul(lcol, xyz(px.ks_pm)), material_pow(cosTheta, px));
-    if (vany_nan(diffuse)) diffuse = mk(0.0f, 0.0f, 0.0f);
-    if (vany_nan(specular)) specular = mk(0.0f, 0.0f, 0.0f);
-    float d = vdistance(px.P, lpos);
+    v3 specular = vscale(vmul(lcol, xyz(px.ks_pm)), pw);
+    // The reference zeroes a term holding a NaN.  When every colour x reflectance product is finite (host
+    // check, SceneDev::shade_finite), a term can only hold one through a non-finite dotNL / pow factor, so
+    // the six per-component tests run only for lanes where one of those two is non-finite.
+    if (!(s.shade_finite && __builtin_isfinite(dotNL) && __builtin_isfinite(pw))) {
+        if (vany_nan(diffuse)) diffuse = mk(0.0f, 0.0f, 0.0f);
+        if (vany_nan(specular)) specular = mk(0.0f, 0.0f, 0.0f);
+    }
     if (fabsf(d) < 1e-5f) d = 1.0f;
     return vdivs(vadd(diffuse, specular), d * d);
 }
 
-__device__ __forceinline__ float target_pdf(const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
-    return vlength(shade(f, px, lpos, lcol));
+__device__ __forceinline__ float target_pdf(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
+#if defined(ROMIS_ABL_SHADE)
+    return fabsf(vdot(vsub(lpos, px.P), px.N)) * (lcol.x + lcol.y);
+#endif
+    return vlength(shade(s, f, px, lpos, lcol));
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -484,13 +514,13 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
                     v3 l23 = vmix(xyz(lt[5]), xyz(lt[6]), a);
                     col = vmix(l01, l23, b);
                 }
-                const float pd = target_pdf(f, px, pos, col);
+                const float pd = target_pdf(s, f, px, pos, col);
                 const float w = s.light_scale != 0.0f ? pd * s.light_scale : pd / invL;   // light.cpp:80
                 res_update<NT>(r, N, pos, col, w, rand01(draw(ps, 4u * c + 3u)), pd);
             }
             for (uint32_t j = 0; j < N; j++) {
                 if (f.initial_vis && !visible(bvh, px.P, r[j].pos)) r[j].W = 0.0f;
-                else r[j].W = contribution_weight(r[j].has_pd ? r[j].pd : target_pdf(f, px, r[j].pos, r[j].col), r[j].M,
+                else r[j].W = contribution_weight(r[j].has_pd ? r[j].pd : target_pdf(s, f, px, r[j].pos, r[j].col), r[j].M,
                                                   r[j].wsum);
             }
         }
@@ -527,17 +557,17 @@ struct Combiner {
         t = 0;
     }
     // combine one input sub-reservoir (reservoir.cpp:47-54 / :75-82)
-    __device__ __forceinline__ void consume(const FeaturesDev& f, const Px& cur, const Sub& in, uint32_t ps, uint32_t slot0) {
-        float pd = target_pdf(f, cur, in.pos, in.col);
+    __device__ __forceinline__ void consume(const SceneDev& s, const FeaturesDev& f, const Px& cur, const Sub& in, uint32_t ps, uint32_t slot0) {
+        float pd = target_pdf(s, f, cur, in.pos, in.col);
         float w = (pd * in.W) * (float)in.M;
         uint32_t k = res_update<NT>(out, n(), in.pos, in.col, w, rand01(draw(ps, slot0 + t)), pd);
         t++;
         macc_add<NT>(macc, k, in.M);
     }
-    __device__ __forceinline__ void finish_biased(const FeaturesDev& f, const Px& cur) {
+    __device__ __forceinline__ void finish_biased(const SceneDev& s, const FeaturesDev& f, const Px& cur) {
         for (uint32_t j = 0; j < n(); j++) out[j].M = macc[j];
         for (uint32_t j = 0; j < n(); j++)
-            out[j].W = contribution_weight(out[j].has_pd ? out[j].pd : target_pdf(f, cur, out[j].pos, out[j].col),
+            out[j].W = contribution_weight(out[j].has_pd ? out[j].pd : target_pdf(s, f, cur, out[j].pos, out[j].col),
                                            out[j].M, out[j].wsum);
     }
 };
@@ -570,9 +600,9 @@ __device__ __forceinline__ void temporal_body(const SceneDev& s, const Region& r
     const uint32_t ps = pix_state(key, y * rg.W + x);
     Combiner<NT> cmb;
     cmb.init(N);
-    for (uint32_t j = 0; j < N; j++) cmb.consume(f, px, cur[j], ps, 0u);
-    for (uint32_t j = 0; j < N; j++) cmb.consume(f, px, prev[j], ps, 0u);
-    cmb.finish_biased(f, px);
+    for (uint32_t j = 0; j < N; j++) cmb.consume(s, f, px, cur[j], ps, 0u);
+    for (uint32_t j = 0; j < N; j++) cmb.consume(s, f, px, prev[j], ps, 0u);
+    cmb.finish_biased(s, f, px);
     for (uint32_t j = 0; j < N; j++) sub_store(cmb.out[j], oa, ob, odbg, j * npx + p);
 }
 
@@ -592,7 +622,10 @@ ROMIS_TEMPORAL_KERNEL(0)
 // order, current last -- render_utils.cpp:108-124), so no per-lane candidate list is kept.  The neighbour
 // draws do not depend on data, so the loads of a batch of kBatch neighbours are all issued before the first
 // is consumed (one memory latency per batch instead of a dependent chain per neighbour).
-constexpr uint32_t kBatch = 5;
+#ifndef ROMIS_SPATIAL_BATCH
+#define ROMIS_SPATIAL_BATCH 5
+#endif
+constexpr uint32_t kBatch = ROMIS_SPATIAL_BATCH;
 
 template <int NT, bool UNBIASED>
 __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
@@ -618,7 +651,11 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
         for (uint32_t i = 0; i < kBatch; i++) {
             const uint32_t n = n0 + i;
             q[i] = (uint32_t)p;
+#if defined(ROMIS_ABL_SPATIAL_SELF)
+            if (n < K && draw(ps, 2u * n) == 0x12345u)
+#else
             if (n < K)
+#endif
                 q[i] = (uint32_t)neighbour_index(rg, x, y, uniform_offset(draw(ps, 2u * n), f.R),
                                        uniform_offset(draw(ps, 2u * n + 1u), f.R));
         }
@@ -645,7 +682,7 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
             // step (static indices only; a rolled loop over a[i] would spill the batch to memory)
 #pragma unroll 1
             for (uint32_t i = 0; i < kBatch; i++) {
-                if (ok[0]) cmb.consume(f, cur, sub_from(a[0], b[0]), ps, slot0);
+                if (ok[0]) cmb.consume(s, f, cur, sub_from(a[0], b[0]), ps, slot0);
 #pragma unroll
                 for (uint32_t j = 0; j + 1 < kBatch; j++) { a[j] = a[j + 1]; b[j] = b[j + 1]; ok[j] = ok[j + 1]; }
             }
@@ -656,7 +693,7 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
                 for (uint32_t j = 0; j < N; j++) {
                     Sub in;
                     sub_load(in, ia, ib, j * npx + q[i]);
-                    cmb.consume(f, cur, in, ps, slot0);
+                    cmb.consume(s, f, cur, in, ps, slot0);
                 }
             }
         }
@@ -664,10 +701,10 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
     for (uint32_t j = 0; j < N; j++) {
         Sub in;
         sub_load(in, ia, ib, j * npx + p);
-        cmb.consume(f, cur, in, ps, slot0);
+        cmb.consume(s, f, cur, in, ps, slot0);
     }
     if (!UNBIASED) {
-        cmb.finish_biased(f, cur);
+        cmb.finish_biased(s, f, cur);
     } else {
         // combineUnbiased (reservoir.cpp:84-103): Z_j = sum over the stream of the input's total M where
         // p_r(y_j) [* vis_r(y_j)] > 0.  The stream is re-derived from the same draws (no rejection here).
@@ -683,13 +720,13 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
             unsigned long long tot = 0;
             for (uint32_t j = 0; j < N; j++) tot += __float_as_uint(ib[j * npx + q].w);
             for (uint32_t j = 0; j < N; j++) {
-                float pd = target_pdf(f, rp, cmb.out[j].pos, cmb.out[j].col);
+                float pd = target_pdf(s, f, rp, cmb.out[j].pos, cmb.out[j].col);
                 if (f.spatial_vis) pd *= visible(bvh, rp.P, cmb.out[j].pos) ? 1.0f : 0.0f;
                 if (pd > 0.0f) Z[j] += tot;
             }
         }
         for (uint32_t j = 0; j < N; j++) {
-            float pc = cmb.out[j].has_pd ? cmb.out[j].pd : target_pdf(f, cur, cmb.out[j].pos, cmb.out[j].col);
+            float pc = cmb.out[j].has_pd ? cmb.out[j].pd : target_pdf(s, f, cur, cmb.out[j].pos, cmb.out[j].col);
             if (pc == 0.0f || Z[j] == 0ull) cmb.out[j].W = 0.0f;
             else cmb.out[j].W = ((1.0f / pc) * (1.0f / (float)Z[j])) * cmb.out[j].wsum;
         }
@@ -697,8 +734,13 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
     for (uint32_t j = 0; j < N; j++) sub_store(cmb.out[j], oa, ob, odbg, j * npx + p);
 }
 
+#ifdef ROMIS_SPATIAL_WPE
+#define ROMIS_SPATIAL_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL_WPE)))
+#else
+#define ROMIS_SPATIAL_ATTR
+#endif
 #define ROMIS_SPATIAL_KERNEL(NT, UB, NAME)                                                                             \
-    extern "C" __global__ __launch_bounds__(256) void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
+    extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,    \
                                                           const float4* ia, const float4* ib, float4* oa, float4* ob,   \
                                                           float2* odbg) {                                               \
@@ -733,7 +775,7 @@ __device__ __forceinline__ void final_body(const SceneDev& s, const Region& rg, 
         for (uint32_t j = 0; j < N; j++) {
             Sub r;
             sub_load(r, ra, rb, j * npx + p);
-            v3 sc = shade(f, px, r.pos, r.col);
+            v3 sc = shade(s, f, px, r.pos, r.col);
             // The visibility test can only matter when the shaded value is non-zero: (vis ? sc : 0) * W equals
             // sc * W when sc == 0 (both are 0 * W), so the shadow ray is skipped exactly then.
             if ((sc.x != 0.0f || sc.y != 0.0f || sc.z != 0.0f) && !visible(bvh, px.P, r.pos)) sc = mk(0.0f, 0.0f, 0.0f);

@@ -522,6 +522,26 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
     s.lights_finite = 1u;
     for (uint32_t i = 0; i < 28 * num_lights; i++)
         if (!std::isfinite(lt[i]) && (i % 4) != 3) s.lights_finite = 0u;
+    // every product colour x kd / colour x ks stays finite (with a margin for the mix() rounding of segment /
+    // parallelogram colours): shade() may then skip its per-component NaN tests for finite dotNL and pow
+    {
+        double cmax = 0.0, kmax = 0.0;
+        bool finite = true;
+        for (uint32_t i = 0; i < num_lights; i++)
+            for (int r = 3; r < 7; r++)
+                for (int a = 0; a < 3; a++) {
+                    const float v = lt[28 * i + 4 * r + a];
+                    finite = finite && std::isfinite(v);
+                    cmax = std::max(cmax, (double)std::fabs(v));
+                }
+        for (uint32_t m = 0; m <= num_meshes; m++)
+            for (int a : {0, 1, 2, 4, 5, 6}) {
+                const float v = mats[12 * m + a];
+                finite = finite && std::isfinite(v);
+                kmax = std::max(kmax, (double)std::fabs(v));
+            }
+        s.shade_finite = (finite && cmax * kmax <= 0x1p120) ? 1u : 0u;
+    }
     c->has_scene = true;
     return RESTIR_OK;
 }

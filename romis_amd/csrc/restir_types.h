@@ -42,6 +42,7 @@ struct SceneDev {
     uint32_t light_types;      // bit t set <=> a light of type t is present
     float light_scale;         // L when 1/L is a power of two (then p / (1/L) == p * L exactly), else 0
     uint32_t lights_finite;    // every light coordinate / colour is finite
+    uint32_t shade_finite;     // every light colour x material kd / ks product is finite (shade()'s NaN tests)
 };
 
 // Image region bookkeeping: global image W x H (y = 0 bottom), storage view (the computed region, row-major)

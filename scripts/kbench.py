@@ -50,16 +50,18 @@ def main():
     ap.add_argument("--scene", default="nightclub_128pt")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--only", nargs="*", help="run only these variants")
     args = ap.parse_args()
+    variants = {k: v for k, v in VARIANTS.items() if not args.only or k in args.only}
     W, H = args.width, args.height
     r = restir.Renderer(0)
     r.set_scene(scene.bench_scene(args.scene))
     cam = scene.camera_for(args.scene, W, H)
     f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=1, temporal_reuse=0)
     ref_rgb = None
-    samples = {v: {k: [] for k in _abi.KERNEL_NAMES} for v in VARIANTS}
+    samples = {v: {k: [] for k in _abi.KERNEL_NAMES} for v in variants}
     for rnd in range(args.rounds):
-        for name, knobs in VARIANTS.items():
+        for name, knobs in variants.items():
             fv = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=1, temporal_reuse=0)
             for k, v in {**DEFAULTS, **knobs}.items():
                 if k.startswith("@"):          # a Features override (changes results: not image-checked)

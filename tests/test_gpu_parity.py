@@ -108,6 +108,55 @@ def test_ris_variants_bit_exact(gpu, oracle, variant):
     assert_bits(gpu.download(_abi.BUF_RES_B), b, "res_b")
 
 
+def _extreme_scene(variant):
+    """Scenes that push shade() off its fast forms: colour x reflectance products past 2^120 (per-component NaN
+    tests, overflowing sums), lights so far that |L|^2 overflows (sqrt / reciprocal guards), and per-mesh
+    shininess mixing integer exponents (non-uniform pow chains) with non-integer ones (general pow)."""
+    import copy
+    base = get_scene("nightclub_128pt")
+    meshes = [copy.copy(m) for m in base.meshes]
+    lights = [copy.copy(l) for l in base.lights]
+    if variant == "huge_colour":
+        for i, l in enumerate(lights):
+            for a in range(3):
+                l.c0[a] = 3.0e38 if i % 3 == 0 else l.c0[a] * 1e30
+    elif variant == "far_lights":
+        for i, l in enumerate(lights):
+            if i % 2 == 0:
+                for a in range(3):
+                    l.p0[a] = l.p0[a] * (1e19 if i % 4 == 0 else 1e-19)
+    elif variant == "mixed_shininess":
+        shin = [250.0, 37.0, 1.0, 2.5, 1048576.0, 3.0, 64.0, 0.5, 17.0, 250.0]
+        for i, m in enumerate(meshes):
+            m.shininess = np.float32(shin[i % len(shin)])
+            m.ks = np.asarray([0.5, 0.25, 0.125], np.float32)
+    return scene.Scene(meshes, lights, "extreme_" + variant)
+
+
+@pytest.mark.parametrize("variant", ["huge_colour", "far_lights", "mixed_shininess"])
+def test_ris_and_spatial_extreme_scenes_bit_exact(gpu, oracle, variant):
+    s = _extreme_scene(variant)
+    gpu.set_scene(s)
+    osc = oracle.OracleScene(s)
+    cam = scene.nightclub_camera(W, H)
+    N = 1
+    gpu.stage_configure(W, H, N)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    gpu.upload(_abi.BUF_GBUF_N_T, n_t)
+    gpu.upload(_abi.BUF_GBUF_P_MAT, p_mat)
+    f = _abi.default_features(num_samples_in_reservoir=N)
+    gpu.stage_ris(cam, f, key(_abi.RESTIR_STAGE_RIS))
+    a, b, d = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
+    assert_bits(gpu.download(_abi.BUF_RES_A), a, "res_a")
+    assert_bits(gpu.download(_abi.BUF_RES_B), b, "res_b")
+    assert_bits(gpu.download(_abi.BUF_RES_DBG), d, "wSum/chosen")
+    gpu.stage_spatial(cam, f, key(_abi.RESTIR_STAGE_SPATIAL, 0))
+    a2, b2, d2 = oracle.spatial_pass(osc, f, key(_abi.RESTIR_STAGE_SPATIAL, 0), origin(oracle, cam), W, H, n_t, p_mat,
+                                     (a, b))
+    assert_bits(gpu.download(_abi.BUF_RES_A), a2, "spatial res_a")
+    assert_bits(gpu.download(_abi.BUF_RES_B), b2, "spatial res_b")
+
+
 def test_ris_no_lights(gpu, oracle):
     s = get_scene("nightclub_128pt")
     empty = scene.Scene(s.meshes, [], "dark")

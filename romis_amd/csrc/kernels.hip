@@ -238,8 +238,8 @@ __device__ __forceinline__ float material_pow(float x, const Px& px) {
     return pm_powf_general(x, px.kd_sh.w);
 }
 
-// computeShading (shading.cpp:7-34)
-__device__ __forceinline__ v3 shade(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
+// computeShading (shading.cpp:7-34), general form: every IEEE special case, any material
+__device__ __forceinline__ v3 shade_ref(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
     v3 kd = xyz(px.kd_sh);
     if (!f.shading) return kd;
     float d;   // glm::distance(hitPos, lightPos) == |lightPos - hitPos|, the length normalize() takes
@@ -262,11 +262,16 @@ __device__ __forceinline__ v3 shade(const SceneDev& s, const FeaturesDev& f, con
     return vdivs(vadd(diffuse, specular), d * d);
 }
 
+__device__ __forceinline__ v3 shade(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
+    return shade_ref(s, f, px, lpos, lcol);
+}
+
+// target pdf = glm::length(computeShading(...)) (light.cpp:84, reservoir.cpp:49)
 __device__ __forceinline__ float target_pdf(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
 #if defined(ROMIS_ABL_SHADE)
     return fabsf(vdot(vsub(lpos, px.P), px.N)) * (lcol.x + lcol.y);
 #endif
-    return vlength(shade(s, f, px, lpos, lcol));
+    return vlength(shade_ref(s, f, px, lpos, lcol));
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -494,11 +499,15 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
             const uint32_t c_end = (px.mat == s.num_materials - 1 && s.lights_finite && !__builtin_isnan(px.P.x + px.P.y + px.P.z))
                                        ? 0u : f.M;
             if (c_end == 0u) r[0].M = f.M;
-            for (uint32_t c = 0; c < c_end; c++) {
+            // candidate c: light sample (genCanonicalSamples' switch, light.cpp:55-78)
+            auto sample = [&](uint32_t c, v3& pos, v3& col) {
+#if defined(ROMIS_ABL_LIGHT0)
+                const float4* lt = lights + 7u * (draw(ps, 4u * c) == 0x12345u ? 1u : 0u);
+#else
                 const float4* lt = lights + 7u * uniform_index(draw(ps, 4u * c), L);
+#endif
                 float4 l0 = lt[0];
                 uint32_t type = __float_as_uint(l0.w);
-                v3 pos, col;
                 if (type == 0u) {
                     pos = xyz(l0);
                     col = xyz(lt[3]);
@@ -514,9 +523,26 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
                     v3 l23 = vmix(xyz(lt[5]), xyz(lt[6]), a);
                     col = vmix(l01, l23, b);
                 }
+            };
+            auto weight = [&](float pd) { return s.light_scale != 0.0f ? pd * s.light_scale : pd / invL; };  // light.cpp:80
+            uint32_t c = 0;
+#if defined(ROMIS_RIS_U2)
+            // two independent target pdfs per iteration (more ILP per wave); updates stay in candidate order
+            for (; c + 1 < c_end; c += 2) {
+                v3 pos0, col0, pos1, col1;
+                sample(c, pos0, col0);
+                sample(c + 1, pos1, col1);
+                const float pd0 = target_pdf(s, f, px, pos0, col0);
+                const float pd1 = target_pdf(s, f, px, pos1, col1);
+                res_update<NT>(r, N, pos0, col0, weight(pd0), rand01(draw(ps, 4u * c + 3u)), pd0);
+                res_update<NT>(r, N, pos1, col1, weight(pd1), rand01(draw(ps, 4u * c + 7u)), pd1);
+            }
+#endif
+            for (; c < c_end; c++) {
+                v3 pos, col;
+                sample(c, pos, col);
                 const float pd = target_pdf(s, f, px, pos, col);
-                const float w = s.light_scale != 0.0f ? pd * s.light_scale : pd / invL;   // light.cpp:80
-                res_update<NT>(r, N, pos, col, w, rand01(draw(ps, 4u * c + 3u)), pd);
+                res_update<NT>(r, N, pos, col, weight(pd), rand01(draw(ps, 4u * c + 3u)), pd);
             }
             for (uint32_t j = 0; j < N; j++) {
                 if (f.initial_vis && !visible(bvh, px.P, r[j].pos)) r[j].W = 0.0f;
@@ -528,18 +554,24 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
     }
 }
 
-#define ROMIS_RIS_KERNEL(NT, LDS, NAME)                                                                               \
-    extern "C" __global__ __launch_bounds__(256) void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
+// RIS: capped at 96 VGPRs = 5 waves per SIMD (uncapped the allocator takes 100 = 4 waves; 5 waves run the
+// latency-bound candidate loop 9 % faster, 6 waves spill -- scripts/ablate.py, profiles/r1)
+#ifndef ROMIS_RIS_WPE
+#define ROMIS_RIS_WPE 5
+#endif
+#define ROMIS_RIS_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_RIS_WPE)))
+#define ROMIS_RIS_KERNEL(NT, LDS, NAME, ATTR)                                                                         \
+    extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,   \
                                                           float4* ra, float4* rb, float2* rdbg) {                       \
         ris_body<NT, LDS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg);                                     \
     }
-ROMIS_RIS_KERNEL(1, false, k_ris_n1)
-ROMIS_RIS_KERNEL(2, false, k_ris_n2)
-ROMIS_RIS_KERNEL(0, false, k_ris_n0)
-ROMIS_RIS_KERNEL(1, true, k_ris_n1_lds)
-ROMIS_RIS_KERNEL(2, true, k_ris_n2_lds)
-ROMIS_RIS_KERNEL(0, true, k_ris_n0_lds)
+ROMIS_RIS_KERNEL(1, false, k_ris_n1, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL(2, false, k_ris_n2, )
+ROMIS_RIS_KERNEL(0, false, k_ris_n0, )
+ROMIS_RIS_KERNEL(1, true, k_ris_n1_lds, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL(2, true, k_ris_n2_lds, )
+ROMIS_RIS_KERNEL(0, true, k_ris_n0_lds, )
 
 // ---------------------------------------------------------------------------------------------------------
 // Combine state shared by temporal and spatial: out[] (Reservoir(N) of the current pixel) + routed M sums.
@@ -628,19 +660,23 @@ ROMIS_TEMPORAL_KERNEL(0)
 constexpr uint32_t kBatch = ROMIS_SPATIAL_BATCH;
 
 template <int NT, bool UNBIASED>
-__device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
-                                             v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
-                                             const float4* __restrict__ ia, const float4* __restrict__ ib,
-                                             float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg) {
-    uint32_t x, y;
-    size_t p;
-    if (!work_pixel(rg, rg.map2d ? xcd_banded_tile() : blockIdx.x, x, y, p)) return;
+__device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
+                                              v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                              const float4* __restrict__ ia, const float4* __restrict__ ib,
+                                              float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
+                                              uint32_t x, uint32_t y, size_t p) {
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
     const uint32_t K = f.K;
     const Px cur = load_px(s, n_t, p_mat, p, origin);
     const uint32_t ps = pix_state(key, y * rg.W + x);
     const uint32_t slot0 = 2u * K;
+#if defined(ROMIS_ABL_SPATIAL_COPY)
+    if (ps != 0x9E3779B9u || cur.t != 1.0f) {
+        for (uint32_t j = 0; j < N; j++) { Sub in; sub_load(in, ia, ib, j * npx + p); sub_store(in, oa, ob, odbg, j * npx + p); }
+        return;
+    }
+#endif
     Combiner<NT> cmb;
     cmb.init(N);
     for (uint32_t n0 = 0; n0 < K; n0 += kBatch) {
@@ -734,11 +770,40 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
     for (uint32_t j = 0; j < N; j++) sub_store(cmb.out[j], oa, ob, odbg, j * npx + p);
 }
 
-#ifdef ROMIS_SPATIAL_WPE
-#define ROMIS_SPATIAL_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL_WPE)))
-#else
-#define ROMIS_SPATIAL_ATTR
+template <int NT, bool UNBIASED>
+__device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
+                                             v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                             const float4* __restrict__ ia, const float4* __restrict__ ib,
+                                             float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg) {
+    const uint32_t T = work_items(rg);
+    if (!rg.map2d) {
+        for (uint32_t item = blockIdx.x; item < T; item += gridDim.x) {
+            uint32_t x, y;
+            size_t p;
+            if (work_pixel(rg, item, x, y, p))
+                spatial_pixel<NT, UNBIASED>(s, rg, f, key, origin, n_t, p_mat, ia, ib, oa, ob, odbg, x, y, p);
+        }
+        return;
+    }
+    // XCD-banded tile order (see xcd_banded_tile): the blocks of XCD b % 8 sweep that XCD's contiguous band
+    const uint32_t nb = gridDim.x, b = blockIdx.x, xcd = b % 8u;
+    const uint32_t xcd_blocks = nb / 8u + (xcd < nb % 8u ? 1u : 0u);
+    const uint32_t q = T / 8u, rem = T % 8u;
+    const uint32_t band0 = xcd * q + min(xcd, rem), band_len = q + (xcd < rem ? 1u : 0u);
+    for (uint32_t t = b / 8u; t < band_len; t += xcd_blocks) {
+        uint32_t x, y;
+        size_t p;
+        if (work_pixel(rg, band0 + t, x, y, p))
+            spatial_pixel<NT, UNBIASED>(s, rg, f, key, origin, n_t, p_mat, ia, ib, oa, ob, odbg, x, y, p);
+    }
+}
+
+// Waves per SIMD the register allocator must leave room for (VGPRs <= 512 / waves).  Spatial: without the
+// cap the allocator settles at 129 VGPRs = 3 waves; capped at 4 (128) it runs 12 % faster (ablate.py).
+#ifndef ROMIS_SPATIAL_WPE
+#define ROMIS_SPATIAL_WPE 4
 #endif
+#define ROMIS_SPATIAL_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL_WPE)))
 #define ROMIS_SPATIAL_KERNEL(NT, UB, NAME)                                                                             \
     extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,    \
@@ -882,10 +947,12 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
                           float4* ob, float2* odbg, const Tuning& tu, hipStream_t stream) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, tu.spatial_xcd);   // XCD-banded order works on 2D tiles
+    uint32_t grid = items_of(rg);
+    if (tu.spatial_blocks) grid = std::min(grid, std::max(8u, tu.spatial_blocks));
     auto k = f.unbiased ? (f.N == 1 ? k_spatial_n1_unbiased : (f.N == 2 ? k_spatial_n2_unbiased : k_spatial_n0_unbiased))
                         : (f.N == 1 ? k_spatial_n1_biased : (f.N == 2 ? k_spatial_n2_biased : k_spatial_n0_biased));
-    hipLaunchKernelGGL(k, dim3(items_of(rg)), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib,
-                       oa, ob, odbg);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa,
+                       ob, odbg);
     return hipGetLastError();
 }
 

@@ -884,6 +884,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "ris.blocks")) t.ris_blocks = v;
     else if (!std::strcmp(key, "ris.lds")) t.ris_lds = v;
     else if (!std::strcmp(key, "spatial.xcd")) t.spatial_xcd = v;
+    else if (!std::strcmp(key, "spatial.blocks")) t.spatial_blocks = v;
     else if (!std::strcmp(key, "final.blocks")) t.final_blocks = v;
     else if (!std::strcmp(key, "final.lds")) t.final_lds = v;
     else if (!std::strcmp(key, "final.2d")) t.final_2d = v;

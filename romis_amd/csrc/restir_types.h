@@ -62,6 +62,7 @@ struct Tuning {
     uint32_t ris_blocks = 0;
     uint32_t ris_lds = 1;          // stage the light table in LDS when it fits
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
+    uint32_t spatial_blocks = 0;
     uint32_t final_blocks = 0;
     uint32_t final_lds = 1;
     uint32_t final_2d = 1;

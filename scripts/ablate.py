@@ -15,16 +15,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 VARIANTS = {
-    "rng": ["ROMIS_ABL_RNG"],
-    "pow": ["ROMIS_ABL_POW"],
-    "spatial_self": ["ROMIS_ABL_SPATIAL_SELF"],
-    "spatial_b1": ["ROMIS_SPATIAL_BATCH=1"],
-    "spatial_b2": ["ROMIS_SPATIAL_BATCH=2"],
-    "spatial_b3": ["ROMIS_SPATIAL_BATCH=3"],
-    "spatial_wpe5": ["ROMIS_SPATIAL_WPE=5"],
-    "spatial_wpe6": ["ROMIS_SPATIAL_WPE=6"],
-    "spatial_wpe8": ["ROMIS_SPATIAL_WPE=8"],
-    "shade": ["ROMIS_ABL_SHADE"],
+    "rng": ["ROMIS_ABL_RNG"],                 # cheap hash instead of the keyed mix32 draws
+    "pow": ["ROMIS_ABL_POW"],                 # pow(cos, n) -> cos * n
+    "shade": ["ROMIS_ABL_SHADE"],             # target pdf -> one dot product
+    "light0": ["ROMIS_ABL_LIGHT0"],           # every candidate reads light 0 (no LDS bank conflicts)
+    "spatial_self": ["ROMIS_ABL_SPATIAL_SELF"],  # spatial neighbours = the pixel itself (no gathers)
+    "spatial_copy": ["ROMIS_ABL_SPATIAL_COPY"],  # spatial = copy own reservoir (memory floor)
+    "ris_u2": ["ROMIS_RIS_U2"],               # two target pdfs per candidate-loop iteration
+    "ris_wpe4": ["ROMIS_RIS_WPE=4"],
+    "spatial_wpe3": ["ROMIS_SPATIAL_WPE=3"],
 }
 
 

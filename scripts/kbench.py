@@ -21,7 +21,7 @@ import numpy as np  # noqa: E402
 from romis_amd import _abi, restir, scene  # noqa: E402
 
 DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 1,
-            "spatial.xcd": 1, "final.blocks": 0, "final.lds": 1, "final.2d": 1}
+            "spatial.xcd": 1, "spatial.blocks": 0, "final.blocks": 0, "final.lds": 1, "final.2d": 1}
 
 VARIANTS = {
     "default": {},
@@ -35,6 +35,9 @@ VARIANTS = {
     "ris_p2048": {"ris.blocks": 2048},
     "ris_lds_p2048": {"ris.lds": 1, "ris.blocks": 2048},
     "spatial_noxcd": {"spatial.xcd": 0},
+    "spatial_p1024": {"spatial.blocks": 1024},
+    "spatial_p2048": {"spatial.blocks": 2048},
+    "spatial_p4096": {"spatial.blocks": 4096},
     "final_1d_global": {"final.2d": 0, "final.lds": 0},
     "final_1d_lds": {"final.2d": 0},
     "final_2d_global": {"final.lds": 0},

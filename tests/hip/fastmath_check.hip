@@ -78,6 +78,10 @@ __global__ void k_div_edges(Counters* c) {
     if (t >= na * nb) return;
     const float a = as[t / nb], b = bs[t % nb];
     const float q = div_by_rcp_d(a, rcp_d(b)), r = a / b;
+    if (t == 0) {   // sqrt_rn_core(+0) == +0: target_pdf takes the core form for q == 0 as well
+        atomicAdd(&c->checked[0], 1ull);
+        if (__float_as_uint(sqrt_rn_core(0.0f)) != 0u) atomicAdd(&c->bad[0], 1ull);
+    }
     atomicAdd(&c->checked[2], 1ull);
     if (__float_as_uint(q) != __float_as_uint(r)) {
         atomicAdd(&c->bad[2], 1ull); c->first[2][0] = __float_as_uint(a); c->first[2][1] = __float_as_uint(b);

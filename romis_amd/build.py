@@ -34,6 +34,18 @@ SOURCES = [
 HEADERS = ["device_math.h", "restir_types.h", "launch.h", "bvh.h"]
 
 
+def source_hash() -> str:
+    """sha256 over the device sources and flags: identifies the kernels a profile was measured on (bench.py
+    reports a committed PMC traffic figure only when it matches)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in [SOURCES[0][0]] + HEADERS:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    h.update(" ".join(COMMON[:6] + DEVICE).encode())
+    return h.hexdigest()[:16]
+
+
 def _stale(target: str, deps: list[str]) -> bool:
     if not os.path.exists(target):
         return True

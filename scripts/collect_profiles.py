@@ -68,6 +68,25 @@ def main():
             k: {"fetch_kib_raw": round(fetch.get(k, 0.0), 1), "write_kib": round(write.get(k, 0.0), 1),
                 "hbm_bytes_corrected": round(fetch.get(k, 0.0) * 1024 * 2 + write.get(k, 0.0) * 1024)}
             for k in sorted(set(fetch) | set(write))}
+    sh = os.path.join(src, "source_hash.txt")
+    if os.path.exists(sh) and "hbm_per_launch" in summary:
+        with open(sh) as fh:
+            summary["source_hash"] = fh.read().strip()
+        sp = {k: v for k, v in summary["hbm_per_launch"].items() if k.startswith("k_spatial")}
+        if len(sp) == 1:
+            (kname, t), = sp.items()
+            trace_bench = os.path.join(src, "trace_bench.json")
+            cfg = None
+            if os.path.exists(trace_bench):
+                with open(trace_bench) as fh:
+                    cfg = json.loads(fh.read().strip().splitlines()[-1]).get("config")
+            rec = {"source_hash": summary["source_hash"], "kernel": kname,
+                   "traffic_bytes_per_launch": t["hbm_bytes_corrected"], "config": cfg,
+                   "profile": os.path.relpath(dst, ROOT),
+                   "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; bytes = "
+                             "FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read correction) + WRITE_SIZE KiB x 1024"}
+            with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as fh:
+                json.dump(rec, fh, indent=1)
     bj = os.path.join(src, "bench.json")
     if os.path.exists(bj):
         with open(bj) as fh:

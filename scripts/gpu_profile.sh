@@ -12,6 +12,7 @@ export TMPDIR=/tmp
 cd "$REPO" || exit 1
 BENCH_ARGS=${BENCH_ARGS:-"--steps 50 --warmup 5"}
 
+python3 -c "from romis_amd import build; print(build.source_hash())" > "$OUT/source_hash.txt" || exit 10
 echo "[profile] plain bench" >&2
 timeout -k 10 300 python3 bench.py $BENCH_ARGS > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 11
 cat "$OUT/bench.json"

@@ -42,7 +42,7 @@ def source_hash() -> str:
     for f in [SOURCES[0][0]] + HEADERS:
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(f.encode() + b"\0" + fh.read())
-    h.update(" ".join(COMMON[:6] + DEVICE).encode())
+    h.update(" ".join([c for c in COMMON + DEVICE if not c.startswith("-I")]).encode())   # flags, not paths
     return h.hexdigest()[:16]
 
 

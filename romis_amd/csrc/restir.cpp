@@ -281,7 +281,7 @@ restir_status ensure_work(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N, b
 restir_status timed_begin(restir_ctx* c, int kernel, Pending& p) {
     p.kernel = kernel;
     p.start = p.stop = nullptr;
-    if (!c->timing) return RESTIR_OK;
+    if (!c->timing || !((c->tuning.timing_mask >> kernel) & 1u)) return RESTIR_OK;
     for (hipEvent_t* e : {&p.start, &p.stop}) {
         if (!c->free_events.empty()) { *e = c->free_events.back(); c->free_events.pop_back(); }
         else HIP_TRY(hipEventCreate(e));
@@ -292,7 +292,7 @@ restir_status timed_begin(restir_ctx* c, int kernel, Pending& p) {
 
 restir_status timed_end(restir_ctx* c, Pending& p, hipError_t launch_err) {
     if (launch_err != hipSuccess) return fail(RESTIR_ERR_HIP, "kernel launch: %s", hipGetErrorString(launch_err));
-    if (!c->timing) return RESTIR_OK;
+    if (!p.start) return RESTIR_OK;
     HIP_TRY(hipEventRecord(p.stop, c->stream));
     c->pending.push_back(p);
     return RESTIR_OK;
@@ -885,6 +885,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "ris.lds")) t.ris_lds = v;
     else if (!std::strcmp(key, "spatial.xcd")) t.spatial_xcd = v;
     else if (!std::strcmp(key, "spatial.blocks")) t.spatial_blocks = v;
+    else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;
     else if (!std::strcmp(key, "final.blocks")) t.final_blocks = v;
     else if (!std::strcmp(key, "final.lds")) t.final_lds = v;
     else if (!std::strcmp(key, "final.2d")) t.final_2d = v;

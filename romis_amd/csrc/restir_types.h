@@ -63,6 +63,7 @@ struct Tuning {
     uint32_t ris_lds = 1;          // stage the light table in LDS when it fits
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
     uint32_t spatial_blocks = 0;
+    uint32_t timing_mask = 0xFFFFFFFFu;   // kernels (bit = RESTIR_K_*) bracketed by HIP events when timing is on
     uint32_t final_blocks = 0;
     uint32_t final_lds = 1;
     uint32_t final_2d = 1;

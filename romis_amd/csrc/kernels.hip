@@ -415,6 +415,23 @@ __device__ __forceinline__ bool work_pixel(const Region& rg, uint32_t item, uint
     return rg.map2d ? tile_pixel_of(rg, item, x, y, p) : region_pixel(rg, item * 256u + threadIdx.x, x, y, p);
 }
 
+// Work items of a persistent block: from the dynamic queue when there is one (thread 0 takes a ticket, the
+// block shares it through LDS), else the static stride blockIdx.x, blockIdx.x + gridDim.x, ...
+struct WorkCursor {
+    WorkQueue q;
+    uint32_t item;
+    __device__ explicit WorkCursor(WorkQueue wq) : q(wq), item(0) {}
+    __device__ __forceinline__ uint32_t fetch() {
+        __shared__ uint32_t s_item;
+        __syncthreads();   // every thread has read the previous ticket
+        if (threadIdx.x == 0) s_item = atomicAdd(q.ctr, 1u) - q.base;
+        __syncthreads();
+        return s_item;
+    }
+    __device__ __forceinline__ uint32_t first() { return item = q.ctr ? fetch() : blockIdx.x; }
+    __device__ __forceinline__ uint32_t next() { return item = q.ctr ? fetch() : item + gridDim.x; }
+};
+
 }  // namespace romis
 
 using namespace romis;
@@ -470,7 +487,8 @@ extern "C" __global__ __launch_bounds__(256) void k_primary_lds(SceneDev s, Regi
 template <int NT, bool LDS_LIGHTS>
 __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                          const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
-                                         float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg) {
+                                         float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
+                                         WorkQueue wq) {
     const uint32_t L = s.num_lights;
     const float4* lights = s.lights;
     if (LDS_LIGHTS) {
@@ -483,7 +501,8 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
     const uint32_t items = work_items(rg);
     const float invL = 1.0f / (float)L;
-    for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {
+    WorkCursor cur(wq);
+    for (uint32_t item = cur.first(); item < items; item = cur.next()) {
         uint32_t x, y;
         size_t p;
         if (!work_pixel(rg, item, x, y, p)) continue;
@@ -563,8 +582,8 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
 #define ROMIS_RIS_KERNEL(NT, LDS, NAME, ATTR)                                                                         \
     extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,   \
-                                                          float4* ra, float4* rb, float2* rdbg) {                       \
-        ris_body<NT, LDS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg);                                     \
+                                                          float4* ra, float4* rb, float2* rdbg, WorkQueue wq) {         \
+        ris_body<NT, LDS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg, wq);                                 \
     }
 ROMIS_RIS_KERNEL(1, false, k_ris_n1, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL(2, false, k_ris_n2, )
@@ -917,15 +936,22 @@ hipError_t launch_primary(const SceneDev& s, const Region& rg0, const CameraDev&
 
 hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
                       const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, const Tuning& tu,
-                      hipStream_t stream) {
+                      QueueState& qs, hipStream_t stream) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, 0);
+    WorkQueue wq{nullptr, 0u};
+    dim3 grid = grid_capped(items_of(rg), tu.ris_blocks);
+    if (tu.ris_queue && qs.ctr) {
+        grid = dim3(std::min(items_of(rg), tu.ris_queue));
+        wq = WorkQueue{qs.ctr, qs.base};
+        qs.base += items_of(rg) + grid.x;
+    }
     const size_t lds = lights_lds_bytes(s);
     const bool use_lds = tu.ris_lds && s.num_lights > 0 && lds <= kLdsBudget;
     auto k = use_lds ? (f.N == 1 ? k_ris_n1_lds : (f.N == 2 ? k_ris_n2_lds : k_ris_n0_lds))
                      : (f.N == 1 ? k_ris_n1 : (f.N == 2 ? k_ris_n2 : k_ris_n0));
-    hipLaunchKernelGGL(k, grid_capped(items_of(rg), tu.ris_blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,
-                       key, o[0], o[1], o[2], n_t, p_mat, ra, rb, rdbg);
+    hipLaunchKernelGGL(k, grid, dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ra,
+                       rb, rdbg, wq);
     return hipGetLastError();
 }
 

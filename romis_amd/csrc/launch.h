@@ -9,7 +9,7 @@ hipError_t launch_primary(const SceneDev& s, const Region& rg, const CameraDev& 
                           const Tuning& tu, hipStream_t stream);
 hipError_t launch_ris(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
                       const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, const Tuning& tu,
-                      hipStream_t stream);
+                      QueueState& qs, hipStream_t stream);
 hipError_t launch_temporal(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
                            const float4* n_t, const float4* p_mat, const float4* ca, const float4* cb,
                            const float4* pa, const float4* pb, float4* oa, float4* ob, float2* odbg,

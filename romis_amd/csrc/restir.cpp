@@ -112,6 +112,8 @@ struct restir_ctx {
 
     // launch-shape knobs (restir_set_tuning)
     Tuning tuning{};
+    DevBuf queue_ctr;      // WorkQueue ticket counter (4 bytes, zeroed at creation, never reset)
+    QueueState queue{};
 
     // RNG
     uint32_t seed = RESTIR_DEFAULT_SEED;
@@ -373,6 +375,12 @@ restir_status restir_create(int device, restir_ctx** out) {
     c->device = device;
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; return fail(RESTIR_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e)); }
+    if (c->queue_ctr.ensure(64) != RESTIR_OK || hipMemset(c->queue_ctr.p, 0, 64) != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return fail(RESTIR_ERR_HIP, "work-queue counter allocation failed");
+    }
+    c->queue.ctr = c->queue_ctr.as<uint32_t>();
     *out = c;
     return RESTIR_OK;
 }
@@ -385,7 +393,7 @@ void restir_destroy(restir_ctx* c) {
         (void)hipStreamSynchronize(c->stream);
         for (DevBuf* b : {&c->nodes, &c->tri_v0, &c->tri_e1, &c->tri_e2, &c->tri_n0, &c->tri_n1, &c->tri_n2,
                           &c->materials, &c->lights, &c->n_t, &c->p_mat, &c->ra[0], &c->ra[1], &c->rb[0], &c->rb[1],
-                          &c->dbg[0], &c->dbg[1], &c->rgb})
+                          &c->dbg[0], &c->dbg[1], &c->rgb, &c->queue_ctr})
             b->release();
         for (Pending& p : c->pending) { (void)hipEventDestroy(p.start); (void)hipEventDestroy(p.stop); }
         for (hipEvent_t ev : c->free_events) (void)hipEventDestroy(ev);
@@ -614,7 +622,7 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
 
     TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, nt, pm, c->tuning, c->stream));
     TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, 0), camd.origin, nt, pm,
-                                      c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), nullptr, c->tuning, c->stream));
+                                      c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), nullptr, c->tuning, c->queue, c->stream));
     if (temporal) {
         TIMED(c, RESTIR_K_TEMPORAL,
               launch_temporal(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0), camd.origin, nt, pm,
@@ -782,7 +790,7 @@ restir_status restir_stage_ris(restir_ctx* c, const restir_camera* cam, const re
     const int cur = c->cur;
     TIMED(c, RESTIR_K_RIS, launch_ris(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                                       c->ra[cur].as<float4>(), c->rb[cur].as<float4>(),
-                                      debug ? c->dbg[cur].as<float2>() : nullptr, c->tuning, c->stream));
+                                      debug ? c->dbg[cur].as<float2>() : nullptr, c->tuning, c->queue, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
@@ -886,6 +894,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.xcd")) t.spatial_xcd = v;
     else if (!std::strcmp(key, "spatial.blocks")) t.spatial_blocks = v;
     else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;
+    else if (!std::strcmp(key, "ris.queue")) t.ris_queue = v;
     else if (!std::strcmp(key, "final.blocks")) t.final_blocks = v;
     else if (!std::strcmp(key, "final.lds")) t.final_lds = v;
     else if (!std::strcmp(key, "final.2d")) t.final_2d = v;

@@ -61,12 +61,27 @@ struct Tuning {
     uint32_t primary_2d = 1;
     uint32_t ris_blocks = 0;
     uint32_t ris_lds = 1;          // stage the light table in LDS when it fits
+    uint32_t ris_queue = 0;        // persistent blocks (this many) pulling tiles from a WorkQueue; 0 = off
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
     uint32_t spatial_blocks = 0;
     uint32_t timing_mask = 0xFFFFFFFFu;   // kernels (bit = RESTIR_K_*) bracketed by HIP events when timing is on
     uint32_t final_blocks = 0;
     uint32_t final_lds = 1;
     uint32_t final_2d = 1;
+};
+
+// Dynamic tile queue for persistent grids: a never-reset ticket counter; a launch hands out tickets
+// base .. base + items + grid - 1 (every block fetches until its first out-of-range ticket), so the host knows
+// the next launch's base without reading the counter back.
+struct WorkQueue {
+    uint32_t* ctr;     // nullptr: no queue (block b takes work items b, b + grid, ...)
+    uint32_t base;
+};
+
+// Host side of the queue: the context's counter and the next launch's base.
+struct QueueState {
+    uint32_t* ctr = nullptr;
+    uint32_t base = 0;
 };
 
 struct CameraDev {

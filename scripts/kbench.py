@@ -20,7 +20,7 @@ import numpy as np  # noqa: E402
 
 from romis_amd import _abi, restir, scene  # noqa: E402
 
-DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 1,
+DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 1, "ris.queue": 0,
             "spatial.xcd": 1, "spatial.blocks": 0, "final.blocks": 0, "final.lds": 1, "final.2d": 1}
 
 VARIANTS = {
@@ -34,6 +34,9 @@ VARIANTS = {
     "ris_nolds": {"ris.lds": 0},
     "ris_p2048": {"ris.blocks": 2048},
     "ris_lds_p2048": {"ris.lds": 1, "ris.blocks": 2048},
+    "ris_q1280": {"ris.queue": 1280},
+    "ris_q2560": {"ris.queue": 2560},
+    "ris_q1024": {"ris.queue": 1024},
     "spatial_noxcd": {"spatial.xcd": 0},
     "spatial_p1024": {"spatial.blocks": 1024},
     "spatial_p2048": {"spatial.blocks": 2048},

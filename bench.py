@@ -12,6 +12,10 @@ tiles -- each rank owns a 1920x1080 tile of a (tx*1920) x (ty*1080) image (2x1, 
 tile plus a ghost zone of passes*r pixels, so no data-path collective is needed (DESIGN.md "Multi-GPU");
 the barrier / max-over-ranks timing uses torch.distributed (RCCL).
 
+Other BASELINE.json configs (--config c1|c3|c4|c5; c2 is the default): c1 CornellBox 512x512 RIS only, c3 two
+spatial passes + temporal reuse threading each frame's grid into the next (1 GPU), c4 4K / 1024 lights and
+c5 8K / 4096 lights / M=64 / unbiased + visibility reuse (strong scaling: the image is fixed and split).
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -34,17 +38,20 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--scene", default="nightclub_128pt")
-    ap.add_argument("--M", type=int, default=32)
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
+                    help="BASELINE.json config (c2 = configs[1], the headline)")
+    ap.add_argument("--scene", default=None, help="override the config's scene")
+    ap.add_argument("--M", type=int, default=None, help="override the config's M")
     ap.add_argument("--N", type=int, default=1)
     ap.add_argument("--k", type=int, default=5)
     ap.add_argument("--r", type=int, default=10)
-    ap.add_argument("--passes", type=int, default=1)
-    ap.add_argument("--tile-width", type=int, default=TILE_W)
-    ap.add_argument("--tile-height", type=int, default=TILE_H)
+    ap.add_argument("--passes", type=int, default=None, help="override the config's spatial passes")
+    ap.add_argument("--tile-width", type=int, default=None)
+    ap.add_argument("--tile-height", type=int, default=None)
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    ap.add_argument("--cpu-rows", type=int, default=540, help="rows of the workload the CPU baseline renders")
+    ap.add_argument("--cpu-rows", type=int, default=None, help="rows of the workload the CPU baseline renders "
+                    "(default: ~1 Mpx worth)")
     ap.add_argument("--traffic-csv", default=None,
                     help="rocprofv3 --pmc CSV (FETCH_SIZE / WRITE_SIZE) of this command for roofline.traffic")
     return ap.parse_args()
@@ -147,28 +154,82 @@ def cpu_baseline(sc, cam_fn, features, rows, W, H):
                       f"OpenMP {threads} threads)"}
 
 
+# BASELINE.json configs.  "weak": each rank owns a tile x tile_h tile of a (tx*tile) x (ty*tile_h) image;
+# "strong": the image is fixed and split over the ranks.  c2 (configs[1]) is the headline and the default.
+CONFIGS = {
+    "c1": dict(scene="cornell_parallelogram", image=(512, 512), M=32, passes=0, temporal=0, unbiased=0, vis=0,
+               workload="C1: CornellBox-Mirror 512x512, 1 parallelogram light, M=32, RIS only (no spatial/temporal)"),
+    "c2": dict(scene="nightclub_128pt", tile=(TILE_W, TILE_H), M=32, passes=1, temporal=0, unbiased=0, vis=0,
+               workload="C2: cornell-nightclub 1080p per GPU, 128 point lights, M=32, N=1, spatial k=5 r=10 x1 "
+                        "biased, no temporal, frame = primary+RIS+spatial+final"),
+    "c3": dict(scene="nightclub_128pt", tile=(TILE_W, TILE_H), M=32, passes=2, temporal=1, unbiased=0, vis=0,
+               workload="C3: cornell-nightclub 1080p, 128 point lights, M=32, spatial k=5 x2 + temporal reuse, "
+                        "every frame reuses the previous one (static camera)"),
+    "c4": dict(scene="cornell_1024", image=(3840, 2160), M=32, passes=1, temporal=0, unbiased=0, vis=0,
+               workload="C4: 4K Cornell box, 32x32 = 1024 ceiling parallelogram lights, M=32, k=5 x1 biased"),
+    "c5": dict(scene="cornell_4096", image=(7680, 4320), M=64, passes=1, temporal=0, unbiased=1, vis=1,
+               workload="C5: 8K Cornell box, 64x64 = 4096 ceiling parallelogram lights, M=64, k=5 x1 unbiased "
+                        "+ spatial visibility reuse"),
+}
+
+
+DATA = {"nightclub_128pt": "prebuilt cornell-nightclub geometry, 128 point lights",
+        "cornell_parallelogram": "prebuilt CornellBox-Mirror-Rotated geometry, 1 parallelogram light",
+        "cornell_1024": "prebuilt Cornell box geometry, 32x32 regularLightGrid ceiling lights",
+        "cornell_4096": "prebuilt Cornell box geometry, 64x64 regularLightGrid ceiling lights"}
+
+
+def spatial_px_per_launch(tile, passes, r):
+    """Average pixels a spatial launch computes: pass p covers the owned rect grown by (P-1-p)*r, clipped."""
+    tot = 0
+    for p in range(passes):
+        g = (passes - 1 - p) * r
+        x0, y0 = max(0, tile.x0 - g), max(0, tile.y0 - g)
+        x1 = min(tile.global_width, tile.x0 + tile.width + g)
+        y1 = min(tile.global_height, tile.y0 + tile.height + g)
+        tot += (x1 - x0) * (y1 - y0)
+    return tot / max(1, passes)
+
+
 def main():
     args = parse()
     rank, world, local, torch = dist_setup(args.gpus)
     from romis_amd import _abi, restir, scene
 
+    cf = dict(CONFIGS[args.config])
+    for key in ("scene", "M", "passes"):
+        if getattr(args, key) is not None:
+            cf[key] = getattr(args, key)
     tx, ty = restir.tile_grid(world)
-    GW, GH = tx * args.tile_width, ty * args.tile_height
-    sc = scene.bench_scene(args.scene)
-    cam = scene.camera_for(args.scene, GW, GH)
-    f = _abi.default_features(initial_light_samples=args.M, num_samples_in_reservoir=args.N,
+    if "tile" in cf:
+        tw, th = args.tile_width or cf["tile"][0], args.tile_height or cf["tile"][1]
+        GW, GH, scaling = tx * tw, ty * th, "weak"
+    else:
+        GW, GH, scaling = cf["image"][0], cf["image"][1], "strong"
+    if cf["temporal"] and world > 1:
+        raise SystemExit(f"{args.config}: temporal reuse runs on one GPU (BASELINE.json configs[2])")
+    sc = scene.bench_scene(cf["scene"])
+    cam = scene.camera_for(cf["scene"], GW, GH)
+    passes = cf["passes"]
+    f = _abi.default_features(initial_light_samples=cf["M"], num_samples_in_reservoir=args.N,
                               num_neighbours_to_sample=args.k, spatial_resample_radius=args.r,
-                              spatial_resampling_passes=args.passes, spatial_reuse=1 if args.passes > 0 else 0,
-                              temporal_reuse=0, unbiased_combination=0)
-    ghost = args.passes * args.r
+                              spatial_resampling_passes=passes, spatial_reuse=1 if passes > 0 else 0,
+                              temporal_reuse=cf["temporal"], unbiased_combination=cf["unbiased"],
+                              spatial_reuse_visibility_check=cf["vis"])
+    ghost = passes * args.r
     tile = restir.tile_plan(GW, GH, tx, ty, rank, ghost)
 
     r = restir.Renderer(local)
     r.set_scene(sc)
     r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
+    state = {"grid": None}
 
     def step():
-        r.render_restir(None, cam, GW, GH, f, tile=tile, want_rgb=False, want_grid=False)
+        if cf["temporal"]:   # thread the previous frame's grid (main.cpp:165)
+            _, g = r.render_restir(state["grid"], cam, GW, GH, f, tile=tile, want_rgb=False, want_grid=True)
+            state["grid"] = g   # the previous handle is released when dropped
+        else:
+            r.render_restir(None, cam, GW, GH, f, tile=tile, want_rgb=False, want_grid=False)
 
     for _ in range(args.warmup):
         step()
@@ -195,25 +256,25 @@ def main():
     r.synchronize()
     r.enable_timing(False)
     kt_all = r.timings()
+    state["grid"] = None
 
     ms_per_step = elapsed / args.steps * 1e3
-    owned_px = tile.width * tile.height            # identical on every rank (even split)
     total = GW * GH * args.N
     value = total / (elapsed / args.steps) / 1e6
 
-    cfg = {"workload": "C2: cornell-nightclub 1080p per GPU, 128 point lights, M=32, N=1, spatial k=5 r=10 "
-                       "x1 biased, no temporal, frame = primary+RIS+spatial+final",
-           "scene": args.scene, "tile": [args.tile_width, args.tile_height], "image": [GW, GH],
-           "tiles": [tx, ty], "M": args.M, "N": args.N, "k": args.k, "r": args.r, "passes": args.passes,
+    cfg = {"workload": cf["workload"], "config": args.config, "scene": cf["scene"],
+           "tile": [tile.width, tile.height] if scaling == "strong" else [GW // tx, GH // ty], "image": [GW, GH],
+           "tiles": [tx, ty], "M": cf["M"], "N": args.N, "k": args.k, "r": args.r, "passes": passes,
+           "temporal": cf["temporal"], "unbiased": cf["unbiased"], "spatial_visibility": cf["vis"],
            "parallelism": f"screen tiles {tx}x{ty}, ghost {ghost}px"}
 
-    # roofline of the spatial pass: algorithmic bytes = 64 B read (own G 32 B + own reservoir 32 B) +
-    # 32 B written per pixel per sub-reservoir ... N=1: read 32 + 32N, write 32N
+    # roofline of the spatial pass: algorithmic bytes per pixel = read 32 (own G-buffer) + 32 N (own
+    # reservoir), write 32 N; neighbour gathers are cache traffic, not counted
     sp_ms, sp_n = kt["spatial"]
     roofline = None
     if sp_n:
-        sp_px = (tile.width + 2 * 0) * tile.height   # pass p computes the tile grown by (P-1-p) r; P=1 -> tile
-        bytes_per_launch = sp_px * (32 + 32 * args.N + 32 * args.N)
+        sp_px = spatial_px_per_launch(tile, passes, args.r)
+        bytes_per_launch = int(sp_px * (32 + 32 * args.N + 32 * args.N))
         avg_s = sp_ms / sp_n / 1e3
         achieved = bytes_per_launch / avg_s / 1e9
         traffic, traffic_src = (pmc_traffic(args.traffic_csv), args.traffic_csv) if args.traffic_csv else (None, None)
@@ -221,12 +282,18 @@ def main():
             traffic, traffic_src = committed_traffic(cfg)
         roofline = {"kernel": "k_spatial", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": traffic, "traffic_source": traffic_src, "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(avg_s * 1e6, 2),
+                    "traffic": traffic, "traffic_source": traffic_src, "bytes_per_launch": bytes_per_launch,
+                    "avg_launch_us": round(avg_s * 1e6, 2),
                     "read_only_frac": round(sp_px * (32 + 32 * args.N) / avg_s / 1e9 / HBM_PEAK_GBS, 4)}
+        # the practical ceiling next to the spec: a streaming-read kernel over 4 GiB (past the Infinity Cache)
+        measured = r.measure_read_bandwidth(4 << 30, 10)
+        roofline["measured_read_peak"] = round(measured, 1)
+        roofline["frac_of_measured_peak"] = round(achieved / measured, 4)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
-        cpu = cpu_baseline(sc, lambda w, h: scene.camera_for(args.scene, w, h), f, args.cpu_rows, GW, GH)
+        rows = args.cpu_rows or min(GH, max(8, 1036800 // GW))   # ~1 Mpx of the workload, ~0.3 s on 16 cores
+        cpu = cpu_baseline(sc, lambda w, h: scene.camera_for(cf["scene"], w, h), f, rows, GW, GH)
 
     kernels = {k: {"us_per_launch": round(v[0] / v[1] * 1e3, 2) if v[1] else None, "launches": int(v[1])}
                for k, v in kt_all.items()}
@@ -241,10 +308,10 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (prebuilt cornell-nightclub geometry, 128 point lights, keyed RNG seed 0x5EED0001)",
+            "data": f"synthetic ({DATA[cf['scene']]}, keyed RNG seed 0x5EED0001)",
             "config": cfg,
             "roofline": roofline,
             "cpu_baseline": cpu,

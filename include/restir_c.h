@@ -232,6 +232,11 @@ restir_status restir_stage_final(restir_ctx* ctx, const restir_camera* cam, cons
 restir_status restir_debug_math(restir_ctx* ctx, const float* x, const float* y, float* out_pow, float* out_exp,
                                 size_t n);
 
+/* Measured HBM read bandwidth of this device (the roofline's practical ceiling next to the 8 TB/s spec): a
+ * streaming-read kernel over `bytes` (rounded down to 16 B; pass >= 1 GiB to defeat the 256 MB Infinity
+ * Cache), timed with HIP events over `iters` launches.  *out_gbps = bytes * iters / time / 1e9. */
+restir_status restir_measure_read_bandwidth(restir_ctx* ctx, uint64_t bytes, uint32_t iters, double* out_gbps);
+
 /* ---- timing ----------------------------------------------------------------------------------------- */
 /* When enabled, every kernel of restir_render / restir_stage_* is bracketed by HIP events on the
  * context's stream; restir_timings returns the accumulated milliseconds and launch counts per kernel. */

@@ -124,6 +124,7 @@ SIGNATURES = {
     "restir_stage_final": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Features)]),
     "restir_debug_math": (C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                     C.POINTER(C.c_float), C.c_size_t]),
+    "restir_measure_read_bandwidth": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
     "restir_enable_timing": (C.c_int, [_P, C.c_int]),
     "restir_set_tuning": (C.c_int, [_P, C.c_char_p, C.c_int]),
     "restir_timings": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),

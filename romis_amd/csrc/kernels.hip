@@ -901,6 +901,20 @@ extern "C" __global__ void k_debug_math(const float* x, const float* y, float* p
     ex[i] = pm_expf(x[i]);
 }
 
+// Streaming read (restir_measure_read_bandwidth): grid-stride 16-byte loads, 4 in flight per lane, one partial
+// sum per block so nothing is dead code.
+extern "C" __global__ __launch_bounds__(256) void k_read_stream(const float4* __restrict__ buf, size_t n4, float* sink) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    float acc = 0.0f;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        const float4 a = buf[i], b = buf[i + stride], c = buf[i + 2 * stride], d = buf[i + 3 * stride];
+        acc += ((a.x + b.y) + (c.z + d.w));
+    }
+    for (; i < n4; i += stride) acc += buf[i].x;
+    if (acc == 12345.0f) sink[blockIdx.x % 256u] = acc;   // buffers are zero: never taken, but not provably so
+}
+
 // ---------------------------------------------------------------------------------------------------------
 // Host launchers (launch.h)
 #include "launch.h"
@@ -993,6 +1007,11 @@ hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev&
                      : (f.N == 1 ? k_final_n1 : (f.N == 2 ? k_final_n2 : k_final_n0));
     hipLaunchKernelGGL(k, grid_capped(items_of(rg), tu.final_blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,
                        o[0], o[1], o[2], n_t, p_mat, ra, rb, rgb);
+    return hipGetLastError();
+}
+
+hipError_t launch_read_stream(const float4* buf, size_t n4, float* sink, hipStream_t stream) {
+    hipLaunchKernelGGL(k_read_stream, dim3(256 * 16), dim3(kBlock), 0, stream, buf, n4, sink);
     return hipGetLastError();
 }
 

@@ -860,6 +860,34 @@ restir_status restir_debug_math(restir_ctx* c, const float* x, const float* y, f
     return RESTIR_OK;
 }
 
+restir_status restir_measure_read_bandwidth(restir_ctx* c, uint64_t bytes, uint32_t iters, double* out_gbps) {
+    if (!c || !out_gbps || iters == 0 || bytes < (1u << 20)) return fail(RESTIR_ERR_INVALID, "bad argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t n4 = (size_t)(bytes / 16);
+    DevBuf buf, sink;
+    ST_TRY(buf.ensure(n4 * 16));
+    ST_TRY(sink.ensure(1 << 20));
+    HIP_TRY(hipMemsetAsync(buf.p, 0, n4 * 16, c->stream));
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    hipError_t e = launch_read_stream(buf.as<float4>(), n4, sink.as<float>(), c->stream);   // warm
+    if (e == hipSuccess) e = hipEventRecord(e0, c->stream);
+    for (uint32_t i = 0; i < iters && e == hipSuccess; i++) e = launch_read_stream(buf.as<float4>(), n4, sink.as<float>(), c->stream);
+    if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0.0f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    buf.release();
+    sink.release();
+    if (e != hipSuccess) return fail(RESTIR_ERR_HIP, "read-bandwidth kernel: %s", hipGetErrorString(e));
+    *out_gbps = (double)n4 * 16.0 * iters / (ms * 1e-3) / 1e9;
+    return RESTIR_OK;
+}
+
 // ---------------------------------------------------------------------------------------------------------
 // timing
 restir_status restir_enable_timing(restir_ctx* c, int enable) {

@@ -85,6 +85,13 @@ class Renderer:
               "restir_download_rgb")
         return rgb
 
+    def measure_read_bandwidth(self, nbytes: int = 4 << 30, iters: int = 10) -> float:
+        """GB/s of a streaming-read kernel over `nbytes` of HBM (restir_measure_read_bandwidth)."""
+        out = C.c_double()
+        check(self.lib, self.lib.restir_measure_read_bandwidth(self.ctx, int(nbytes), int(iters), C.byref(out)),
+              "restir_measure_read_bandwidth")
+        return out.value
+
     # ---- timing ---------------------------------------------------------------------------------------
     def enable_timing(self, on: bool = True) -> None:
         check(self.lib, self.lib.restir_enable_timing(self.ctx, 1 if on else 0), "restir_enable_timing")

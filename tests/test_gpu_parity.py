@@ -265,15 +265,19 @@ def test_device_math_matches_oracle(gpu, oracle):
 
 # --------------------------------------------------------------------------------------------------------
 # whole frames through restir_render (renderReSTIR)
-@pytest.mark.parametrize("name,N,passes,unbiased", [("nightclub_128pt", 1, 1, 0), ("nightclub_512", 2, 2, 0),
-                                                    ("cornell_parallelogram", 1, 2, 1)])
-def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased):
+# the BASELINE.json configs at parity-test size: C1 (RIS only), C2, the 512-parallelogram nightclub, C4 (1024
+# ceiling lights), C5 (4096 lights, M=64, unbiased + visibility reuse), plus the default N=2 / two passes
+@pytest.mark.parametrize("name,N,passes,unbiased,M,vis", [
+    ("cornell_parallelogram", 1, 0, 0, 32, 0), ("nightclub_128pt", 1, 1, 0, 32, 0), ("nightclub_512", 2, 2, 0, 32, 0),
+    ("cornell_parallelogram", 1, 2, 1, 32, 0), ("cornell_1024", 1, 1, 0, 32, 0), ("cornell_4096", 1, 1, 1, 64, 1)])
+def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased, M, vis):
     s = get_scene(name)
     gpu.set_scene(s)
     osc = oracle.OracleScene(s)
     cam = scene.camera_for(name, W, H)
     f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=passes, unbiased_combination=unbiased,
-                              temporal_reuse=0)
+                              temporal_reuse=0, initial_light_samples=M, spatial_reuse=1 if passes else 0,
+                              spatial_reuse_visibility_check=vis)
     gpu.set_seed(SEED, 0)
     rgb, grid = gpu.render_restir(None, cam, W, H, f)
     want, _, _ = oracle.render_frame(osc, cam, f, W, H, SEED, 0)
@@ -391,6 +395,11 @@ def test_full_1080p_render_deterministic(gpu):
     b, _ = gpu.render_restir(None, cam, 1920, 1080, f, want_grid=False)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     assert np.isfinite(a).all() and (a >= 0).all() and a.mean() > 0.01
+
+
+def test_measured_read_bandwidth_is_plausible(gpu):
+    gbs = gpu.measure_read_bandwidth(1 << 30, 3)
+    assert 1000.0 < gbs < 9000.0, gbs     # MI355X HBM3E: 8 TB/s spec
 
 
 def test_errors_are_reported(gpu):

@@ -338,7 +338,7 @@ __device__ __forceinline__ void macc_add(uint32_t* macc, uint32_t k, uint32_t m)
 
 __device__ __forceinline__ float contribution_weight(float p, uint32_t M, float wsum) {
     if (p == 0.0f) return 0.0f;
-    return ((1.0f / p) * (1.0f / (float)M)) * wsum;
+    return (rcp_rn(p) * rcp_rn((float)M)) * wsum;   // rcp_rn(b) == 1.0f / b bit for bit (device_math.h)
 }
 
 __device__ __forceinline__ Sub sub_from(float4 fa, float4 fb) {
@@ -683,7 +683,7 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
                                               v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                               const float4* __restrict__ ia, const float4* __restrict__ ib,
                                               float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
-                                              uint32_t x, uint32_t y, size_t p) {
+                                              uint32_t x, uint32_t y, size_t p, const Bvh& bvh) {
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
     const uint32_t K = f.K;
@@ -698,6 +698,12 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
 #endif
     Combiner<NT> cmb;
     cmb.init(N);
+#if defined(ROMIS_SPATIAL_DEPTH_DIV)
+    const bool t_fast = false;
+#else
+    const bool t_fast = div_fast_ok(cur.t);
+#endif
+    const double rt = rcp_d(cur.t);
     for (uint32_t n0 = 0; n0 < K; n0 += kBatch) {
         uint32_t q[kBatch];
         float4 g[kBatch];
@@ -722,7 +728,9 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
         for (uint32_t i = 0; i < kBatch; i++) {
             ok[i] = n0 + i < K;
             if (!UNBIASED && ok[i]) {   // render_utils.cpp:114-118
-                float depthFracDiff = fabsf(1.0f - (g[i].w / cur.t));
+                // t_n / t_c: the k quotients share the denominator -> one double reciprocal (div_by_rcp_d)
+                const float q = t_fast ? div_by_rcp_d(g[i].w, rt) : g[i].w / cur.t;
+                float depthFracDiff = fabsf(1.0f - q);
                 float normalsDotProd = vdot(xyz(g[i]), cur.N);
                 if (depthFracDiff > 0.1f || normalsDotProd < 0.90630778703f) ok[i] = false;
             }
@@ -763,7 +771,7 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
     } else {
         // combineUnbiased (reservoir.cpp:84-103): Z_j = sum over the stream of the input's total M where
         // p_r(y_j) [* vis_r(y_j)] > 0.  The stream is re-derived from the same draws (no rejection here).
-        const Bvh bvh = global_bvh(s);
+        // p * vis > 0 needs p > 0 whatever vis is (p is a length: >= 0 or NaN), so the shadow ray is cast only then.
         for (uint32_t j = 0; j < N; j++) cmb.out[j].M = cmb.macc[j];
         unsigned long long Z[NT > 0 ? NT : RESTIR_MAX_N_DEV];
         for (uint32_t j = 0; j < N; j++) Z[j] = 0ull;
@@ -775,15 +783,14 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
             unsigned long long tot = 0;
             for (uint32_t j = 0; j < N; j++) tot += __float_as_uint(ib[j * npx + q].w);
             for (uint32_t j = 0; j < N; j++) {
-                float pd = target_pdf(s, f, rp, cmb.out[j].pos, cmb.out[j].col);
-                if (f.spatial_vis) pd *= visible(bvh, rp.P, cmb.out[j].pos) ? 1.0f : 0.0f;
-                if (pd > 0.0f) Z[j] += tot;
+                const float pd = target_pdf(s, f, rp, cmb.out[j].pos, cmb.out[j].col);
+                if (pd > 0.0f && (!f.spatial_vis || visible(bvh, rp.P, cmb.out[j].pos))) Z[j] += tot;
             }
         }
         for (uint32_t j = 0; j < N; j++) {
             float pc = cmb.out[j].has_pd ? cmb.out[j].pd : target_pdf(s, f, cur, cmb.out[j].pos, cmb.out[j].col);
             if (pc == 0.0f || Z[j] == 0ull) cmb.out[j].W = 0.0f;
-            else cmb.out[j].W = ((1.0f / pc) * (1.0f / (float)Z[j])) * cmb.out[j].wsum;
+            else cmb.out[j].W = (rcp_rn(pc) * rcp_rn((float)Z[j])) * cmb.out[j].wsum;
         }
     }
     for (uint32_t j = 0; j < N; j++) sub_store(cmb.out[j], oa, ob, odbg, j * npx + p);
@@ -793,14 +800,19 @@ template <int NT, bool UNBIASED>
 __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
                                              v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                              const float4* __restrict__ ia, const float4* __restrict__ ib,
-                                             float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg) {
+                                             float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
+                                             uint32_t bvh_lds) {
+    // unbiased combine with visibility reuse casts (k+1) N shadow rays per pixel: the block stages the BVH in
+    // LDS first (every thread reaches this: bvh_lds is uniform over the launch)
+    Bvh bvh = global_bvh(s);
+    if (UNBIASED && bvh_lds) bvh = stage_bvh(s, g_lds);
     const uint32_t T = work_items(rg);
     if (!rg.map2d) {
         for (uint32_t item = blockIdx.x; item < T; item += gridDim.x) {
             uint32_t x, y;
             size_t p;
             if (work_pixel(rg, item, x, y, p))
-                spatial_pixel<NT, UNBIASED>(s, rg, f, key, origin, n_t, p_mat, ia, ib, oa, ob, odbg, x, y, p);
+                spatial_pixel<NT, UNBIASED>(s, rg, f, key, origin, n_t, p_mat, ia, ib, oa, ob, odbg, x, y, p, bvh);
         }
         return;
     }
@@ -813,7 +825,7 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
         uint32_t x, y;
         size_t p;
         if (work_pixel(rg, band0 + t, x, y, p))
-            spatial_pixel<NT, UNBIASED>(s, rg, f, key, origin, n_t, p_mat, ia, ib, oa, ob, odbg, x, y, p);
+            spatial_pixel<NT, UNBIASED>(s, rg, f, key, origin, n_t, p_mat, ia, ib, oa, ob, odbg, x, y, p, bvh);
     }
 }
 
@@ -827,8 +839,8 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
     extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,    \
                                                           const float4* ia, const float4* ib, float4* oa, float4* ob,   \
-                                                          float2* odbg) {                                               \
-        spatial_body<NT, UB>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg);                          \
+                                                          float2* odbg, uint32_t bvh_lds) {                             \
+        spatial_body<NT, UB>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, bvh_lds);                          \
     }
 ROMIS_SPATIAL_KERNEL(1, false, k_spatial_n1_biased)
 ROMIS_SPATIAL_KERNEL(2, false, k_spatial_n2_biased)
@@ -991,8 +1003,10 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
     if (tu.spatial_blocks) grid = std::min(grid, std::max(8u, tu.spatial_blocks));
     auto k = f.unbiased ? (f.N == 1 ? k_spatial_n1_unbiased : (f.N == 2 ? k_spatial_n2_unbiased : k_spatial_n0_unbiased))
                         : (f.N == 1 ? k_spatial_n1_biased : (f.N == 2 ? k_spatial_n2_biased : k_spatial_n0_biased));
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa,
-                       ob, odbg);
+    const size_t lds = bvh_lds_bytes(s);
+    const uint32_t bvh_lds = (f.unbiased && f.spatial_vis && lds <= kLdsBudget) ? 1u : 0u;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), bvh_lds ? lds : 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat,
+                       ia, ib, oa, ob, odbg, bvh_lds);
     return hipGetLastError();
 }
 

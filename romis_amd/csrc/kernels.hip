@@ -518,30 +518,36 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
             const uint32_t c_end = (px.mat == s.num_materials - 1 && s.lights_finite && !__builtin_isnan(px.P.x + px.P.y + px.P.z))
                                        ? 0u : f.M;
             if (c_end == 0u) r[0].M = f.M;
-            // candidate c: light sample (genCanonicalSamples' switch, light.cpp:55-78)
-            auto sample = [&](uint32_t c, v3& pos, v3& col) {
-#if defined(ROMIS_ABL_LIGHT0)
-                const float4* lt = lights + 7u * (draw(ps, 4u * c) == 0x12345u ? 1u : 0u);
-#else
-                const float4* lt = lights + 7u * uniform_index(draw(ps, 4u * c), L);
-#endif
-                float4 l0 = lt[0];
+            // candidate c: light sample (genCanonicalSamples' switch, light.cpp:55-78) from its table record lt,
+            // whose rows 0 (first point, type) and 3 (first colour) the caller has already read
+            auto sample_rec = [&](uint32_t c, const float4* lt, float4 l0, float4 l3, v3& pos, v3& col) {
                 uint32_t type = __float_as_uint(l0.w);
                 if (type == 0u) {
                     pos = xyz(l0);
-                    col = xyz(lt[3]);
+                    col = xyz(l3);
                 } else if (type == 1u) {
                     float fr = rand01(draw(ps, 4u * c + 1u));
                     pos = vmix(xyz(l0), xyz(lt[1]), fr);
-                    col = vmix(xyz(lt[3]), xyz(lt[4]), fr);
+                    col = vmix(xyz(l3), xyz(lt[4]), fr);
                 } else {
                     float a = rand01(draw(ps, 4u * c + 1u));
                     float b = rand01(draw(ps, 4u * c + 2u));
                     pos = vadd(vadd(xyz(l0), vscale(xyz(lt[1]), a)), vscale(xyz(lt[2]), b));
-                    v3 l01 = vmix(xyz(lt[3]), xyz(lt[4]), a);
+                    v3 l01 = vmix(xyz(l3), xyz(lt[4]), a);
                     v3 l23 = vmix(xyz(lt[5]), xyz(lt[6]), a);
                     col = vmix(l01, l23, b);
                 }
+            };
+            auto record = [&](uint32_t c) {
+#if defined(ROMIS_ABL_LIGHT0)
+                return lights + 7u * (draw(ps, 4u * c) == 0x12345u ? 1u : 0u);
+#else
+                return lights + 7u * uniform_index(draw(ps, 4u * c), L);
+#endif
+            };
+            auto sample = [&](uint32_t c, v3& pos, v3& col) {
+                const float4* lt = record(c);
+                sample_rec(c, lt, lt[0], lt[3], pos, col);
             };
             auto weight = [&](float pd) { return s.light_scale != 0.0f ? pd * s.light_scale : pd / invL; };  // light.cpp:80
             uint32_t c = 0;
@@ -698,12 +704,6 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
 #endif
     Combiner<NT> cmb;
     cmb.init(N);
-#if defined(ROMIS_SPATIAL_DEPTH_DIV)
-    const bool t_fast = false;
-#else
-    const bool t_fast = div_fast_ok(cur.t);
-#endif
-    const double rt = rcp_d(cur.t);
     for (uint32_t n0 = 0; n0 < K; n0 += kBatch) {
         uint32_t q[kBatch];
         float4 g[kBatch];
@@ -728,9 +728,7 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
         for (uint32_t i = 0; i < kBatch; i++) {
             ok[i] = n0 + i < K;
             if (!UNBIASED && ok[i]) {   // render_utils.cpp:114-118
-                // t_n / t_c: the k quotients share the denominator -> one double reciprocal (div_by_rcp_d)
-                const float q = t_fast ? div_by_rcp_d(g[i].w, rt) : g[i].w / cur.t;
-                float depthFracDiff = fabsf(1.0f - q);
+                float depthFracDiff = fabsf(1.0f - (g[i].w / cur.t));
                 float normalsDotProd = vdot(xyz(g[i]), cur.N);
                 if (depthFracDiff > 0.1f || normalsDotProd < 0.90630778703f) ok[i] = false;
             }

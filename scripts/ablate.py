@@ -22,7 +22,6 @@ VARIANTS = {
     "spatial_self": ["ROMIS_ABL_SPATIAL_SELF"],  # spatial neighbours = the pixel itself (no gathers)
     "spatial_copy": ["ROMIS_ABL_SPATIAL_COPY"],  # spatial = copy own reservoir (memory floor)
     "ris_u2": ["ROMIS_RIS_U2"],               # two target pdfs per candidate-loop iteration
-    "spatial_depth_div": ["ROMIS_SPATIAL_DEPTH_DIV"],   # library division in the depth test
     "ris_wpe4": ["ROMIS_RIS_WPE=4"],
     "spatial_wpe3": ["ROMIS_SPATIAL_WPE=3"],
 }

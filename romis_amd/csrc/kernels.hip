@@ -889,6 +889,100 @@ __device__ __forceinline__ void final_body(const SceneDev& s, const Region& rg, 
     }
 }
 
+// N = 1 with ray binning: a wave's shadow rays are traversed in lockstep, so its cost is the union of its
+// lanes' paths; rays from one 32x8 tile toward nearby targets follow nearly the same path.  The block bins its
+// rays by a 256-cell grid of the target position (scene bounds = the BVH root box), lays them out in bin order
+// in LDS, traces ray i on thread i, and hands each result back to its pixel.  Same rays, same arithmetic:
+// only which lane traces which ray changes.  One 32x8 tile per block (every thread reaches the barriers).
+__device__ __forceinline__ uint32_t target_bin(const Bvh& b, v3 y) {
+    const float4 lo = b.nodes[0], hi = b.nodes[1];
+    auto q = [](float v, float l, float h, float cells) {
+        float t = (v - l) / fmaxf(h - l, 1e-30f) * cells;
+        return (uint32_t)fminf(fmaxf(t, 0.0f), cells - 1.0f);
+    };
+    const uint32_t qx = q(y.x, lo.x, hi.x, 8.0f), qy = q(y.y, lo.y, hi.y, 8.0f), qz = q(y.z, lo.z, hi.z, 4.0f);
+    // interleave (x2 y2 z1 x1 y1 z0 x0 y0) so that nearby cells get nearby bins
+    return ((qx >> 2) << 7) | ((qy >> 2) << 6) | ((qz >> 1) << 5) | (((qx >> 1) & 1u) << 4) | (((qy >> 1) & 1u) << 3) |
+           ((qz & 1u) << 2) | ((qx & 1u) << 1) | (qy & 1u);
+}
+
+template <bool LDS_BVH>
+__device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, v3 origin,
+                                                  const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                                  const float4* __restrict__ ra, const float4* __restrict__ rb,
+                                                  float* __restrict__ rgb) {
+    __shared__ uint32_t s_hist[256];
+    __shared__ uint32_t s_wsum[4];
+    __shared__ float4 s_from[256], s_to[256];
+    __shared__ uint32_t s_vis[256];
+    const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
+    const float g = 1.0f / f.gamma;
+    const uint32_t t = threadIdx.x;
+    uint32_t x, y;
+    size_t p;
+    const bool valid = work_pixel(rg, blockIdx.x, x, y, p);
+    Px px;
+    Sub r;
+    v3 sc = mk(0.0f, 0.0f, 0.0f);
+    bool need = false;
+    if (valid) {
+        px = load_px(s, n_t, p_mat, p, origin);
+        sub_load(r, ra, rb, p);
+        sc = shade(s, f, px, r.pos, r.col);
+        need = sc.x != 0.0f || sc.y != 0.0f || sc.z != 0.0f;   // see final_body: no ray when sc == 0
+    }
+    s_hist[t] = 0u;
+    __syncthreads();
+    const uint32_t bin = need ? target_bin(bvh, r.pos) : 0u;
+    const uint32_t rank = need ? atomicAdd(&s_hist[bin], 1u) : 0u;
+    __syncthreads();
+    // exclusive scan of the 256 bin counts: wave scan + wave totals
+    const uint32_t cnt = s_hist[t];
+    uint32_t inc = cnt;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t v = __shfl_up(inc, d, 64);
+        if ((t & 63u) >= d) inc += v;
+    }
+    if ((t & 63u) == 63u) s_wsum[t >> 6] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < (t >> 6); w++) base += s_wsum[w];
+    const uint32_t excl = base + inc - cnt;
+    const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+    __syncthreads();
+    s_hist[t] = excl;
+    __syncthreads();
+    if (need) {
+        const uint32_t slot = s_hist[bin] + rank;
+        s_from[slot] = make_float4(px.P.x, px.P.y, px.P.z, __uint_as_float(t));
+        s_to[slot] = make_float4(r.pos.x, r.pos.y, r.pos.z, 0.0f);
+    }
+    __syncthreads();
+    if (t < total) {
+        const float4 a = s_from[t], b = s_to[t];
+        s_vis[__float_as_uint(a.w)] = visible(bvh, xyz(a), xyz(b)) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!valid) return;
+    if (need && !s_vis[t]) sc = mk(0.0f, 0.0f, 0.0f);
+    v3 color = vadd(mk(0.0f, 0.0f, 0.0f), vscale(sc, r.W));   // final_body's accumulation from 0 (-0 -> +0)
+    color = vdivs(color, 1.0f);
+    if (f.tone_map) {
+        v3 e = vscale(mk(-color.x, -color.y, -color.z), f.exposure);
+        v3 mapped = mk(1.0f - pm_expf(e.x), 1.0f - pm_expf(e.y), 1.0f - pm_expf(e.z));
+        color = g == 1.0f ? mapped : mk(pm_powf(mapped.x, g), pm_powf(mapped.y, g), pm_powf(mapped.z, g));
+    }
+    const uint32_t row = rg.rh - 1u - (y - rg.ry0);
+    float* o = rgb + 3 * ((size_t)row * rg.rw + (x - rg.rx0));
+    o[0] = color.x; o[1] = color.y; o[2] = color.z;
+}
+
+extern "C" __global__ __launch_bounds__(256) void k_final_n1_sorted(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,
+                                                                   float oz, const float4* n_t, const float4* p_mat,
+                                                                   const float4* ra, const float4* rb, float* rgb) {
+    final_sorted_body<true>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb);
+}
+
 #define ROMIS_FINAL_KERNEL(NT, LDS, NAME)                                                                              \
     extern "C" __global__ __launch_bounds__(256) void NAME(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,     \
                                                           float oz, const float4* n_t, const float4* p_mat,             \
@@ -1017,6 +1111,11 @@ hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev&
     const bool use_lds = tu.final_lds && lds <= kLdsBudget;
     auto k = use_lds ? (f.N == 1 ? k_final_n1_lds : (f.N == 2 ? k_final_n2_lds : k_final_n0_lds))
                      : (f.N == 1 ? k_final_n1 : (f.N == 2 ? k_final_n2 : k_final_n0));
+    if (tu.final_sort && use_lds && f.N == 1 && rg.map2d) {   // one tile per block
+        hipLaunchKernelGGL(k_final_n1_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, s, rg, f, o[0], o[1], o[2],
+                           n_t, p_mat, ra, rb, rgb);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k, grid_capped(items_of(rg), tu.final_blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,
                        o[0], o[1], o[2], n_t, p_mat, ra, rb, rgb);
     return hipGetLastError();

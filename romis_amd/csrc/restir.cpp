@@ -442,7 +442,7 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
         }
     }
     if (tris.size() >= (1u << 24)) return fail(RESTIR_ERR_INVALID, "too many triangles (%zu)", tris.size());
-    FlatBvh bvh = build_bvh(tris, 4);
+    FlatBvh bvh = build_bvh(tris, c->tuning.bvh_max_leaf);
     const size_t T = tris.size();
     std::vector<float> v0(4 * std::max<size_t>(T, 1)), e1(v0.size()), e2(v0.size());
     for (size_t k = 0; k < T; k++) {
@@ -923,6 +923,8 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.blocks")) t.spatial_blocks = v;
     else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;
     else if (!std::strcmp(key, "ris.queue")) t.ris_queue = v;
+    else if (!std::strcmp(key, "bvh.max_leaf")) t.bvh_max_leaf = v;
+    else if (!std::strcmp(key, "final.sort")) t.final_sort = v;   // applies from the next restir_set_scene
     else if (!std::strcmp(key, "final.blocks")) t.final_blocks = v;
     else if (!std::strcmp(key, "final.lds")) t.final_lds = v;
     else if (!std::strcmp(key, "final.2d")) t.final_2d = v;

@@ -64,10 +64,12 @@ struct Tuning {
     uint32_t ris_queue = 0;        // persistent blocks (this many) pulling tiles from a WorkQueue; 0 = off
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
     uint32_t spatial_blocks = 0;
-    uint32_t timing_mask = 0xFFFFFFFFu;   // kernels (bit = RESTIR_K_*) bracketed by HIP events when timing is on
+    uint32_t timing_mask = 0xFFFFFFFFu;
+    uint32_t bvh_max_leaf = 2;     // triangles per BVH leaf (used by restir_set_scene); 2 beat 1/4/8 (kbench)   // kernels (bit = RESTIR_K_*) bracketed by HIP events when timing is on
     uint32_t final_blocks = 0;
     uint32_t final_lds = 1;
     uint32_t final_2d = 1;
+    uint32_t final_sort = 0;       // N = 1: bin each tile's shadow rays by target before tracing
 };
 
 // Dynamic tile queue for persistent grids: a never-reset ticket counter; a launch hands out tickets

@@ -21,7 +21,8 @@ import numpy as np  # noqa: E402
 from romis_amd import _abi, restir, scene  # noqa: E402
 
 DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 1, "ris.queue": 0,
-            "spatial.xcd": 1, "spatial.blocks": 0, "final.blocks": 0, "final.lds": 1, "final.2d": 1}
+            "spatial.xcd": 1, "spatial.blocks": 0, "bvh.max_leaf": 2, "final.blocks": 0, "final.lds": 1, "final.2d": 1,
+            "final.sort": 0}
 
 VARIANTS = {
     "default": {},
@@ -38,6 +39,12 @@ VARIANTS = {
     "ris_q2560": {"ris.queue": 2560},
     "ris_q1024": {"ris.queue": 1024},
     "spatial_noxcd": {"spatial.xcd": 0},
+    "final_sort": {"final.sort": 1},
+    "bvh_leaf1": {"bvh.max_leaf": 1},
+    "bvh_leaf3": {"bvh.max_leaf": 3},
+    "bvh_leaf4": {"bvh.max_leaf": 4},
+    "bvh_leaf1_sort": {"bvh.max_leaf": 1, "final.sort": 1},
+    "bvh_leaf8": {"bvh.max_leaf": 8},
     "spatial_p1024": {"spatial.blocks": 1024},
     "spatial_p2048": {"spatial.blocks": 2048},
     "spatial_p4096": {"spatial.blocks": 4096},
@@ -61,7 +68,9 @@ def main():
     variants = {k: v for k, v in VARIANTS.items() if not args.only or k in args.only}
     W, H = args.width, args.height
     r = restir.Renderer(0)
-    r.set_scene(scene.bench_scene(args.scene))
+    sc = scene.bench_scene(args.scene)
+    r.set_scene(sc)
+    prev_leaf = 2
     cam = scene.camera_for(args.scene, W, H)
     f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=1, temporal_reuse=0)
     ref_rgb = None
@@ -74,6 +83,9 @@ def main():
                     setattr(fv, k[1:], v)
                 else:
                     r.set_tuning(k, v)
+            if "bvh.max_leaf" in knobs or prev_leaf != knobs.get("bvh.max_leaf", 2):
+                r.set_scene(sc)            # the BVH is built at set_scene
+                prev_leaf = knobs.get("bvh.max_leaf", 2)
             r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
             rgb, _ = r.render_restir(None, cam, W, H, fv, want_grid=False)   # warm + result check
             if ref_rgb is None:

@@ -155,7 +155,25 @@ typedef struct restir_tile {
 restir_status restir_tile_plan(uint32_t global_width, uint32_t global_height, uint32_t tiles_x, uint32_t tiles_y,
                                uint32_t rank, uint32_t ghost, restir_tile* out);
 
+/* Reservoir halo exchange between tiles (multi-GPU frames with temporal reuse).  In halo mode a
+ * rank computes RIS / temporal / spatial / final only on its owned tile; before every spatial pass the
+ * reservoirs within `radius` of a tile border are exchanged with the adjacent ranks.  restir_halo_plan lists,
+ * for `rank`, one segment per adjacent rank (ascending rank order): `send[i]` = the rectangle of this rank's
+ * owned pixels that rank send[i].rank reads, `recv[i]` = the rectangle of that rank's owned pixels this rank
+ * reads.  A segment's bytes = w * h * N * 32, laid out [sub-reservoir j][pixel row-major][res_a, res_b];
+ * `offset` is its byte offset in the contiguous send / recv buffer (segments back to back in list order).
+ * Pure host; every rank computes the same plan.  *count: in = capacity (>= 8 suffices), out = segments. */
+typedef struct restir_halo_segment {
+    uint32_t rank;
+    uint32_t x0, y0, width, height;          /* global pixel rectangle */
+    uint64_t offset, bytes;
+} restir_halo_segment;
+restir_status restir_halo_plan(uint32_t global_width, uint32_t global_height, uint32_t tiles_x, uint32_t tiles_y,
+                               uint32_t rank, uint32_t radius, uint32_t N, restir_halo_segment* send,
+                               restir_halo_segment* recv, uint32_t* count);
+
 /* ---- context ----------------------------------------------------------------------------------------- */
+/* (halo-mode frame functions: after the render / stage API below) */
 typedef struct restir_ctx   restir_ctx;
 typedef struct restir_frame restir_frame;
 
@@ -231,6 +249,26 @@ restir_status restir_stage_final(restir_ctx* ctx, const restir_camera* cam, cons
 /* Device portable powf / expf over arrays (parity of the device math with the oracle's). */
 restir_status restir_debug_math(restir_ctx* ctx, const float* x, const float* y, float* out_pow, float* out_exp,
                                 size_t n);
+
+/* ---- halo-mode frames (multi-GPU tiles with temporal reuse) ----------------------------------------------
+ * The stages of restir_render for rank `rank` of a tiles_x x tiles_y split, with the spatial passes' ghost
+ * zone replaced by a reservoir exchange (restir_halo_plan).  Per frame:
+ *   restir_halo_begin   primary rays on the tile + radius ring, RIS and temporal reuse on the owned tile;
+ *                       returns the pack / unpack buffer sizes
+ *   per spatial pass:   restir_halo_pack(send) -> move segment i of send to rank send[i].rank and receive
+ *                       recv[i] from rank recv[i].rank (RCCL ncclSend/ncclRecv, torch.distributed, ...) ->
+ *                       restir_halo_unpack(recv) -> restir_halo_spatial
+ *   restir_halo_end     final shading of the owned tile; *out_next = the grid for the next frame's temporal reuse
+ * Bit-identical to the same pixels of a single-GPU restir_render frame.  Buffers are device memory (or host
+ * memory when host_memory != 0, staged by the library); pack returns after the buffer is written, unpack
+ * expects the received bytes complete when called. */
+restir_status restir_halo_begin(restir_ctx* ctx, const restir_camera* cam, const restir_features* features,
+                                uint32_t width, uint32_t height, uint32_t tiles_x, uint32_t tiles_y, uint32_t rank,
+                                const restir_frame* prev, uint64_t* send_bytes, uint64_t* recv_bytes);
+restir_status restir_halo_pack(restir_ctx* ctx, void* send_buf, uint64_t bytes, int host_memory);
+restir_status restir_halo_unpack(restir_ctx* ctx, const void* recv_buf, uint64_t bytes, int host_memory);
+restir_status restir_halo_spatial(restir_ctx* ctx);
+restir_status restir_halo_end(restir_ctx* ctx, restir_frame** out_next, float* out_rgb);
 
 /* Measured HBM read bandwidth of this device (the roofline's practical ceiling next to the 8 TB/s spec): a
  * streaming-read kernel over `bytes` (rounded down to 16 B; pass >= 1 GiB to defeat the 256 MB Infinity

@@ -67,6 +67,11 @@ class Features(C.Structure):
                 ("gamma", C.c_float), ("exposure", C.c_float)]
 
 
+class HaloSegment(C.Structure):
+    _fields_ = [("rank", C.c_uint32), ("x0", C.c_uint32), ("y0", C.c_uint32), ("width", C.c_uint32),
+                ("height", C.c_uint32), ("offset", C.c_uint64), ("bytes", C.c_uint64)]
+
+
 class Tile(C.Structure):
     _fields_ = [("global_width", C.c_uint32), ("global_height", C.c_uint32),
                 ("x0", C.c_uint32), ("y0", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32),
@@ -124,6 +129,15 @@ SIGNATURES = {
     "restir_stage_final": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Features)]),
     "restir_debug_math": (C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                     C.POINTER(C.c_float), C.c_size_t]),
+    "restir_halo_plan": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                   C.c_uint32, C.POINTER(HaloSegment), C.POINTER(HaloSegment),
+                                   C.POINTER(C.c_uint32)]),
+    "restir_halo_begin": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Features), C.c_uint32, C.c_uint32, C.c_uint32,
+                                    C.c_uint32, C.c_uint32, _P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "restir_halo_pack": (C.c_int, [_P, _P, C.c_uint64, C.c_int]),
+    "restir_halo_unpack": (C.c_int, [_P, _P, C.c_uint64, C.c_int]),
+    "restir_halo_spatial": (C.c_int, [_P]),
+    "restir_halo_end": (C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_float)]),
     "restir_measure_read_bandwidth": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
     "restir_enable_timing": (C.c_int, [_P, C.c_int]),
     "restir_set_tuning": (C.c_int, [_P, C.c_char_p, C.c_int]),

@@ -1005,6 +1005,46 @@ extern "C" __global__ void k_debug_math(const float* x, const float* y, float* p
     ex[i] = pm_expf(x[i]);
 }
 
+// Halo exchange (restir_halo_pack / restir_halo_unpack): segment i's pixels, row-major, each as N x (res_a,
+// res_b) pairs laid out [j][pixel] inside the segment (include/restir_c.h, restir_halo_plan).
+__device__ __forceinline__ bool halo_locate(const HaloSegs& hs, uint32_t g, uint32_t& seg, uint32_t& x, uint32_t& y) {
+    if (g >= hs.px0[hs.n]) return false;
+    seg = 0;
+    while (g >= hs.px0[seg + 1]) seg++;
+    const uint32_t l = g - hs.px0[seg];
+    x = hs.x0[seg] + l % hs.w[seg];
+    y = hs.y0[seg] + l / hs.w[seg];
+    return true;
+}
+
+extern "C" __global__ __launch_bounds__(256) void k_halo_pack(Region rg, HaloSegs hs, uint32_t N, const float4* __restrict__ ra,
+                                                             const float4* __restrict__ rb, float4* __restrict__ out) {
+    uint32_t seg, x, y;
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!halo_locate(hs, g, seg, x, y)) return;
+    const size_t npx = (size_t)rg.vw * rg.vh, p = (size_t)(y - rg.vy0) * rg.vw + (x - rg.vx0);
+    const uint32_t spx = hs.px0[seg + 1] - hs.px0[seg], l = g - hs.px0[seg];
+    for (uint32_t j = 0; j < N; j++) {
+        const size_t o = 2 * ((size_t)hs.px0[seg] * N + (size_t)j * spx + l);
+        out[o] = ra[j * npx + p];
+        out[o + 1] = rb[j * npx + p];
+    }
+}
+
+extern "C" __global__ __launch_bounds__(256) void k_halo_unpack(Region rg, HaloSegs hs, uint32_t N, const float4* __restrict__ in,
+                                                               float4* __restrict__ ra, float4* __restrict__ rb) {
+    uint32_t seg, x, y;
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!halo_locate(hs, g, seg, x, y)) return;
+    const size_t npx = (size_t)rg.vw * rg.vh, p = (size_t)(y - rg.vy0) * rg.vw + (x - rg.vx0);
+    const uint32_t spx = hs.px0[seg + 1] - hs.px0[seg], l = g - hs.px0[seg];
+    for (uint32_t j = 0; j < N; j++) {
+        const size_t o = 2 * ((size_t)hs.px0[seg] * N + (size_t)j * spx + l);
+        ra[j * npx + p] = in[o];
+        rb[j * npx + p] = in[o + 1];
+    }
+}
+
 // Streaming read (restir_measure_read_bandwidth): grid-stride 16-byte loads, 4 in flight per lane, one partial
 // sum per block so nothing is dead code.
 extern "C" __global__ __launch_bounds__(256) void k_read_stream(const float4* __restrict__ buf, size_t n4, float* sink) {
@@ -1118,6 +1158,22 @@ hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev&
     }
     hipLaunchKernelGGL(k, grid_capped(items_of(rg), tu.final_blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,
                        o[0], o[1], o[2], n_t, p_mat, ra, rb, rgb);
+    return hipGetLastError();
+}
+
+hipError_t launch_halo_pack(const Region& rg, const HaloSegs& hs, uint32_t N, const float4* ra, const float4* rb, float4* out,
+                            hipStream_t stream) {
+    const uint32_t n = hs.px0[hs.n];
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_halo_pack, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, rg, hs, N, ra, rb, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_halo_unpack(const Region& rg, const HaloSegs& hs, uint32_t N, const float4* in, float4* ra, float4* rb,
+                              hipStream_t stream) {
+    const uint32_t n = hs.px0[hs.n];
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_halo_unpack, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, rg, hs, N, in, ra, rb);
     return hipGetLastError();
 }
 

@@ -20,6 +20,10 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg, const FeaturesDev
 hipError_t launch_final(const SceneDev& s, const Region& rg, const FeaturesDev& f, const float* origin,
                         const float4* n_t, const float4* p_mat, const float4* ra, const float4* rb, float* rgb,
                         const Tuning& tu, hipStream_t stream);
+hipError_t launch_halo_pack(const Region& rg, const HaloSegs& hs, uint32_t N, const float4* ra, const float4* rb, float4* out,
+                            hipStream_t stream);
+hipError_t launch_halo_unpack(const Region& rg, const HaloSegs& hs, uint32_t N, const float4* in, float4* ra, float4* rb,
+                              hipStream_t stream);
 hipError_t launch_read_stream(const float4* buf, size_t n4, float* sink, hipStream_t stream);
 hipError_t launch_debug_math(const float* x, const float* y, float* pw, float* ex, uint32_t n, hipStream_t stream);
 

@@ -119,6 +119,19 @@ struct restir_ctx {
     uint32_t seed = RESTIR_DEFAULT_SEED;
     uint32_t frame_index = 0;
 
+    // halo-mode frame in flight (restir_halo_begin .. restir_halo_end)
+    struct {
+        bool active = false;
+        uint32_t W = 0, H = 0, frame = 0, pass = 0, passes = 0;
+        Region view{}, owned{};
+        FeaturesDev f{};
+        CameraDev camd{};
+        HaloSegs send{}, recv{};
+        uint64_t send_bytes = 0, recv_bytes = 0;
+        int cur = 0;
+    } halo;
+    DevBuf halo_scratch;
+
     // stage API region
     Region stage_rg{};
     bool stage_ok = false;
@@ -219,6 +232,48 @@ restir_status restir_tile_plan(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_
     const uint32_t gy1 = std::min<uint64_t>((uint64_t)t.y0 + t.height + ghost, H);
     t.gx0 = gx0; t.gy0 = gy0; t.gwidth = gx1 - gx0; t.gheight = gy1 - gy0;
     *out = t;
+    return RESTIR_OK;
+}
+
+restir_status restir_halo_plan(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t tiles_y, uint32_t rank, uint32_t radius,
+                               uint32_t N, restir_halo_segment* send, restir_halo_segment* recv, uint32_t* count) {
+    if (!count || !send || !recv || N == 0) return fail(RESTIR_ERR_INVALID, "restir_halo_plan: null argument / N = 0");
+    restir_tile me{};
+    ST_TRY(restir_tile_plan(W, H, tiles_x, tiles_y, rank, 0, &me));
+    struct R { uint64_t x0, y0, x1, y1; };
+    auto grow = [&](const restir_tile& t) {
+        return R{t.x0 > radius ? t.x0 - radius : 0u, t.y0 > radius ? t.y0 - radius : 0u,
+                 std::min<uint64_t>((uint64_t)t.x0 + t.width + radius, W), std::min<uint64_t>((uint64_t)t.y0 + t.height + radius, H)};
+    };
+    auto owned = [](const restir_tile& t) { return R{t.x0, t.y0, (uint64_t)t.x0 + t.width, (uint64_t)t.y0 + t.height}; };
+    auto meet = [](R a, R b) {
+        R r{std::max(a.x0, b.x0), std::max(a.y0, b.y0), std::min(a.x1, b.x1), std::min(a.y1, b.y1)};
+        if (r.x1 <= r.x0 || r.y1 <= r.y0) r = R{0, 0, 0, 0};
+        return r;
+    };
+    const uint32_t cap = *count;
+    uint32_t n = 0;
+    uint64_t so = 0, ro = 0;
+    for (uint32_t q = 0; q < tiles_x * tiles_y; q++) {
+        if (q == rank) continue;
+        restir_tile tq{};
+        ST_TRY(restir_tile_plan(W, H, tiles_x, tiles_y, q, 0, &tq));
+        const R s_ = meet(owned(me), grow(tq)), r_ = meet(owned(tq), grow(me));
+        if (s_.x1 == 0 || r_.x1 == 0) continue;
+        if (n >= cap) return fail(RESTIR_ERR_INVALID, "restir_halo_plan: more than %u segments", cap);
+        auto fill = [&](restir_halo_segment& g, R r, uint64_t& off) {
+            g.rank = q;
+            g.x0 = (uint32_t)r.x0; g.y0 = (uint32_t)r.y0;
+            g.width = (uint32_t)(r.x1 - r.x0); g.height = (uint32_t)(r.y1 - r.y0);
+            g.offset = off;
+            g.bytes = (uint64_t)g.width * g.height * N * 32u;
+            off += g.bytes;
+        };
+        fill(send[n], s_, so);
+        fill(recv[n], r_, ro);
+        n++;
+    }
+    *count = n;
     return RESTIR_OK;
 }
 
@@ -393,7 +448,7 @@ void restir_destroy(restir_ctx* c) {
         (void)hipStreamSynchronize(c->stream);
         for (DevBuf* b : {&c->nodes, &c->tri_v0, &c->tri_e1, &c->tri_e2, &c->tri_n0, &c->tri_n1, &c->tri_n2,
                           &c->materials, &c->lights, &c->n_t, &c->p_mat, &c->ra[0], &c->ra[1], &c->rb[0], &c->rb[1],
-                          &c->dbg[0], &c->dbg[1], &c->rgb, &c->queue_ctr})
+                          &c->dbg[0], &c->dbg[1], &c->rgb, &c->queue_ctr, &c->halo_scratch})
             b->release();
         for (Pending& p : c->pending) { (void)hipEventDestroy(p.start); (void)hipEventDestroy(p.stop); }
         for (hipEvent_t ev : c->free_events) (void)hipEventDestroy(ev);
@@ -602,8 +657,8 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
             return fail(RESTIR_ERR_INVALID, "temporal predecessor grid does not match this frame's region / N");
         const bool has_ghost = t.gwidth != t.width || t.gheight != t.height;
         if (has_ghost && passes > 0)
-            return fail(RESTIR_ERR_UNSUPPORTED, "temporal reuse on a ghost-zoned tile needs the predecessor's ghost zone "
-                                                "(halo exchange not implemented)");
+            return fail(RESTIR_ERR_UNSUPPORTED, "temporal reuse on a ghost-zoned tile needs the predecessor's ghost zone: "
+                                                "render such tiles with the halo-exchange stages (restir_halo_begin)");
     }
 
     ST_TRY(ensure_work(c, t.gwidth, t.gheight, N, false));
@@ -885,6 +940,163 @@ restir_status restir_measure_read_bandwidth(restir_ctx* c, uint64_t bytes, uint3
     sink.release();
     if (e != hipSuccess) return fail(RESTIR_ERR_HIP, "read-bandwidth kernel: %s", hipGetErrorString(e));
     *out_gbps = (double)n4 * 16.0 * iters / (ms * 1e-3) / 1e9;
+    return RESTIR_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// halo-mode frames (include/restir_c.h "Reservoir halo exchange"): the stages of restir_render with the
+// ghost-zone recomputation replaced by an exchange of the owned border strips before each spatial pass
+namespace {
+restir_status to_segs(const restir_halo_segment* g, uint32_t n, HaloSegs& hs, uint64_t& bytes) {
+    if (n > RESTIR_MAX_HALO_SEGS) return fail(RESTIR_ERR_INVALID, "halo: %u segments", n);
+    hs = HaloSegs{};
+    hs.n = n;
+    uint64_t px = 0;
+    bytes = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        hs.x0[i] = g[i].x0; hs.y0[i] = g[i].y0; hs.w[i] = g[i].width; hs.h[i] = g[i].height;
+        hs.px0[i] = (uint32_t)px;
+        px += (uint64_t)g[i].width * g[i].height;
+        bytes += g[i].bytes;
+    }
+    if (px >= (1ull << 31)) return fail(RESTIR_ERR_INVALID, "halo: %llu pixels", (unsigned long long)px);
+    hs.px0[n] = (uint32_t)px;
+    return RESTIR_OK;
+}
+}  // namespace
+
+restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const restir_features* features, uint32_t width,
+                                uint32_t height, uint32_t tiles_x, uint32_t tiles_y, uint32_t rank, const restir_frame* prev,
+                                uint64_t* send_bytes, uint64_t* recv_bytes) {
+    if (!c || !cam) return fail(RESTIR_ERR_INVALID, "null argument");
+    ST_TRY(check_features(features));
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->has_scene) return fail(RESTIR_ERR_STATE, "restir_halo_begin before restir_set_scene");
+    HIP_TRY(hipSetDevice(c->device));
+    const FeaturesDev f = to_dev(features);
+    const uint32_t passes = features->spatial_reuse ? features->spatial_resampling_passes : 0u;
+    restir_tile t{};
+    ST_TRY(restir_tile_plan(width, height, tiles_x, tiles_y, rank, passes ? f.R : 0u, &t));
+    restir_halo_segment sg[RESTIR_MAX_HALO_SEGS], rg_[RESTIR_MAX_HALO_SEGS];
+    uint32_t n = RESTIR_MAX_HALO_SEGS;
+    ST_TRY(restir_halo_plan(width, height, tiles_x, tiles_y, rank, f.R, f.N, sg, rg_, &n));
+    auto& h = c->halo;
+    ST_TRY(to_segs(sg, n, h.send, h.send_bytes));
+    ST_TRY(to_segs(rg_, n, h.recv, h.recv_bytes));
+    if (!passes) { h.send.n = h.recv.n = 0; h.send.px0[0] = h.recv.px0[0] = 0; h.send_bytes = h.recv_bytes = 0; }
+    const bool temporal = features->temporal_reuse && prev != nullptr;
+    if (temporal && (prev->N != f.N || prev->vw != t.gwidth || prev->vh != t.gheight || prev->vx0 != t.gx0 ||
+                     prev->vy0 != t.gy0 || prev->W != width || prev->H != height))
+        return fail(RESTIR_ERR_INVALID, "temporal predecessor grid does not match this tile's view / N");
+    ST_TRY(ensure_work(c, t.gwidth, t.gheight, f.N, false));
+    ST_TRY(c->rgb.ensure((size_t)t.width * t.height * 12));
+    c->rgb_w = t.width; c->rgb_h = t.height;
+    h.W = width; h.H = height;
+    h.view = make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.gx0, t.gy0, t.gwidth, t.gheight);
+    h.owned = make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.x0, t.y0, t.width, t.height);
+    h.f = f;
+    h.camd = camera_dev(cam);
+    h.frame = c->frame_index++;
+    h.pass = 0;
+    h.passes = passes;
+    h.cur = 0;
+    const SceneDev& s = c->sdev;
+    float4* nt = c->n_t.as<float4>();
+    float4* pm = c->p_mat.as<float4>();
+    // G-buffer on the whole view (the spatial passes read the neighbours' depth / normal / position),
+    // reservoirs only on the owned rectangle
+    TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, h.view, h.camd, nt, pm, c->tuning, c->stream));
+    TIMED(c, RESTIR_K_RIS, launch_ris(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_RIS, 0), h.camd.origin,
+                                      nt, pm, c->ra[0].as<float4>(), c->rb[0].as<float4>(), nullptr, c->tuning, c->queue,
+                                      c->stream));
+    if (temporal)
+        TIMED(c, RESTIR_K_TEMPORAL,
+              launch_temporal(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_TEMPORAL, 0), h.camd.origin, nt,
+                              pm, c->ra[0].as<float4>(), c->rb[0].as<float4>(), prev->a.as<float4>(), prev->b.as<float4>(),
+                              c->ra[0].as<float4>(), c->rb[0].as<float4>(), nullptr, c->tuning, c->stream));
+    h.active = true;
+    if (send_bytes) *send_bytes = h.send_bytes;
+    if (recv_bytes) *recv_bytes = h.recv_bytes;
+    return RESTIR_OK;
+}
+
+restir_status restir_halo_pack(restir_ctx* c, void* buf, uint64_t bytes, int host_memory) {
+    if (!c || (bytes && !buf)) return fail(RESTIR_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    auto& h = c->halo;
+    if (!h.active || h.pass >= h.passes) return fail(RESTIR_ERR_STATE, "restir_halo_pack outside a halo frame's passes");
+    if (bytes != h.send_bytes) return fail(RESTIR_ERR_INVALID, "halo send buffer is %llu bytes, plan needs %llu",
+                                           (unsigned long long)bytes, (unsigned long long)h.send_bytes);
+    HIP_TRY(hipSetDevice(c->device));
+    float4* dst = static_cast<float4*>(buf);
+    if (host_memory) { ST_TRY(c->halo_scratch.ensure(bytes)); dst = c->halo_scratch.as<float4>(); }
+    HIP_TRY(launch_halo_pack(h.view, h.send, h.f.N, c->ra[h.cur].as<float4>(), c->rb[h.cur].as<float4>(), dst, c->stream));
+    if (host_memory && bytes) HIP_TRY(hipMemcpyAsync(buf, dst, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));   // the caller's transport reads the buffer next
+    return RESTIR_OK;
+}
+
+restir_status restir_halo_unpack(restir_ctx* c, const void* buf, uint64_t bytes, int host_memory) {
+    if (!c || (bytes && !buf)) return fail(RESTIR_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    auto& h = c->halo;
+    if (!h.active || h.pass >= h.passes) return fail(RESTIR_ERR_STATE, "restir_halo_unpack outside a halo frame's passes");
+    if (bytes != h.recv_bytes) return fail(RESTIR_ERR_INVALID, "halo recv buffer is %llu bytes, plan needs %llu",
+                                           (unsigned long long)bytes, (unsigned long long)h.recv_bytes);
+    HIP_TRY(hipSetDevice(c->device));
+    const float4* src = static_cast<const float4*>(buf);
+    if (host_memory && bytes) {
+        ST_TRY(c->halo_scratch.ensure(bytes));
+        HIP_TRY(hipMemcpyAsync(c->halo_scratch.p, buf, bytes, hipMemcpyHostToDevice, c->stream));
+        src = c->halo_scratch.as<float4>();
+    }
+    HIP_TRY(launch_halo_unpack(h.view, h.recv, h.f.N, src, c->ra[h.cur].as<float4>(), c->rb[h.cur].as<float4>(), c->stream));
+    if (host_memory) HIP_TRY(hipStreamSynchronize(c->stream));   // the host buffer may be reused on return
+    return RESTIR_OK;
+}
+
+restir_status restir_halo_spatial(restir_ctx* c) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    auto& h = c->halo;
+    if (!h.active || h.pass >= h.passes) return fail(RESTIR_ERR_STATE, "restir_halo_spatial: no pass left");
+    HIP_TRY(hipSetDevice(c->device));
+    const int nxt = h.cur ^ 1;
+    TIMED(c, RESTIR_K_SPATIAL,
+          launch_spatial(c->sdev, h.owned, h.f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_SPATIAL, h.pass), h.camd.origin,
+                         c->n_t.as<float4>(), c->p_mat.as<float4>(), c->ra[h.cur].as<float4>(), c->rb[h.cur].as<float4>(),
+                         c->ra[nxt].as<float4>(), c->rb[nxt].as<float4>(), nullptr, c->tuning, c->stream));
+    h.cur = nxt;
+    h.pass++;
+    return RESTIR_OK;
+}
+
+restir_status restir_halo_end(restir_ctx* c, restir_frame** out_next, float* out_rgb) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    if (out_next) *out_next = nullptr;
+    std::lock_guard<std::mutex> lk(c->mu);
+    auto& h = c->halo;
+    if (!h.active || h.pass != h.passes)
+        return fail(RESTIR_ERR_STATE, "restir_halo_end after %u of %u spatial passes", h.pass, h.passes);
+    HIP_TRY(hipSetDevice(c->device));
+    TIMED(c, RESTIR_K_FINAL, launch_final(c->sdev, h.owned, h.f, h.camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
+                                          c->ra[h.cur].as<float4>(), c->rb[h.cur].as<float4>(), c->rgb.as<float>(), c->tuning,
+                                          c->stream));
+    c->cur = h.cur;
+    h.active = false;
+    if (out_next) {
+        restir_frame* fr = new restir_frame();
+        fr->device = c->device;
+        fr->W = h.W; fr->H = h.H; fr->vx0 = h.view.vx0; fr->vy0 = h.view.vy0; fr->vw = h.view.vw; fr->vh = h.view.vh;
+        fr->N = h.f.N;
+        std::swap(fr->a, c->ra[h.cur]);
+        std::swap(fr->b, c->rb[h.cur]);
+        *out_next = fr;
+    }
+    if (out_rgb) {
+        HIP_TRY(hipMemcpyAsync(out_rgb, c->rgb.p, (size_t)h.owned.rw * h.owned.rh * 12, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
     return RESTIR_OK;
 }
 

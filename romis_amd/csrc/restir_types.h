@@ -80,6 +80,14 @@ struct WorkQueue {
     uint32_t base;
 };
 
+// Halo segments of one exchange (restir_halo_plan), pixel prefix offsets into the packed buffer.
+#define RESTIR_MAX_HALO_SEGS 8u
+struct HaloSegs {
+    uint32_t n;
+    uint32_t x0[RESTIR_MAX_HALO_SEGS], y0[RESTIR_MAX_HALO_SEGS], w[RESTIR_MAX_HALO_SEGS], h[RESTIR_MAX_HALO_SEGS];
+    uint32_t px0[RESTIR_MAX_HALO_SEGS + 1];   // px0[i] = pixels before segment i; px0[n] = total
+};
+
 // Host side of the queue: the context's counter and the next launch's base.
 struct QueueState {
     uint32_t* ctr = nullptr;

@@ -85,6 +85,32 @@ class Renderer:
               "restir_download_rgb")
         return rgb
 
+    # ---- halo-mode frames (include/restir_c.h "halo-mode frames") -------------------------------------
+    def halo_begin(self, prev, camera, width, height, features, tiles, rank):
+        """Primary rays on the tile + ring, RIS / temporal on the owned tile.  Returns (send_bytes, recv_bytes)."""
+        sb, rb_ = C.c_uint64(), C.c_uint64()
+        check(self.lib, self.lib.restir_halo_begin(self.ctx, C.byref(camera), C.byref(features), width, height, tiles[0],
+                                                   tiles[1], rank, prev.handle if prev is not None else None,
+                                                   C.byref(sb), C.byref(rb_)), "restir_halo_begin")
+        return sb.value, rb_.value
+
+    def halo_pack(self, buf_ptr: int, nbytes: int, host: bool) -> None:
+        check(self.lib, self.lib.restir_halo_pack(self.ctx, buf_ptr, nbytes, int(host)), "restir_halo_pack")
+
+    def halo_unpack(self, buf_ptr: int, nbytes: int, host: bool) -> None:
+        check(self.lib, self.lib.restir_halo_unpack(self.ctx, buf_ptr, nbytes, int(host)), "restir_halo_unpack")
+
+    def halo_spatial(self) -> None:
+        check(self.lib, self.lib.restir_halo_spatial(self.ctx), "restir_halo_spatial")
+
+    def halo_end(self, tile, want_rgb: bool = True, want_grid: bool = True):
+        out = C.c_void_p()
+        rgb = np.zeros((tile.height, tile.width, 3), np.float32) if want_rgb else None
+        check(self.lib, self.lib.restir_halo_end(self.ctx, C.byref(out) if want_grid else None,
+                                                 rgb.ctypes.data_as(C.POINTER(C.c_float)) if want_rgb else None),
+              "restir_halo_end")
+        return rgb, (ReservoirGrid(self.lib, out) if want_grid and out.value else None)
+
     def measure_read_bandwidth(self, nbytes: int = 4 << 30, iters: int = 10) -> float:
         """GB/s of a streaming-read kernel over `nbytes` of HBM (restir_measure_read_bandwidth)."""
         out = C.c_double()
@@ -166,6 +192,17 @@ class Renderer:
 
 def rng_key(seed: int, frame: int, stage: int, pass_: int = 0) -> int:
     return _abi.load_library().restir_rng_key(seed, frame, stage, pass_)
+
+
+def halo_plan(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, radius: int, N: int):
+    """restir_halo_plan: ([send segments], [recv segments]) for `rank`, one pair per adjacent rank."""
+    lib = _abi.load_library()
+    send = (_abi.HaloSegment * 8)()
+    recv = (_abi.HaloSegment * 8)()
+    n = C.c_uint32(8)
+    check(lib, lib.restir_halo_plan(width, height, tiles_x, tiles_y, rank, radius, N, send, recv, C.byref(n)),
+          "restir_halo_plan")
+    return list(send[:n.value]), list(recv[:n.value])
 
 
 def tile_plan(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, ghost: int) -> _abi.Tile:

@@ -86,3 +86,29 @@ def test_context_calls_fail_cleanly_on_null(abi_lib):
     assert abi_lib.restir_set_seed(None, 1, 2) == 1
     assert abi_lib.restir_synchronize(None) == 1
     assert abi_lib.restir_render(None, None, None, 1, 1, None, None, None, None) == 1
+
+
+@pytest.mark.parametrize("W,H,tx,ty,R,N", [(72, 40, 2, 1, 10, 1), (97, 61, 2, 2, 10, 2), (3840, 2160, 4, 2, 10, 1),
+                                          (50, 30, 4, 2, 7, 1)])
+def test_halo_plan_is_symmetric_and_covers_the_ring(abi_lib, W, H, tx, ty, R, N):
+    from romis_amd import restir
+    plans = {q: restir.halo_plan(W, H, tx, ty, q, R, N) for q in range(tx * ty)}
+    for q, (send, recv) in plans.items():
+        assert [s.rank for s in send] == [r.rank for r in recv] == sorted(s.rank for s in send)
+        off = 0
+        for s in send:
+            assert s.offset == off and s.bytes == s.width * s.height * N * 32
+            off += s.bytes
+        # what q sends to p is exactly what p expects from q
+        for s in send:
+            peer_recv = {r.rank: r for r in plans[s.rank][1]}[q]
+            assert (peer_recv.x0, peer_recv.y0, peer_recv.width, peer_recv.height) == (s.x0, s.y0, s.width, s.height)
+        # the received rectangles tile the ring: (owned grown by R, clipped) minus owned
+        t = restir.tile_plan(W, H, tx, ty, q, R)
+        cover = np.zeros((H, W), np.int32)
+        for r in recv:
+            cover[r.y0:r.y0 + r.height, r.x0:r.x0 + r.width] += 1
+        want = np.zeros((H, W), np.int32)
+        want[t.gy0:t.gy0 + t.gheight, t.gx0:t.gx0 + t.gwidth] = 1
+        want[t.y0:t.y0 + t.height, t.x0:t.x0 + t.width] = 0
+        assert np.array_equal(cover, want)

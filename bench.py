@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
                     help="BASELINE.json config (c2 = configs[1], the headline)")
     ap.add_argument("--scene", default=None, help="override the config's scene")
+    ap.add_argument("--mode", default="auto", choices=["auto", "ghost", "halo"],
+                    help="multi-GPU tiles: recompute a ghost zone (no communication) or exchange reservoir halos "
+                         "over RCCL before each spatial pass; auto = halo when temporal reuse is on")
     ap.add_argument("--M", type=int, default=None, help="override the config's M")
     ap.add_argument("--N", type=int, default=1)
     ap.add_argument("--k", type=int, default=5)
@@ -206,8 +209,8 @@ def main():
         GW, GH, scaling = tx * tw, ty * th, "weak"
     else:
         GW, GH, scaling = cf["image"][0], cf["image"][1], "strong"
-    if cf["temporal"] and world > 1:
-        raise SystemExit(f"{args.config}: temporal reuse runs on one GPU (BASELINE.json configs[2])")
+    # multi-GPU temporal reuse needs the predecessor's reservoirs around each tile: halo-exchange frames
+    halo = world > 1 and (args.mode == "halo" or (args.mode == "auto" and cf["temporal"]))
     sc = scene.bench_scene(cf["scene"])
     cam = scene.camera_for(cf["scene"], GW, GH)
     passes = cf["passes"]
@@ -223,9 +226,17 @@ def main():
     r.set_scene(sc)
     r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
     state = {"grid": None}
+    hf = None
+    if halo:
+        from romis_amd import distributed
+        hf = distributed.HaloFrames(r, GW, GH, (tx, ty), rank, f)
+        tile = hf.tile
 
     def step():
-        if cf["temporal"]:   # thread the previous frame's grid (main.cpp:165)
+        if hf is not None:   # RCCL halo exchange of the reservoirs before every spatial pass
+            _, g = hf.render(state["grid"] if cf["temporal"] else None, cam, want_rgb=False, want_grid=cf["temporal"])
+            state["grid"] = g
+        elif cf["temporal"]:   # thread the previous frame's grid (main.cpp:165)
             _, g = r.render_restir(state["grid"], cam, GW, GH, f, tile=tile, want_rgb=False, want_grid=True)
             state["grid"] = g   # the previous handle is released when dropped
         else:
@@ -266,14 +277,14 @@ def main():
            "tile": [tile.width, tile.height] if scaling == "strong" else [GW // tx, GH // ty], "image": [GW, GH],
            "tiles": [tx, ty], "M": cf["M"], "N": args.N, "k": args.k, "r": args.r, "passes": passes,
            "temporal": cf["temporal"], "unbiased": cf["unbiased"], "spatial_visibility": cf["vis"],
-           "parallelism": f"screen tiles {tx}x{ty}, ghost {ghost}px"}
+           "parallelism": f"screen tiles {tx}x{ty}, " + (f"RCCL reservoir halo {args.r}px" if halo else f"ghost {ghost}px")}
 
     # roofline of the spatial pass: algorithmic bytes per pixel = read 32 (own G-buffer) + 32 N (own
     # reservoir), write 32 N; neighbour gathers are cache traffic, not counted
     sp_ms, sp_n = kt["spatial"]
     roofline = None
     if sp_n:
-        sp_px = spatial_px_per_launch(tile, passes, args.r)
+        sp_px = tile.width * tile.height if halo else spatial_px_per_launch(tile, passes, args.r)
         bytes_per_launch = int(sp_px * (32 + 32 * args.N + 32 * args.N))
         avg_s = sp_ms / sp_n / 1e3
         achieved = bytes_per_launch / avg_s / 1e9

@@ -286,7 +286,8 @@ restir_status restir_enable_timing(restir_ctx* ctx, int enable);
 /* Launch-shape knobs (never change results): "primary.blocks|lds|2d", "ris.blocks|lds", "spatial.xcd|blocks",
  * "final.blocks|lds|2d".  *.blocks = persistent grid cap (0 = one block per work item).  "timing.mask": the
  * kernels (bit 1 << RESTIR_K_*) restir_enable_timing brackets with HIP events (default all).  "bvh.max_leaf":
- * triangles per BVH leaf for the next restir_set_scene (default 2). */
+ * triangles per BVH leaf for the next restir_set_scene (default 2).  "layout.records": restir_render's buffers as
+ * per-pixel records [n_t, res_a, res_b] (1) or SoA planes (0, default). */
 restir_status restir_set_tuning(restir_ctx* ctx, const char* key, int value);
 restir_status restir_timings(restir_ctx* ctx, double* ms /*[RESTIR_K_COUNT]*/, uint64_t* launches /*[RESTIR_K_COUNT]*/);
 restir_status restir_reset_timings(restir_ctx* ctx);

@@ -187,9 +187,12 @@ __device__ __forceinline__ Px make_px(const SceneDev& s, float4 a, float4 b, v3 
     return r;
 }
 
-__device__ __forceinline__ Px load_px(const SceneDev& s, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
-                                      size_t p, v3 origin) {
-    return make_px(s, n_t[p], p_mat[p], origin);
+__device__ __forceinline__ size_t gidx(const Region& rg, size_t p) { return p * rg.ps; }
+__device__ __forceinline__ size_t ridx(const Region& rg, uint32_t j, size_t p) { return (size_t)j * rg.js + p * rg.ps; }
+
+__device__ __forceinline__ Px load_px(const SceneDev& s, const Region& rg, const float4* __restrict__ n_t,
+                                      const float4* __restrict__ p_mat, size_t p, v3 origin) {
+    return make_px(s, n_t[gidx(rg, p)], p_mat[p], origin);
 }
 
 // |x|^n (n >= 1) by binary powering in double: exactly the product sequence of pm_powf's integer branch
@@ -355,10 +358,10 @@ __device__ __forceinline__ void sub_load(Sub& r, const float4* __restrict__ a, c
 }
 
 __device__ __forceinline__ void sub_store(const Sub& r, float4* __restrict__ a, float4* __restrict__ b,
-                                          float2* __restrict__ dbg, size_t i) {
+                                          float2* __restrict__ dbg, size_t i, size_t idbg) {
     a[i] = make_float4(r.pos.x, r.pos.y, r.pos.z, r.W);
     b[i] = make_float4(r.col.x, r.col.y, r.col.z, __uint_as_float(r.M));
-    if (dbg) dbg[i] = make_float2(r.wsum, r.chosen);
+    if (dbg) dbg[idbg] = make_float2(r.wsum, r.chosen);
 }
 
 // Neighbour (x + dx, y + dy) clamped to the image (render_utils.cpp:109-110), then -- defensively -- to the
@@ -441,7 +444,7 @@ extern __shared__ __attribute__((aligned(16))) float4 g_lds[];
 // ---------------------------------------------------------------------------------------------------------
 // k_primary: persistent blocks stage the BVH into LDS once, then sweep 32x8 tiles; writes n_t / p_mat.
 template <bool LDS_BVH>
-__device__ __forceinline__ void primary_body(const SceneDev& s, const Region& rg, const CameraDev& cam,
+__device__ __forceinline__ void primary_body(const SceneDev& s, const Region& rg, const CameraDev& cam, float4* __restrict__ n_t2,
                                              float4* __restrict__ n_t, float4* __restrict__ p_mat) {
     const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
     const uint32_t nt = work_items(rg);
@@ -467,17 +470,20 @@ __device__ __forceinline__ void primary_body(const SceneDev& s, const Region& rg
             t = ROMIS_FLT_MAX;
         }
         v3 P = vadd(o, vscale(d, t));
-        n_t[p] = make_float4(n.x, n.y, n.z, t);
+        const float4 nt = make_float4(n.x, n.y, n.z, t);
+        n_t[gidx(rg, p)] = nt;
+        if (n_t2) n_t2[gidx(rg, p)] = nt;   // the other record buffer of the ping-pong pair
         p_mat[p] = make_float4(P.x, P.y, P.z, __uint_as_float(m));
     }
 }
 
-extern "C" __global__ __launch_bounds__(256) void k_primary(SceneDev s, Region rg, CameraDev cam, float4* n_t, float4* p_mat) {
-    primary_body<false>(s, rg, cam, n_t, p_mat);
+extern "C" __global__ __launch_bounds__(256) void k_primary(SceneDev s, Region rg, CameraDev cam, float4* n_t, float4* p_mat,
+                                                           float4* n_t2) {
+    primary_body<false>(s, rg, cam, n_t2, n_t, p_mat);
 }
 extern "C" __global__ __launch_bounds__(256) void k_primary_lds(SceneDev s, Region rg, CameraDev cam, float4* n_t,
-                                                               float4* p_mat) {
-    primary_body<true>(s, rg, cam, n_t, p_mat);
+                                                               float4* p_mat, float4* n_t2) {
+    primary_body<true>(s, rg, cam, n_t2, n_t, p_mat);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -509,7 +515,7 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
         Sub r[NT > 0 ? NT : RESTIR_MAX_N_DEV];
         for (uint32_t j = 0; j < N; j++) sub_init(r[j]);
         if (L != 0) {
-            Px px = load_px(s, n_t, p_mat, p, origin);
+            Px px = load_px(s, rg, n_t, p_mat, p, origin);
             const uint32_t ps = pix_state(key, y * rg.W + x);
             for (uint32_t j = 0; j < N; j++) r[j].M = 0u;
             // A primary-ray miss carries the value-initialised HitInfo (kd = ks = 0, N = 0): its target pdf is
@@ -575,7 +581,7 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
                                                   r[j].wsum);
             }
         }
-        for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, j * npx + p);
+        for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, ridx(rg, j, p), j * npx + p);
     }
 }
 
@@ -640,12 +646,12 @@ __device__ __forceinline__ void temporal_body(const SceneDev& s, const Region& r
     if (!region_pixel(rg, blockIdx.x * blockDim.x + threadIdx.x, x, y, p)) return;
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
-    Px px = load_px(s, n_t, p_mat, p, origin);
+    Px px = load_px(s, rg, n_t, p_mat, p, origin);
     Sub cur[NT > 0 ? NT : RESTIR_MAX_N_DEV], prev[NT > 0 ? NT : RESTIR_MAX_N_DEV];
     unsigned long long mcur = 0, mprev = 0;
     for (uint32_t j = 0; j < N; j++) {
-        sub_load(cur[j], ca, cb, j * npx + p);
-        sub_load(prev[j], pa, pb, j * npx + p);
+        sub_load(cur[j], ca, cb, ridx(rg, j, p));
+        sub_load(prev[j], pa, pb, ridx(rg, j, p));
         mcur += cur[j].M;
         mprev += prev[j].M;
     }
@@ -660,7 +666,7 @@ __device__ __forceinline__ void temporal_body(const SceneDev& s, const Region& r
     for (uint32_t j = 0; j < N; j++) cmb.consume(s, f, px, cur[j], ps, 0u);
     for (uint32_t j = 0; j < N; j++) cmb.consume(s, f, px, prev[j], ps, 0u);
     cmb.finish_biased(s, f, px);
-    for (uint32_t j = 0; j < N; j++) sub_store(cmb.out[j], oa, ob, odbg, j * npx + p);
+    for (uint32_t j = 0; j < N; j++) sub_store(cmb.out[j], oa, ob, odbg, ridx(rg, j, p), j * npx + p);
 }
 
 #define ROMIS_TEMPORAL_KERNEL(NT)                                                                                      \
@@ -693,12 +699,12 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
     const uint32_t K = f.K;
-    const Px cur = load_px(s, n_t, p_mat, p, origin);
+    const Px cur = load_px(s, rg, n_t, p_mat, p, origin);
     const uint32_t ps = pix_state(key, y * rg.W + x);
     const uint32_t slot0 = 2u * K;
 #if defined(ROMIS_ABL_SPATIAL_COPY)
     if (ps != 0x9E3779B9u || cur.t != 1.0f) {
-        for (uint32_t j = 0; j < N; j++) { Sub in; sub_load(in, ia, ib, j * npx + p); sub_store(in, oa, ob, odbg, j * npx + p); }
+        for (uint32_t j = 0; j < N; j++) { Sub in; sub_load(in, ia, ib, ridx(rg, j, p)); sub_store(in, oa, ob, odbg, ridx(rg, j, p), j * npx + p); }
         return;
     }
 #endif
@@ -722,7 +728,7 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
         }
         if constexpr (!UNBIASED) {
 #pragma unroll
-            for (uint32_t i = 0; i < kBatch; i++) g[i] = n_t[q[i]];
+            for (uint32_t i = 0; i < kBatch; i++) g[i] = n_t[gidx(rg, q[i])];
         }
 #pragma unroll
         for (uint32_t i = 0; i < kBatch; i++) {
@@ -737,7 +743,12 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
             float4 a[kBatch], b[kBatch];
 #pragma unroll
             for (uint32_t i = 0; i < kBatch; i++) {
-                if (ok[i]) { a[i] = ia[q[i]]; b[i] = ib[q[i]]; }
+#if defined(ROMIS_ABL_SPATIAL_SAMELINE)
+                // ablation: the neighbour's reservoir read from the cache line its G-buffer record came from
+                if (ok[i]) { a[i] = n_t[gidx(rg, q[i])]; b[i] = make_float4(g[i].x, g[i].y, g[i].z, __uint_as_float(1u)); }
+#else
+                if (ok[i]) { a[i] = ia[gidx(rg, q[i])]; b[i] = ib[gidx(rg, q[i])]; }
+#endif
             }
             // consume in draw order with ONE inlined combine body: the batch is shifted down a register per
             // step (static indices only; a rolled loop over a[i] would spill the batch to memory)
@@ -753,7 +764,7 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
                 if (!ok[i]) continue;
                 for (uint32_t j = 0; j < N; j++) {
                     Sub in;
-                    sub_load(in, ia, ib, j * npx + q[i]);
+                    sub_load(in, ia, ib, ridx(rg, j, q[i]));
                     cmb.consume(s, f, cur, in, ps, slot0);
                 }
             }
@@ -761,7 +772,7 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
     }
     for (uint32_t j = 0; j < N; j++) {
         Sub in;
-        sub_load(in, ia, ib, j * npx + p);
+        sub_load(in, ia, ib, ridx(rg, j, p));
         cmb.consume(s, f, cur, in, ps, slot0);
     }
     if (!UNBIASED) {
@@ -777,9 +788,9 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
             size_t q = p;
             if (n < K) q = neighbour_index(rg, x, y, uniform_offset(draw(ps, 2u * n), f.R),
                                            uniform_offset(draw(ps, 2u * n + 1u), f.R));
-            Px rp = load_px(s, n_t, p_mat, q, origin);
+            Px rp = load_px(s, rg, n_t, p_mat, q, origin);
             unsigned long long tot = 0;
-            for (uint32_t j = 0; j < N; j++) tot += __float_as_uint(ib[j * npx + q].w);
+            for (uint32_t j = 0; j < N; j++) tot += __float_as_uint(ib[ridx(rg, j, q)].w);
             for (uint32_t j = 0; j < N; j++) {
                 const float pd = target_pdf(s, f, rp, cmb.out[j].pos, cmb.out[j].col);
                 if (pd > 0.0f && (!f.spatial_vis || visible(bvh, rp.P, cmb.out[j].pos))) Z[j] += tot;
@@ -791,7 +802,7 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
             else cmb.out[j].W = (rcp_rn(pc) * rcp_rn((float)Z[j])) * cmb.out[j].wsum;
         }
     }
-    for (uint32_t j = 0; j < N; j++) sub_store(cmb.out[j], oa, ob, odbg, j * npx + p);
+    for (uint32_t j = 0; j < N; j++) sub_store(cmb.out[j], oa, ob, odbg, ridx(rg, j, p), j * npx + p);
 }
 
 template <int NT, bool UNBIASED>
@@ -864,11 +875,11 @@ __device__ __forceinline__ void final_body(const SceneDev& s, const Region& rg, 
         uint32_t x, y;
         size_t p;
         if (!work_pixel(rg, tile, x, y, p)) continue;
-        Px px = load_px(s, n_t, p_mat, p, origin);
+        Px px = load_px(s, rg, n_t, p_mat, p, origin);
         v3 color = mk(0.0f, 0.0f, 0.0f);
         for (uint32_t j = 0; j < N; j++) {
             Sub r;
-            sub_load(r, ra, rb, j * npx + p);
+            sub_load(r, ra, rb, ridx(rg, j, p));
             v3 sc = shade(s, f, px, r.pos, r.col);
             // The visibility test can only matter when the shaded value is non-zero: (vis ? sc : 0) * W equals
             // sc * W when sc == 0 (both are 0 * W), so the shadow ray is skipped exactly then.
@@ -926,8 +937,8 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
     v3 sc = mk(0.0f, 0.0f, 0.0f);
     bool need = false;
     if (valid) {
-        px = load_px(s, n_t, p_mat, p, origin);
-        sub_load(r, ra, rb, p);
+        px = load_px(s, rg, n_t, p_mat, p, origin);
+        sub_load(r, ra, rb, ridx(rg, 0, p));
         sc = shade(s, f, px, r.pos, r.col);
         need = sc.x != 0.0f || sc.y != 0.0f || sc.z != 0.0f;   // see final_body: no ray when sc == 0
     }
@@ -1026,8 +1037,8 @@ extern "C" __global__ __launch_bounds__(256) void k_halo_pack(Region rg, HaloSeg
     const uint32_t spx = hs.px0[seg + 1] - hs.px0[seg], l = g - hs.px0[seg];
     for (uint32_t j = 0; j < N; j++) {
         const size_t o = 2 * ((size_t)hs.px0[seg] * N + (size_t)j * spx + l);
-        out[o] = ra[j * npx + p];
-        out[o + 1] = rb[j * npx + p];
+        out[o] = ra[ridx(rg, j, p)];
+        out[o + 1] = rb[ridx(rg, j, p)];
     }
 }
 
@@ -1040,8 +1051,8 @@ extern "C" __global__ __launch_bounds__(256) void k_halo_unpack(Region rg, HaloS
     const uint32_t spx = hs.px0[seg + 1] - hs.px0[seg], l = g - hs.px0[seg];
     for (uint32_t j = 0; j < N; j++) {
         const size_t o = 2 * ((size_t)hs.px0[seg] * N + (size_t)j * spx + l);
-        ra[j * npx + p] = in[o];
-        rb[j * npx + p] = in[o + 1];
+        ra[ridx(rg, j, p)] = in[o];
+        rb[ridx(rg, j, p)] = in[o + 1];
     }
 }
 
@@ -1080,15 +1091,15 @@ inline Region with_map(Region rg, uint32_t map2d) { rg.map2d = map2d; return rg;
 }  // namespace
 
 hipError_t launch_primary(const SceneDev& s, const Region& rg0, const CameraDev& cam, float4* n_t, float4* p_mat,
-                          const Tuning& tu, hipStream_t stream) {
+                          float4* n_t2, const Tuning& tu, hipStream_t stream) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, tu.primary_2d);
     const size_t lds = bvh_lds_bytes(s);
     const dim3 grid = grid_capped(items_of(rg), tu.primary_blocks);
     if (tu.primary_lds && lds <= kLdsBudget)
-        hipLaunchKernelGGL(k_primary_lds, grid, dim3(kBlock), lds, stream, s, rg, cam, n_t, p_mat);
+        hipLaunchKernelGGL(k_primary_lds, grid, dim3(kBlock), lds, stream, s, rg, cam, n_t, p_mat, n_t2);
     else
-        hipLaunchKernelGGL(k_primary, grid, dim3(kBlock), 0, stream, s, rg, cam, n_t, p_mat);
+        hipLaunchKernelGGL(k_primary, grid, dim3(kBlock), 0, stream, s, rg, cam, n_t, p_mat, n_t2);
     return hipGetLastError();
 }
 

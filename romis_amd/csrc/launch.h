@@ -5,8 +5,9 @@
 
 namespace romis {
 
+// n_t2 (nullable): a second record buffer that also receives the G-buffer n_t (the ping-pong partner)
 hipError_t launch_primary(const SceneDev& s, const Region& rg, const CameraDev& cam, float4* n_t, float4* p_mat,
-                          const Tuning& tu, hipStream_t stream);
+                          float4* n_t2, const Tuning& tu, hipStream_t stream);
 hipError_t launch_ris(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
                       const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, const Tuning& tu,
                       QueueState& qs, hipStream_t stream);

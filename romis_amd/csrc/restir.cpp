@@ -90,7 +90,8 @@ struct Pending {
 struct restir_frame {
     std::atomic<int> refs{1};
     int device = 0;
-    DevBuf a, b;
+    DevBuf rec;   // the frame's reservoirs over its view: per-pixel records [n_t, a_0, b_0, ...] or [a planes | b planes]
+    bool records = true;
     uint32_t W = 0, H = 0, vx0 = 0, vy0 = 0, vw = 0, vh = 0, N = 0;
 };
 
@@ -106,7 +107,8 @@ struct restir_ctx {
 
     // work buffers for one view
     uint32_t vw = 0, vh = 0, N = 0;
-    DevBuf n_t, p_mat, ra[2], rb[2], dbg[2], rgb;
+    DevBuf n_t, p_mat, ra[2], rb[2], dbg[2], rgb;   // stage API: SoA planes
+    DevBuf rec[2];                                  // restir_render / halo frames: per-pixel records
     int cur = 0;
     uint32_t rgb_w = 0, rgb_h = 0;
 
@@ -129,6 +131,7 @@ struct restir_ctx {
         HaloSegs send{}, recv{};
         uint64_t send_bytes = 0, recv_bytes = 0;
         int cur = 0;
+        bool fb_records = true;
     } halo;
     DevBuf halo_scratch;
 
@@ -394,7 +397,43 @@ Region make_region(uint32_t W, uint32_t H, uint32_t vx0, uint32_t vy0, uint32_t 
     r.W = W; r.H = H;
     r.vx0 = vx0; r.vy0 = vy0; r.vw = vw; r.vh = vh;
     r.rx0 = rx0; r.ry0 = ry0; r.rw = rw; r.rh = rh;
+    r.ps = 1; r.js = vw * vh;   // SoA planes (the stage API's buffers)
     return r;
+}
+
+// The frame path keeps one record per pixel, [n_t, res_a_0, res_b_0, res_a_1, ...]: a neighbour's depth /
+// normal test and its reservoir come from the same cache lines (the spatial pass's gathers touch one record
+// instead of three planes).
+Region with_records(Region r, uint32_t N) {
+    r.ps = 1u + 2u * N;
+    r.js = 2u;
+    return r;
+}
+
+// Frame-path buffers in either layout (tuning "layout.records"): records = rec[i] holds [n_t, a_j, b_j] per
+// pixel; planes = rec[i] holds N res_a planes then N res_b planes, n_t is the separate plane n_t.
+struct FrameBufs {
+    restir_ctx* c;
+    bool records;
+    size_t npx;
+    uint32_t N;
+    float4* nt(int i) const { return records ? c->rec[i].as<float4>() : c->n_t.as<float4>(); }
+    float4* ra(int i) const { return c->rec[i].as<float4>() + (records ? 1 : 0); }
+    float4* rb(int i) const { return c->rec[i].as<float4>() + (records ? 2 : npx * N); }
+    float4* nt2() const { return records ? c->rec[1].as<float4>() : nullptr; }
+    const float4* pa(const restir_frame* f) const { return f->rec.as<float4>() + (records ? 1 : 0); }
+    const float4* pb(const restir_frame* f) const { return f->rec.as<float4>() + (records ? 2 : npx * N); }
+    Region region(Region r) const { return records ? with_records(r, N) : r; }
+};
+
+restir_status ensure_records(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N, FrameBufs& fb) {
+    const size_t npx = (size_t)vw * vh;
+    fb = FrameBufs{c, c->tuning.records != 0, npx, N};
+    ST_TRY(c->p_mat.ensure(npx * 16));
+    if (!fb.records) ST_TRY(c->n_t.ensure(npx * 16));
+    for (int i = 0; i < 2; i++) ST_TRY(c->rec[i].ensure(npx * (fb.records ? 1u + 2u * N : 2u * N) * 16));
+    c->vw = vw; c->vh = vh; c->N = N;
+    return RESTIR_OK;
 }
 
 // rect grown by g, clipped to the view
@@ -448,7 +487,7 @@ void restir_destroy(restir_ctx* c) {
         (void)hipStreamSynchronize(c->stream);
         for (DevBuf* b : {&c->nodes, &c->tri_v0, &c->tri_e1, &c->tri_e2, &c->tri_n0, &c->tri_n1, &c->tri_n2,
                           &c->materials, &c->lights, &c->n_t, &c->p_mat, &c->ra[0], &c->ra[1], &c->rb[0], &c->rb[1],
-                          &c->dbg[0], &c->dbg[1], &c->rgb, &c->queue_ctr, &c->halo_scratch})
+                          &c->dbg[0], &c->dbg[1], &c->rgb, &c->queue_ctr, &c->halo_scratch, &c->rec[0], &c->rec[1]})
             b->release();
         for (Pending& p : c->pending) { (void)hipEventDestroy(p.start); (void)hipEventDestroy(p.stop); }
         for (hipEvent_t ev : c->free_events) (void)hipEventDestroy(ev);
@@ -661,50 +700,49 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                                                 "render such tiles with the halo-exchange stages (restir_halo_begin)");
     }
 
-    ST_TRY(ensure_work(c, t.gwidth, t.gheight, N, false));
-    const size_t npx = (size_t)t.gwidth * t.gheight;
+    FrameBufs fb;
+    ST_TRY(ensure_records(c, t.gwidth, t.gheight, N, fb));
+    if (temporal && prev->records != fb.records)
+        return fail(RESTIR_ERR_INVALID, "temporal predecessor grid was rendered with the other buffer layout");
     ST_TRY(c->rgb.ensure((size_t)t.width * t.height * 12));
     c->rgb_w = t.width; c->rgb_h = t.height;
 
     const CameraDev camd = camera_dev(cam);
-    const Region view = make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.gx0, t.gy0, t.gwidth, t.gheight);
-    const Region owned = make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.x0, t.y0, t.width, t.height);
+    const Region view = fb.region(make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.gx0, t.gy0, t.gwidth, t.gheight));
+    const Region owned = fb.region(make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.x0, t.y0, t.width, t.height));
     const uint32_t frame = c->frame_index++;
     const SceneDev& s = c->sdev;
-    float4* nt = c->n_t.as<float4>();
     float4* pm = c->p_mat.as<float4>();
     int cur = 0;
 
-    TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, nt, pm, c->tuning, c->stream));
-    TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, 0), camd.origin, nt, pm,
-                                      c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), nullptr, c->tuning, c->queue, c->stream));
+    TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, fb.nt(0), pm, fb.nt2(), c->tuning, c->stream));
+    TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, 0), camd.origin, fb.nt(cur),
+                                      pm, fb.ra(cur), fb.rb(cur), nullptr, c->tuning, c->queue, c->stream));
     if (temporal) {
         TIMED(c, RESTIR_K_TEMPORAL,
-              launch_temporal(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0), camd.origin, nt, pm,
-                              c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), prev->a.as<float4>(),
-                              prev->b.as<float4>(), c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), nullptr, c->tuning, c->stream));
+              launch_temporal(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0), camd.origin, fb.nt(cur), pm,
+                              fb.ra(cur), fb.rb(cur), fb.pa(prev), fb.pb(prev), fb.ra(cur), fb.rb(cur), nullptr, c->tuning,
+                              c->stream));
     }
     for (uint32_t pass = 0; pass < passes; pass++) {
         const Region pr = grow_rect(owned, (passes - 1u - pass) * f.R);
         const int nxt = cur ^ 1;
         TIMED(c, RESTIR_K_SPATIAL,
-              launch_spatial(s, pr, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_SPATIAL, pass), camd.origin, nt, pm,
-                             c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->ra[nxt].as<float4>(),
-                             c->rb[nxt].as<float4>(), nullptr, c->tuning, c->stream));
+              launch_spatial(s, pr, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_SPATIAL, pass), camd.origin, fb.nt(cur), pm,
+                             fb.ra(cur), fb.rb(cur), fb.ra(nxt), fb.rb(nxt), nullptr, c->tuning, c->stream));
         cur = nxt;
     }
-    TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, nt, pm, c->ra[cur].as<float4>(), c->rb[cur].as<float4>(),
-                                          c->rgb.as<float>(), c->tuning, c->stream));
+    TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), c->rgb.as<float>(),
+                                          c->tuning, c->stream));
     c->cur = cur;
 
     if (out_next) {
         restir_frame* fr = new restir_frame();
         fr->device = c->device;
         fr->W = width; fr->H = height; fr->vx0 = t.gx0; fr->vy0 = t.gy0; fr->vw = t.gwidth; fr->vh = t.gheight; fr->N = N;
-        // hand the final grid's buffers to the frame (no copy); the context re-allocates lazily
-        std::swap(fr->a, c->ra[cur]);
-        std::swap(fr->b, c->rb[cur]);
-        (void)npx;
+        // hand the final grid's records to the frame (no copy); the context re-allocates lazily
+        std::swap(fr->rec, c->rec[cur]);
+        fr->records = fb.records;
         *out_next = fr;
     }
     if (out_rgb) {
@@ -725,8 +763,7 @@ void restir_frame_release(restir_frame* fr) {
     if (fr->refs.fetch_sub(1) == 1) {
         (void)hipSetDevice(fr->device);
         (void)hipDeviceSynchronize();
-        fr->a.release();
-        fr->b.release();
+        fr->rec.release();
         delete fr;
     }
 }
@@ -823,7 +860,8 @@ restir_status restir_stage_primary(restir_ctx* c, const restir_camera* cam) {
     if (!cam) return fail(RESTIR_ERR_INVALID, "camera is NULL");
     STAGE_PRELUDE();
     const CameraDev camd = camera_dev(cam);
-    TIMED(c, RESTIR_K_PRIMARY, launch_primary(c->sdev, c->stage_rg, camd, c->n_t.as<float4>(), c->p_mat.as<float4>(), c->tuning, c->stream));
+    TIMED(c, RESTIR_K_PRIMARY, launch_primary(c->sdev, c->stage_rg, camd, c->n_t.as<float4>(), c->p_mat.as<float4>(), nullptr,
+                                              c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
@@ -988,12 +1026,16 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
     if (temporal && (prev->N != f.N || prev->vw != t.gwidth || prev->vh != t.gheight || prev->vx0 != t.gx0 ||
                      prev->vy0 != t.gy0 || prev->W != width || prev->H != height))
         return fail(RESTIR_ERR_INVALID, "temporal predecessor grid does not match this tile's view / N");
-    ST_TRY(ensure_work(c, t.gwidth, t.gheight, f.N, false));
+    FrameBufs fb;
+    ST_TRY(ensure_records(c, t.gwidth, t.gheight, f.N, fb));
+    if (temporal && prev->records != fb.records)
+        return fail(RESTIR_ERR_INVALID, "temporal predecessor grid was rendered with the other buffer layout");
     ST_TRY(c->rgb.ensure((size_t)t.width * t.height * 12));
     c->rgb_w = t.width; c->rgb_h = t.height;
     h.W = width; h.H = height;
-    h.view = make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.gx0, t.gy0, t.gwidth, t.gheight);
-    h.owned = make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.x0, t.y0, t.width, t.height);
+    h.view = fb.region(make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.gx0, t.gy0, t.gwidth, t.gheight));
+    h.owned = fb.region(make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.x0, t.y0, t.width, t.height));
+    h.fb_records = fb.records;
     h.f = f;
     h.camd = camera_dev(cam);
     h.frame = c->frame_index++;
@@ -1001,19 +1043,17 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
     h.passes = passes;
     h.cur = 0;
     const SceneDev& s = c->sdev;
-    float4* nt = c->n_t.as<float4>();
     float4* pm = c->p_mat.as<float4>();
     // G-buffer on the whole view (the spatial passes read the neighbours' depth / normal / position),
     // reservoirs only on the owned rectangle
-    TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, h.view, h.camd, nt, pm, c->tuning, c->stream));
+    TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, h.view, h.camd, fb.nt(0), pm, fb.nt2(), c->tuning, c->stream));
     TIMED(c, RESTIR_K_RIS, launch_ris(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_RIS, 0), h.camd.origin,
-                                      nt, pm, c->ra[0].as<float4>(), c->rb[0].as<float4>(), nullptr, c->tuning, c->queue,
-                                      c->stream));
+                                      fb.nt(0), pm, fb.ra(0), fb.rb(0), nullptr, c->tuning, c->queue, c->stream));
     if (temporal)
         TIMED(c, RESTIR_K_TEMPORAL,
-              launch_temporal(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_TEMPORAL, 0), h.camd.origin, nt,
-                              pm, c->ra[0].as<float4>(), c->rb[0].as<float4>(), prev->a.as<float4>(), prev->b.as<float4>(),
-                              c->ra[0].as<float4>(), c->rb[0].as<float4>(), nullptr, c->tuning, c->stream));
+              launch_temporal(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_TEMPORAL, 0), h.camd.origin, fb.nt(0),
+                              pm, fb.ra(0), fb.rb(0), fb.pa(prev), fb.pb(prev), fb.ra(0), fb.rb(0), nullptr, c->tuning,
+                              c->stream));
     h.active = true;
     if (send_bytes) *send_bytes = h.send_bytes;
     if (recv_bytes) *recv_bytes = h.recv_bytes;
@@ -1030,7 +1070,8 @@ restir_status restir_halo_pack(restir_ctx* c, void* buf, uint64_t bytes, int hos
     HIP_TRY(hipSetDevice(c->device));
     float4* dst = static_cast<float4*>(buf);
     if (host_memory) { ST_TRY(c->halo_scratch.ensure(bytes)); dst = c->halo_scratch.as<float4>(); }
-    HIP_TRY(launch_halo_pack(h.view, h.send, h.f.N, c->ra[h.cur].as<float4>(), c->rb[h.cur].as<float4>(), dst, c->stream));
+    const FrameBufs fb{c, h.fb_records, (size_t)h.view.vw * h.view.vh, h.f.N};
+    HIP_TRY(launch_halo_pack(h.view, h.send, h.f.N, fb.ra(h.cur), fb.rb(h.cur), dst, c->stream));
     if (host_memory && bytes) HIP_TRY(hipMemcpyAsync(buf, dst, bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));   // the caller's transport reads the buffer next
     return RESTIR_OK;
@@ -1050,7 +1091,8 @@ restir_status restir_halo_unpack(restir_ctx* c, const void* buf, uint64_t bytes,
         HIP_TRY(hipMemcpyAsync(c->halo_scratch.p, buf, bytes, hipMemcpyHostToDevice, c->stream));
         src = c->halo_scratch.as<float4>();
     }
-    HIP_TRY(launch_halo_unpack(h.view, h.recv, h.f.N, src, c->ra[h.cur].as<float4>(), c->rb[h.cur].as<float4>(), c->stream));
+    const FrameBufs fb{c, h.fb_records, (size_t)h.view.vw * h.view.vh, h.f.N};
+    HIP_TRY(launch_halo_unpack(h.view, h.recv, h.f.N, src, fb.ra(h.cur), fb.rb(h.cur), c->stream));
     if (host_memory) HIP_TRY(hipStreamSynchronize(c->stream));   // the host buffer may be reused on return
     return RESTIR_OK;
 }
@@ -1062,10 +1104,11 @@ restir_status restir_halo_spatial(restir_ctx* c) {
     if (!h.active || h.pass >= h.passes) return fail(RESTIR_ERR_STATE, "restir_halo_spatial: no pass left");
     HIP_TRY(hipSetDevice(c->device));
     const int nxt = h.cur ^ 1;
+    const FrameBufs fb{c, h.fb_records, (size_t)h.view.vw * h.view.vh, h.f.N};
     TIMED(c, RESTIR_K_SPATIAL,
           launch_spatial(c->sdev, h.owned, h.f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_SPATIAL, h.pass), h.camd.origin,
-                         c->n_t.as<float4>(), c->p_mat.as<float4>(), c->ra[h.cur].as<float4>(), c->rb[h.cur].as<float4>(),
-                         c->ra[nxt].as<float4>(), c->rb[nxt].as<float4>(), nullptr, c->tuning, c->stream));
+                         fb.nt(h.cur), c->p_mat.as<float4>(), fb.ra(h.cur), fb.rb(h.cur), fb.ra(nxt), fb.rb(nxt), nullptr,
+                         c->tuning, c->stream));
     h.cur = nxt;
     h.pass++;
     return RESTIR_OK;
@@ -1079,9 +1122,9 @@ restir_status restir_halo_end(restir_ctx* c, restir_frame** out_next, float* out
     if (!h.active || h.pass != h.passes)
         return fail(RESTIR_ERR_STATE, "restir_halo_end after %u of %u spatial passes", h.pass, h.passes);
     HIP_TRY(hipSetDevice(c->device));
-    TIMED(c, RESTIR_K_FINAL, launch_final(c->sdev, h.owned, h.f, h.camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
-                                          c->ra[h.cur].as<float4>(), c->rb[h.cur].as<float4>(), c->rgb.as<float>(), c->tuning,
-                                          c->stream));
+    const FrameBufs fb{c, h.fb_records, (size_t)h.view.vw * h.view.vh, h.f.N};
+    TIMED(c, RESTIR_K_FINAL, launch_final(c->sdev, h.owned, h.f, h.camd.origin, fb.nt(h.cur), c->p_mat.as<float4>(),
+                                          fb.ra(h.cur), fb.rb(h.cur), c->rgb.as<float>(), c->tuning, c->stream));
     c->cur = h.cur;
     h.active = false;
     if (out_next) {
@@ -1089,8 +1132,8 @@ restir_status restir_halo_end(restir_ctx* c, restir_frame** out_next, float* out
         fr->device = c->device;
         fr->W = h.W; fr->H = h.H; fr->vx0 = h.view.vx0; fr->vy0 = h.view.vy0; fr->vw = h.view.vw; fr->vh = h.view.vh;
         fr->N = h.f.N;
-        std::swap(fr->a, c->ra[h.cur]);
-        std::swap(fr->b, c->rb[h.cur]);
+        std::swap(fr->rec, c->rec[h.cur]);
+        fr->records = h.fb_records;
         *out_next = fr;
     }
     if (out_rgb) {
@@ -1136,7 +1179,8 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;
     else if (!std::strcmp(key, "ris.queue")) t.ris_queue = v;
     else if (!std::strcmp(key, "bvh.max_leaf")) t.bvh_max_leaf = v;
-    else if (!std::strcmp(key, "final.sort")) t.final_sort = v;   // applies from the next restir_set_scene
+    else if (!std::strcmp(key, "final.sort")) t.final_sort = v;
+    else if (!std::strcmp(key, "layout.records")) t.records = v;   // frame-path buffer layout   // applies from the next restir_set_scene
     else if (!std::strcmp(key, "final.blocks")) t.final_blocks = v;
     else if (!std::strcmp(key, "final.lds")) t.final_lds = v;
     else if (!std::strcmp(key, "final.2d")) t.final_2d = v;

@@ -21,6 +21,7 @@ VARIANTS = {
     "light0": ["ROMIS_ABL_LIGHT0"],           # every candidate reads light 0 (no LDS bank conflicts)
     "spatial_self": ["ROMIS_ABL_SPATIAL_SELF"],  # spatial neighbours = the pixel itself (no gathers)
     "spatial_copy": ["ROMIS_ABL_SPATIAL_COPY"],  # spatial = copy own reservoir (memory floor)
+    "spatial_sameline": ["ROMIS_ABL_SPATIAL_SAMELINE"],  # neighbour reservoir from the G-buffer record's line
     "ris_u2": ["ROMIS_RIS_U2"],               # two target pdfs per candidate-loop iteration
     "ris_wpe4": ["ROMIS_RIS_WPE=4"],
     "spatial_wpe3": ["ROMIS_SPATIAL_WPE=3"],

@@ -303,8 +303,18 @@ def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased, M, 
     assert_bits(rgb, want, "rgb")
 
 
-def test_temporal_sequence_matches_oracle(gpu, oracle):
-    """C3-style: 4 static frames, temporal reuse threading the previous frame's grid (main.cpp:165)."""
+@pytest.mark.parametrize("records", [0, 1])
+def test_temporal_sequence_matches_oracle(gpu, oracle, records):
+    """C3-style: 4 static frames, temporal reuse threading the previous frame's grid (main.cpp:165); both frame
+    buffer layouts (SoA planes, per-pixel records)."""
+    gpu.set_tuning("layout.records", records)
+    try:
+        _temporal_sequence(gpu, oracle)
+    finally:
+        gpu.set_tuning("layout.records", 0)
+
+
+def _temporal_sequence(gpu, oracle):
     name = "nightclub_128pt"
     s = get_scene(name)
     gpu.set_scene(s)

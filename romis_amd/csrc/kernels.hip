@@ -385,8 +385,14 @@ __device__ __forceinline__ uint32_t num_tiles(const Region& rg) {
 __device__ __forceinline__ bool tile_pixel_of(const Region& rg, uint32_t tile, uint32_t& x, uint32_t& y, size_t& p) {
     const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
     const uint32_t tx = tile % ntx, ty = tile / ntx;
-    x = rg.rx0 + tx * kTileW + threadIdx.x % kTileW;
-    y = rg.ry0 + ty * kTileH + threadIdx.x / kTileW;
+    if (rg.map2d == 2u) {   // each wave an 8x8 block of the 32x8 tile (a squarer gather footprint per wave)
+        const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+        x = rg.rx0 + tx * kTileW + w * 8u + (l & 7u);
+        y = rg.ry0 + ty * kTileH + (l >> 3);
+    } else {
+        x = rg.rx0 + tx * kTileW + threadIdx.x % kTileW;
+        y = rg.ry0 + ty * kTileH + threadIdx.x / kTileW;
+    }
     if (x >= rg.rx0 + rg.rw || y >= rg.ry0 + rg.rh) return false;
     p = (size_t)(y - rg.vy0) * rg.vw + (x - rg.vx0);
     return true;
@@ -1141,7 +1147,8 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
                           const float4* n_t, const float4* p_mat, const float4* ia, const float4* ib, float4* oa,
                           float4* ob, float2* odbg, const Tuning& tu, hipStream_t stream) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
-    const Region rg = with_map(rg0, tu.spatial_xcd);   // XCD-banded order works on 2D tiles
+    Region rg = with_map(rg0, tu.spatial_xcd);   // XCD-banded order works on 2D tiles
+    if (rg.map2d && tu.spatial_wave8) rg.map2d = 2u;
     uint32_t grid = items_of(rg);
     if (tu.spatial_blocks) grid = std::min(grid, std::max(8u, tu.spatial_blocks));
     auto k = f.unbiased ? (f.N == 1 ? k_spatial_n1_unbiased : (f.N == 2 ? k_spatial_n2_unbiased : k_spatial_n0_unbiased))

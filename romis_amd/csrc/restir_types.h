@@ -51,7 +51,7 @@ struct Region {
     uint32_t W, H;
     uint32_t vx0, vy0, vw, vh;
     uint32_t rx0, ry0, rw, rh;
-    uint32_t map2d;   // work item = a 32x8 tile (1) or 256 consecutive row-major pixels (0)
+    uint32_t map2d;   // work item = a 32x8 tile (1: waves 32x2, 2: waves 8x8) or 256 row-major pixels (0)
     // Record layout of the G-buffer n_t and reservoir (res_a, res_b) arrays: element (j, p) of view pixel p
     // lives at index j * js + p * ps.  SoA planes: ps = 1, js = view pixels.  Per-pixel records
     // [n_t, a_0, b_0, a_1, b_1, ...] (restir_render): ps = 1 + 2N, js = 2, with res_a = rec + 1, res_b = rec + 2.
@@ -68,6 +68,7 @@ struct Tuning {
     uint32_t ris_queue = 0;        // persistent blocks (this many) pulling tiles from a WorkQueue; 0 = off
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
     uint32_t spatial_blocks = 0;
+    uint32_t spatial_wave8 = 1;    // waves cover 8x8 pixel blocks instead of 32x2 rows (-2..4 %, kbench)
     uint32_t timing_mask = 0xFFFFFFFFu;
     uint32_t records = 0;          // frame path: per-pixel records (1) or SoA planes (0); planes measured faster
     uint32_t bvh_max_leaf = 2;     // triangles per BVH leaf (used by restir_set_scene); 2 beat 1/4/8 (kbench)   // kernels (bit = RESTIR_K_*) bracketed by HIP events when timing is on

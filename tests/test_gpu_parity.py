@@ -303,6 +303,27 @@ def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased, M, 
     assert_bits(rgb, want, "rgb")
 
 
+@pytest.mark.parametrize("w,h,N,passes,M", [(1, 1, 1, 2, 32), (37, 23, 2, 2, 32), (33, 9, 1, 1, 1), (40, 24, 32, 1, 8),
+                                          (64, 1, 3, 2, 16), (1, 50, 1, 1, 32)])
+def test_odd_sizes_and_extremes_match_oracle(gpu, oracle, w, h, N, passes, M):
+    """Image sizes that are not tile multiples (1x1, 1-pixel rows / columns, ragged 32x8 tiles), the largest N
+    (RESTIR_MAX_N = 32), M = 1 -- two temporal frames each."""
+    name = "nightclub_512"
+    s = get_scene(name)
+    gpu.set_scene(s)
+    osc = oracle.OracleScene(s)
+    cam = scene.camera_for(name, w, h)
+    f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=passes, temporal_reuse=1,
+                              initial_light_samples=M)
+    gpu.set_seed(SEED, 0)
+    prev_gpu, prev_or = None, None
+    for frame in range(2):
+        rgb, grid = gpu.render_restir(prev_gpu, cam, w, h, f)
+        want, res, _ = oracle.render_frame(osc, cam, f, w, h, SEED, frame, prev=prev_or)
+        assert_bits(rgb, want, f"{w}x{h} N={N} frame {frame}")
+        prev_gpu, prev_or = grid, res
+
+
 @pytest.mark.parametrize("records", [0, 1])
 def test_temporal_sequence_matches_oracle(gpu, oracle, records):
     """C3-style: 4 static frames, temporal reuse threading the previous frame's grid (main.cpp:165); both frame

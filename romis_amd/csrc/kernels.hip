@@ -1080,7 +1080,30 @@ extern "C" __global__ __launch_bounds__(256) void k_read_stream(const float4* __
 // Host launchers (launch.h)
 #include "launch.h"
 
+#include <hip/hip_ext.h>
+
 namespace romis {
+
+// Timed launches: restir.cpp's TIMED hands a start / stop event pair to the next launch, which records them
+// inside its own dispatch (hipExtLaunchKernelGGL) -- no separate event packets, hence no stream gaps.
+namespace {
+thread_local hipEvent_t g_ev_start = nullptr, g_ev_stop = nullptr;
+thread_local bool g_launched = false;
+}  // namespace
+
+void set_launch_events(hipEvent_t start, hipEvent_t stop) {
+    g_ev_start = start;
+    g_ev_stop = stop;
+    g_launched = false;
+}
+bool launch_events_used() { return g_launched; }
+
+#define ROMIS_LAUNCH(kernel, grid, block, lds, stream, ...)                                                    \
+    do {                                                                                                      \
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, g_ev_start, g_ev_stop, 0, __VA_ARGS__);      \
+        g_launched = true;                                                                                    \
+    } while (0)
+
 namespace {
 constexpr uint32_t kBlock = 256;
 static_assert(kTileW * kTileH == kBlock, "one lane per tile pixel");
@@ -1103,9 +1126,9 @@ hipError_t launch_primary(const SceneDev& s, const Region& rg0, const CameraDev&
     const size_t lds = bvh_lds_bytes(s);
     const dim3 grid = grid_capped(items_of(rg), tu.primary_blocks);
     if (tu.primary_lds && lds <= kLdsBudget)
-        hipLaunchKernelGGL(k_primary_lds, grid, dim3(kBlock), lds, stream, s, rg, cam, n_t, p_mat, n_t2);
+        ROMIS_LAUNCH(k_primary_lds, grid, dim3(kBlock), lds, stream, s, rg, cam, n_t, p_mat, n_t2);
     else
-        hipLaunchKernelGGL(k_primary, grid, dim3(kBlock), 0, stream, s, rg, cam, n_t, p_mat, n_t2);
+        ROMIS_LAUNCH(k_primary, grid, dim3(kBlock), 0, stream, s, rg, cam, n_t, p_mat, n_t2);
     return hipGetLastError();
 }
 
@@ -1125,7 +1148,7 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f
     const bool use_lds = tu.ris_lds && s.num_lights > 0 && lds <= kLdsBudget;
     auto k = use_lds ? (f.N == 1 ? k_ris_n1_lds : (f.N == 2 ? k_ris_n2_lds : k_ris_n0_lds))
                      : (f.N == 1 ? k_ris_n1 : (f.N == 2 ? k_ris_n2 : k_ris_n0));
-    hipLaunchKernelGGL(k, grid, dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ra,
+    ROMIS_LAUNCH(k, grid, dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ra,
                        rb, rdbg, wq);
     return hipGetLastError();
 }
@@ -1138,7 +1161,7 @@ hipError_t launch_temporal(const SceneDev& s, const Region& rg0, const FeaturesD
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, 0);
     auto k = f.N == 1 ? k_temporal_n1 : (f.N == 2 ? k_temporal_n2 : k_temporal_n0);
-    hipLaunchKernelGGL(k, dim3(items_of(rg)), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ca, cb,
+    ROMIS_LAUNCH(k, dim3(items_of(rg)), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ca, cb,
                        pa, pb, oa, ob, odbg);
     return hipGetLastError();
 }
@@ -1155,7 +1178,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
                         : (f.N == 1 ? k_spatial_n1_biased : (f.N == 2 ? k_spatial_n2_biased : k_spatial_n0_biased));
     const size_t lds = bvh_lds_bytes(s);
     const uint32_t bvh_lds = (f.unbiased && f.spatial_vis && lds <= kLdsBudget) ? 1u : 0u;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), bvh_lds ? lds : 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat,
+    ROMIS_LAUNCH(k, dim3(grid), dim3(kBlock), bvh_lds ? lds : 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat,
                        ia, ib, oa, ob, odbg, bvh_lds);
     return hipGetLastError();
 }
@@ -1170,11 +1193,11 @@ hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev&
     auto k = use_lds ? (f.N == 1 ? k_final_n1_lds : (f.N == 2 ? k_final_n2_lds : k_final_n0_lds))
                      : (f.N == 1 ? k_final_n1 : (f.N == 2 ? k_final_n2 : k_final_n0));
     if (tu.final_sort && use_lds && f.N == 1 && rg.map2d) {   // one tile per block
-        hipLaunchKernelGGL(k_final_n1_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, s, rg, f, o[0], o[1], o[2],
+        ROMIS_LAUNCH(k_final_n1_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, s, rg, f, o[0], o[1], o[2],
                            n_t, p_mat, ra, rb, rgb);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(k, grid_capped(items_of(rg), tu.final_blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,
+    ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.final_blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,
                        o[0], o[1], o[2], n_t, p_mat, ra, rb, rgb);
     return hipGetLastError();
 }

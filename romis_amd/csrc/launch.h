@@ -25,6 +25,10 @@ hipError_t launch_halo_pack(const Region& rg, const HaloSegs& hs, uint32_t N, co
                             hipStream_t stream);
 hipError_t launch_halo_unpack(const Region& rg, const HaloSegs& hs, uint32_t N, const float4* in, float4* ra, float4* rb,
                               hipStream_t stream);
+// The next frame-kernel launch records `start` / `stop` (nullptr: none) within its dispatch; launch_events_used()
+// tells whether a launch consumed them since the last set_launch_events.
+void set_launch_events(hipEvent_t start, hipEvent_t stop);
+bool launch_events_used();
 hipError_t launch_read_stream(const float4* buf, size_t n4, float* sink, hipStream_t stream);
 hipError_t launch_debug_math(const float* x, const float* y, float* pw, float* ex, uint32_t n, hipStream_t stream);
 

@@ -341,19 +341,26 @@ restir_status ensure_work(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N, b
 restir_status timed_begin(restir_ctx* c, int kernel, Pending& p) {
     p.kernel = kernel;
     p.start = p.stop = nullptr;
+    set_launch_events(nullptr, nullptr);
     if (!c->timing || !((c->tuning.timing_mask >> kernel) & 1u)) return RESTIR_OK;
     for (hipEvent_t* e : {&p.start, &p.stop}) {
         if (!c->free_events.empty()) { *e = c->free_events.back(); c->free_events.pop_back(); }
         else HIP_TRY(hipEventCreate(e));
     }
-    HIP_TRY(hipEventRecord(p.start, c->stream));
+    set_launch_events(p.start, p.stop);   // recorded by the launch itself (hipExtLaunchKernelGGL)
     return RESTIR_OK;
 }
 
 restir_status timed_end(restir_ctx* c, Pending& p, hipError_t launch_err) {
+    const bool used = launch_events_used();
+    set_launch_events(nullptr, nullptr);
     if (launch_err != hipSuccess) return fail(RESTIR_ERR_HIP, "kernel launch: %s", hipGetErrorString(launch_err));
     if (!p.start) return RESTIR_OK;
-    HIP_TRY(hipEventRecord(p.stop, c->stream));
+    if (!used) {   // nothing launched (empty region): the events were never recorded
+        c->free_events.push_back(p.start);
+        c->free_events.push_back(p.stop);
+        return RESTIR_OK;
+    }
     c->pending.push_back(p);
     return RESTIR_OK;
 }

@@ -21,11 +21,6 @@ VARIANTS = {
     "light0": ["ROMIS_ABL_LIGHT0"],           # every candidate reads light 0 (no LDS bank conflicts)
     "spatial_self": ["ROMIS_ABL_SPATIAL_SELF"],  # spatial neighbours = the pixel itself (no gathers)
     "spatial_copy": ["ROMIS_ABL_SPATIAL_COPY"],  # spatial = copy own reservoir (memory floor)
-    "spatial_sameline": ["ROMIS_ABL_SPATIAL_SAMELINE"],  # neighbour reservoir from the G-buffer record's line
-    "sp_b2": ["ROMIS_SPATIAL_BATCH=2"],
-    "sp_b2_w5": ["ROMIS_SPATIAL_BATCH=2", "ROMIS_SPATIAL_WPE=5"],
-    "sp_b1_w5": ["ROMIS_SPATIAL_BATCH=1", "ROMIS_SPATIAL_WPE=5"],
-    "sp_b3_w5": ["ROMIS_SPATIAL_BATCH=3", "ROMIS_SPATIAL_WPE=5"],
 }
 
 

@@ -865,6 +865,159 @@ ROMIS_SPATIAL_KERNEL(2, true, k_spatial_n2_unbiased)
 ROMIS_SPATIAL_KERNEL(0, true, k_spatial_n0_unbiased)
 
 // ---------------------------------------------------------------------------------------------------------
+// k_spatial1: the N = 1 biased pass (the headline configuration), written for a small VALU stream.
+// Same arithmetic and RNG slots as spatial_pixel<1, false>; what changes is how it is laid out:
+//  - 32-bit byte offsets from the plane bases (saddr + voffset loads, no 64-bit address math), neighbour
+//    clamping by v_med3 against precomputed bounds;
+//  - the five depth tests share one double reciprocal of the pixel's depth (exact: div_by_rcp_d), and are
+//    evaluated only for lanes whose normal test passed (a miss pixel's zero normal rejects every neighbour);
+//  - the pixel's own G-buffer + reservoir are loaded together with the five neighbour G-buffer records; the
+//    accepted neighbours' reservoirs are loaded one neighbour ahead of the consume sequence (91 VGPRs = 5 waves
+//    per SIMD; the whole batch at once took 111 = 4 waves and ran 8 % slower), and the target pdf of the
+//    pixel's own sample (consumed last) is evaluated while the first neighbour's reservoir is in flight;
+//  - the neighbours are consumed by a fully unrolled sequence (static register indices, no batch shifting),
+//    each behind a branch that the wave skips when none of its lanes accepted that neighbour.
+// Measured (scripts/kbench.py, 1080p C2): 99-100 us against 103-106 us for spatial_pixel<1, false>; SQ counters:
+// 15 % fewer VALU instructions (no 64-bit address math, no packed-bool bookkeeping, shared depth reciprocal).
+// Only SoA planes (Region ps = 1) and K <= kLeanK take this path (launch_spatial checks).
+constexpr uint32_t kLeanK = 5;
+
+template <class T>
+__device__ __forceinline__ T ld_at(const T* __restrict__ base, uint32_t byte_ofs) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_ofs);
+}
+template <class T>
+__device__ __forceinline__ void st_at(T* __restrict__ base, uint32_t byte_ofs, T v) {
+    *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_ofs) = v;
+}
+
+// Combine state of one output sub-reservoir (N = 1): Reservoir::update (reservoir.cpp:10-32) without the M
+// increment (combineBiased replaces M by the routed sum, reservoir.cpp:55-57).
+struct Comb1 {
+    v3 pos, col;
+    float wsum, chosen, pd;
+    uint32_t macc;
+    bool has_pd;
+    uint32_t h;   // ps + slot * 0x9E3779B9 of the next accept draw
+    __device__ __forceinline__ void take(float pd_in, float W, uint32_t M, v3 p, v3 c) {
+        const float w = (pd_in * W) * (float)M;          // reservoir.cpp:50
+        macc += M;
+        wsum += w;
+        const float u = rand01(mix32(h));
+        h += 0x9E3779B9u;
+        if (u < (w / wsum)) { pos = p; col = c; chosen = w; pd = pd_in; has_pd = true; }
+    }
+};
+
+template <bool DBG>
+__device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
+                                               v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                               const float4* __restrict__ ia, const float4* __restrict__ ib,
+                                               float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
+                                               uint32_t x, uint32_t y) {
+    const uint32_t K = f.K;   // <= kLeanK (host check)
+    const int rx = (int)(x - rg.vx0), ry = (int)(y - rg.vy0);
+    const uint32_t pofs = ((uint32_t)ry * rg.vw + (uint32_t)rx) << 4;
+    const float4 cn = ld_at(n_t, pofs), cpm = ld_at(p_mat, pofs);
+    const float4 ca = ld_at(ia, pofs), cb = ld_at(ib, pofs);
+    // clamp to the image (render_utils.cpp:109-110), then to the stored view; view-relative coordinates
+    const int xlo = max(0, (int)rg.vx0) - (int)rg.vx0, xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1 - (int)rg.vx0;
+    const int ylo = max(0, (int)rg.vy0) - (int)rg.vy0, yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1 - (int)rg.vy0;
+    const uint32_t ps = pix_state(key, y * rg.W + x);
+    const uint32_t span = 2u * f.R + 1u;
+    const int bx = rx - (int)f.R, by = ry - (int)f.R;
+    uint32_t qo[kLeanK];
+    float4 g[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        qo[n] = pofs;
+        if (n < K) {
+            const int nx = min(max(bx + (int)__umulhi(draw(ps, 2u * n), span), xlo), xhi);
+            const int ny = min(max(by + (int)__umulhi(draw(ps, 2u * n + 1u), span), ylo), yhi);
+            qo[n] = ((uint32_t)ny * rg.vw + (uint32_t)nx) << 4;
+            g[n] = ld_at(n_t, qo[n]);
+        }
+    }
+    float4 na[kLeanK], nb[kLeanK];
+    // pixel shading context (material + view vector) while the neighbour records are in flight
+    const Px cur = make_px(s, cn, cpm, origin);
+    // depth / normal heuristic (render_utils.cpp:114-118): one shared reciprocal of the pixel's depth
+    const double rt = rcp_d(cur.t);
+    const bool rt_ok = div_fast_ok(cur.t);
+    bool ok[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        ok[n] = false;
+        if (n < K) {
+            const float nd = vdot(xyz(g[n]), cur.N);
+            bool rej = nd < 0.90630778703f;
+            if (!rej) {
+                float q = div_by_rcp_d(g[n].w, rt);
+                if (!rt_ok) q = g[n].w / cur.t;
+                rej = fabsf(1.0f - q) > 0.1f;
+            }
+            ok[n] = !rej;
+        }
+    }
+    // accepted neighbours' reservoirs, one neighbour ahead of the consume sequence (two in flight: 16 VGPRs
+    // instead of 40 for the whole batch, which keeps the kernel at 91 VGPRs = 5 waves per SIMD)
+    if (ok[0]) { na[0] = ld_at(ia, qo[0]); nb[0] = ld_at(ib, qo[0]); }
+    // the pixel's own sample is consumed last; its target pdf does not depend on the stream
+    const float pd_cur = target_pdf(s, f, cur, xyz(ca), xyz(cb));
+    Comb1 cmb;
+    cmb.pos = mk(0.0f, 0.0f, 0.0f); cmb.col = mk(0.0f, 0.0f, 0.0f);
+    cmb.wsum = ROMIS_FLT_MIN; cmb.chosen = 0.0f; cmb.pd = 0.0f; cmb.macc = 0u; cmb.has_pd = false;
+    cmb.h = ps + 2u * K * 0x9E3779B9u;
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        if (n + 1 < kLeanK && ok[n + 1]) { na[n + 1] = ld_at(ia, qo[n + 1]); nb[n + 1] = ld_at(ib, qo[n + 1]); }
+        if (ok[n]) {
+            const v3 p = xyz(na[n]), c = xyz(nb[n]);
+            cmb.take(target_pdf(s, f, cur, p, c), na[n].w, __float_as_uint(nb[n].w), p, c);
+        }
+    }
+    cmb.take(pd_cur, ca.w, __float_as_uint(cb.w), xyz(ca), xyz(cb));
+    // finish_biased: M = routed sum, W from the held sample's target pdf (light.cpp:90-93 / reservoir.cpp:61-64)
+    float p = cmb.pd;
+    if (!cmb.has_pd) p = target_pdf(s, f, cur, cmb.pos, cmb.col);
+    const float W = contribution_weight(p, cmb.macc, cmb.wsum);
+    st_at(oa, pofs, make_float4(cmb.pos.x, cmb.pos.y, cmb.pos.z, W));
+    st_at(ob, pofs, make_float4(cmb.col.x, cmb.col.y, cmb.col.z, __uint_as_float(cmb.macc)));
+    if (DBG) st_at(odbg, pofs >> 1, make_float2(cmb.wsum, cmb.chosen));
+}
+
+template <bool DBG>
+__device__ __forceinline__ void spatial1_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
+                                              v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                              const float4* __restrict__ ia, const float4* __restrict__ ib,
+                                              float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg) {
+    // XCD-banded 32x8 tiles, waves of 8x8 pixels (rg.map2d = 2), as spatial_body
+    const uint32_t T = num_tiles(rg);
+    const uint32_t nb = gridDim.x, b = blockIdx.x, xcd = b % 8u;
+    const uint32_t xcd_blocks = nb / 8u + (xcd < nb % 8u ? 1u : 0u);
+    const uint32_t q = T / 8u, rem = T % 8u;
+    const uint32_t band0 = xcd * q + min(xcd, rem), band_len = q + (xcd < rem ? 1u : 0u);
+    for (uint32_t t = b / 8u; t < band_len; t += xcd_blocks) {
+        uint32_t x, y;
+        size_t p;
+        if (tile_pixel_of(rg, band0 + t, x, y, p))
+            spatial1_pixel<DBG>(s, rg, f, key, origin, n_t, p_mat, ia, ib, oa, ob, odbg, x, y);
+    }
+}
+
+#define ROMIS_SPATIAL1_KERNEL(DBG, NAME)                                                                              \
+    extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f,      \
+                                                                            uint32_t key, float ox, float oy, float oz, \
+                                                                            const float4* n_t, const float4* p_mat,     \
+                                                                            const float4* ia, const float4* ib,         \
+                                                                            float4* oa, float4* ob, float2* odbg) {     \
+        spatial1_body<DBG>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg);                           \
+    }
+ROMIS_SPATIAL1_KERNEL(false, k_spatial1)
+ROMIS_SPATIAL1_KERNEL(true, k_spatial1_dbg)
+
+
+// ---------------------------------------------------------------------------------------------------------
 // k_final: finalShading + exposureToneMapping + Screen::setPixel y-flip.  rgb rows: row 0 = top of rect.
 // Persistent blocks stage the BVH into LDS once (shadow rays are the kernel's main cost).
 template <int NT, bool LDS_BVH>
@@ -1174,6 +1327,12 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
     if (rg.map2d && tu.spatial_wave8) rg.map2d = 2u;
     uint32_t grid = items_of(rg);
     if (tu.spatial_blocks) grid = std::min(grid, std::max(8u, tu.spatial_blocks));
+    if (tu.spatial_lean && !f.unbiased && f.N == 1 && f.K <= kLeanK && rg.ps == 1u && rg.map2d == 2u &&
+        (size_t)rg.vw * rg.vh * 16u <= 0xFFFFFFFFull) {
+        ROMIS_LAUNCH(odbg ? k_spatial1_dbg : k_spatial1, dim3(grid), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1],
+                     o[2], n_t, p_mat, ia, ib, oa, ob, odbg);
+        return hipGetLastError();
+    }
     auto k = f.unbiased ? (f.N == 1 ? k_spatial_n1_unbiased : (f.N == 2 ? k_spatial_n2_unbiased : k_spatial_n0_unbiased))
                         : (f.N == 1 ? k_spatial_n1_biased : (f.N == 2 ? k_spatial_n2_biased : k_spatial_n0_biased));
     const size_t lds = bvh_lds_bytes(s);

@@ -1184,6 +1184,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.xcd")) t.spatial_xcd = v;
     else if (!std::strcmp(key, "spatial.blocks")) t.spatial_blocks = v;
     else if (!std::strcmp(key, "spatial.wave8")) t.spatial_wave8 = v;
+    else if (!std::strcmp(key, "spatial.lean")) t.spatial_lean = v;
     else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;
     else if (!std::strcmp(key, "ris.queue")) t.ris_queue = v;
     else if (!std::strcmp(key, "bvh.max_leaf")) t.bvh_max_leaf = v;

@@ -68,7 +68,8 @@ struct Tuning {
     uint32_t ris_queue = 0;        // persistent blocks (this many) pulling tiles from a WorkQueue; 0 = off
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
     uint32_t spatial_blocks = 0;
-    uint32_t spatial_wave8 = 1;    // waves cover 8x8 pixel blocks instead of 32x2 rows (-2..4 %, kbench)
+    uint32_t spatial_wave8 = 1;
+    uint32_t spatial_lean = 1;     // N = 1 biased passes through k_spatial1 (0: the general kernel)    // waves cover 8x8 pixel blocks instead of 32x2 rows (-2..4 %, kbench)
     uint32_t timing_mask = 0xFFFFFFFFu;
     uint32_t records = 0;          // frame path: per-pixel records (1) or SoA planes (0); planes measured faster
     uint32_t bvh_max_leaf = 2;     // triangles per BVH leaf (used by restir_set_scene); 2 beat 1/4/8 (kbench)   // kernels (bit = RESTIR_K_*) bracketed by HIP events when timing is on

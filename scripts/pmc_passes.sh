@@ -7,9 +7,10 @@ TAG=$1; shift
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 export TMPDIR=/tmp
 cd "$REPO" || exit 1
+mkdir -p "gpurun_out/$TAG"
 i=0
 for G in "$@"; do
-    timeout -k 10 300 rocprofv3 --pmc $G --output-format csv -d "gpurun_out/$TAG/pmc$i" -o run -- \
+    timeout -s KILL 120 rocprofv3 --pmc $G --output-format csv -d "gpurun_out/$TAG/pmc$i" -o run -- \
         python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > "gpurun_out/$TAG/pmc$i.json" 2> "gpurun_out/$TAG/pmc$i.err" || exit $((20 + i))
     i=$((i + 1))
 done

@@ -200,7 +200,11 @@ def test_temporal_bit_exact(gpu, oracle, N, clamp):
 @pytest.mark.parametrize("name", ["nightclub_128pt", "cornell_parallelogram"])
 @pytest.mark.parametrize("N", [1, 2, 3])
 @pytest.mark.parametrize("mode", ["biased", "unbiased", "unbiased_vis"])
-def test_spatial_pass_bit_exact(gpu, oracle, name, N, mode):
+@pytest.mark.parametrize("lean", [1, 0])
+def test_spatial_pass_bit_exact(gpu, oracle, name, N, mode, lean):
+    if lean == 0 and (N != 1 or mode != "biased"):
+        pytest.skip("spatial.lean only selects the kernel of N = 1 biased passes")
+    gpu.set_tuning("spatial.lean", lean)   # 1: k_spatial1 (default), 0: the general spatial kernel
     _, osc, cam = setup(gpu, oracle, name, N)
     n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
     f = _abi.default_features(num_samples_in_reservoir=N, unbiased_combination=int(mode != "biased"),
@@ -215,6 +219,7 @@ def test_spatial_pass_bit_exact(gpu, oracle, name, N, mode):
         assert_bits(gpu.download(_abi.BUF_RES_A), a, f"pass {p} res_a")
         assert_bits(gpu.download(_abi.BUF_RES_B), b, f"pass {p} res_b")
         assert_bits(gpu.download(_abi.BUF_RES_DBG), d, f"pass {p} wSum/chosen")
+    gpu.set_tuning("spatial.lean", 1)
 
 
 @pytest.mark.parametrize("k,r", [(0, 10), (10, 30), (5, 1)])

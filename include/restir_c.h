@@ -280,11 +280,12 @@ restir_status restir_measure_read_bandwidth(restir_ctx* ctx, uint64_t bytes, uin
  * context's stream; restir_timings returns the accumulated milliseconds and launch counts per kernel. */
 typedef enum restir_kernel {
     RESTIR_K_PRIMARY = 0, RESTIR_K_RIS = 1, RESTIR_K_TEMPORAL = 2, RESTIR_K_SPATIAL = 3, RESTIR_K_FINAL = 4,
-    RESTIR_K_COUNT = 5
+    RESTIR_K_PRIMARY_RIS = 5,   /* primary rays + initial RIS fused (restir_render, tuning "fuse.primary_ris") */
+    RESTIR_K_COUNT = 6
 } restir_kernel;
 restir_status restir_enable_timing(restir_ctx* ctx, int enable);
-/* Launch-shape knobs (never change results): "primary.blocks|lds|2d", "ris.blocks|lds", "spatial.xcd|blocks",
- * "final.blocks|lds|2d".  *.blocks = persistent grid cap (0 = one block per work item).  "timing.mask": the
+/* Launch-shape knobs (never change results): "primary.blocks|lds|2d", "ris.blocks|lds", "spatial.xcd|blocks|lean",
+ * "final.blocks|lds|2d", "fuse.primary_ris" (restir_render runs primary rays + RIS as one kernel, default 1).  *.blocks = persistent grid cap (0 = one block per work item).  "timing.mask": the
  * kernels (bit 1 << RESTIR_K_*) restir_enable_timing brackets with HIP events (default all).  "bvh.max_leaf":
  * triangles per BVH leaf for the next restir_set_scene (default 2).  "layout.records": restir_render's buffers as
  * per-pixel records [n_t, res_a, res_b] (1) or SoA planes (0, default). */

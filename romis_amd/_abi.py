@@ -23,8 +23,8 @@ MODE_RESTIR, MODE_RMIS, MODE_ROMIS = 0, 1, 2
 BUF_GBUF_N_T, BUF_GBUF_P_MAT, BUF_RES_A, BUF_RES_B, BUF_RES_DBG = 0, 1, 2, 3, 4
 BUF_PREV_A, BUF_PREV_B, BUF_PREV_DBG, BUF_RGB = 5, 6, 7, 8
 
-K_PRIMARY, K_RIS, K_TEMPORAL, K_SPATIAL, K_FINAL, K_COUNT = 0, 1, 2, 3, 4, 5
-KERNEL_NAMES = ["primary", "ris", "temporal", "spatial", "final"]
+K_PRIMARY, K_RIS, K_TEMPORAL, K_SPATIAL, K_FINAL, K_PRIMARY_RIS, K_COUNT = 0, 1, 2, 3, 4, 5, 6
+KERNEL_NAMES = ["primary", "ris", "temporal", "spatial", "final", "primary_ris"]
 
 STATUS_NAMES = {0: "OK", 1: "INVALID", 2: "HIP", 3: "NO_DEVICE", 4: "STATE", 5: "UNSUPPORTED", 6: "COMM"}
 

@@ -448,17 +448,13 @@ using namespace romis;
 extern __shared__ __attribute__((aligned(16))) float4 g_lds[];
 
 // ---------------------------------------------------------------------------------------------------------
-// k_primary: persistent blocks stage the BVH into LDS once, then sweep 32x8 tiles; writes n_t / p_mat.
-template <bool LDS_BVH>
-__device__ __forceinline__ void primary_body(const SceneDev& s, const Region& rg, const CameraDev& cam, float4* __restrict__ n_t2,
-                                             float4* __restrict__ n_t, float4* __restrict__ p_mat) {
-    const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
-    const uint32_t nt = work_items(rg);
+// genPrimaryRayHits for pixel (x, y) at view index p: writes and returns the G-buffer records (n_t, p_mat)
+__device__ __forceinline__ void primary_pixel(const SceneDev& s, const Region& rg, const CameraDev& cam, const Bvh& bvh,
+                                              uint32_t x, uint32_t y, size_t p, float4* __restrict__ n_t2,
+                                              float4* __restrict__ n_t, float4* __restrict__ p_mat, float4& nt_out,
+                                              float4& pm_out) {
     const v3 o = mk(cam.origin[0], cam.origin[1], cam.origin[2]);
-    for (uint32_t tile = blockIdx.x; tile < nt; tile += gridDim.x) {
-        uint32_t x, y;
-        size_t p;
-        if (!work_pixel(rg, tile, x, y, p)) continue;
+    {
         float nx = (float)x / (float)rg.W * 2.0f - 1.0f;
         float ny = (float)y / (float)rg.H * 2.0f - 1.0f;
         v3 csd = vnormalize(mk(-nx * cam.half_w, ny * cam.half_h, 1.0f));
@@ -479,7 +475,24 @@ __device__ __forceinline__ void primary_body(const SceneDev& s, const Region& rg
         const float4 nt = make_float4(n.x, n.y, n.z, t);
         n_t[gidx(rg, p)] = nt;
         if (n_t2) n_t2[gidx(rg, p)] = nt;   // the other record buffer of the ping-pong pair
-        p_mat[p] = make_float4(P.x, P.y, P.z, __uint_as_float(m));
+        pm_out = make_float4(P.x, P.y, P.z, __uint_as_float(m));
+        p_mat[p] = pm_out;
+        nt_out = nt;
+    }
+}
+
+// k_primary: persistent blocks stage the BVH into LDS once, then sweep 32x8 tiles; writes n_t / p_mat.
+template <bool LDS_BVH>
+__device__ __forceinline__ void primary_body(const SceneDev& s, const Region& rg, const CameraDev& cam, float4* __restrict__ n_t2,
+                                             float4* __restrict__ n_t, float4* __restrict__ p_mat) {
+    const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
+    const uint32_t nt = work_items(rg);
+    for (uint32_t tile = blockIdx.x; tile < nt; tile += gridDim.x) {
+        uint32_t x, y;
+        size_t p;
+        if (!work_pixel(rg, tile, x, y, p)) continue;
+        float4 a, b;
+        primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, a, b);
     }
 }
 
@@ -493,35 +506,22 @@ extern "C" __global__ __launch_bounds__(256) void k_primary_lds(SceneDev s, Regi
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// k_ris: genCanonicalSamples per pixel.  Lane-serial candidate loop (M iterations) -- VALU bound.  The light
-// table is staged into LDS once per persistent block when it fits (LDS_LIGHTS), so the per-candidate random
-// light fetch is an LDS read instead of a dependent global load.
-template <int NT, bool LDS_LIGHTS>
-__device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
-                                         const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
-                                         float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
-                                         WorkQueue wq) {
+// genCanonicalSamples for one pixel whose G-buffer records are (nt, pm); lights = the light table (global or
+// the block's LDS copy), bvh = the traversal arrays for the initial visibility rays.
+template <int NT>
+__device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
+                                          const float4* lights, const Bvh& bvh, float4 nt, float4 pm, uint32_t x,
+                                          uint32_t y, size_t p, float4* __restrict__ ra, float4* __restrict__ rb,
+                                          float2* __restrict__ rdbg) {
     const uint32_t L = s.num_lights;
-    const float4* lights = s.lights;
-    if (LDS_LIGHTS) {
-        for (uint32_t i = threadIdx.x; i < 7u * L; i += blockDim.x) g_lds[i] = s.lights[i];
-        __syncthreads();
-        lights = g_lds;
-    }
-    const Bvh bvh = global_bvh(s);
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
-    const uint32_t items = work_items(rg);
     const float invL = 1.0f / (float)L;
-    WorkCursor cur(wq);
-    for (uint32_t item = cur.first(); item < items; item = cur.next()) {
-        uint32_t x, y;
-        size_t p;
-        if (!work_pixel(rg, item, x, y, p)) continue;
+    {
         Sub r[NT > 0 ? NT : RESTIR_MAX_N_DEV];
         for (uint32_t j = 0; j < N; j++) sub_init(r[j]);
         if (L != 0) {
-            Px px = load_px(s, rg, n_t, p_mat, p, origin);
+            Px px = make_px(s, nt, pm, origin);
             const uint32_t ps = pix_state(key, y * rg.W + x);
             for (uint32_t j = 0; j < N; j++) r[j].M = 0u;
             // A primary-ray miss carries the value-initialised HitInfo (kd = ks = 0, N = 0): its target pdf is
@@ -591,6 +591,59 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
     }
 }
 
+// k_ris: genCanonicalSamples per pixel.  Lane-serial candidate loop (M iterations) -- VALU bound.  The light
+// table is staged into LDS once per persistent block when it fits (LDS_LIGHTS), so the per-candidate random
+// light fetch is an LDS read instead of a dependent global load.
+template <int NT, bool LDS_LIGHTS>
+__device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
+                                         const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                         float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
+                                         WorkQueue wq) {
+    const float4* lights = s.lights;
+    if (LDS_LIGHTS) {
+        for (uint32_t i = threadIdx.x; i < 7u * s.num_lights; i += blockDim.x) g_lds[i] = s.lights[i];
+        __syncthreads();
+        lights = g_lds;
+    }
+    const Bvh bvh = global_bvh(s);
+    const uint32_t items = work_items(rg);
+    WorkCursor cur(wq);
+    for (uint32_t item = cur.first(); item < items; item = cur.next()) {
+        uint32_t x, y;
+        size_t p;
+        if (!work_pixel(rg, item, x, y, p)) continue;
+        ris_pixel<NT>(s, rg, f, key, origin, lights, bvh, n_t[gidx(rg, p)], p_mat[p], x, y, p, ra, rb, rdbg);
+    }
+}
+
+// k_primary_ris: genPrimaryRayHits and genCanonicalSamples fused (they cover the same region in restir_render):
+// the G-buffer records go to memory for the later passes and straight into the pixel's RIS, and the primary
+// ray's latency-bound BVH traversal runs beside other waves' VALU-bound candidate loops.  The block stages the
+// BVH and, when it fits beside it, the light table in LDS.
+template <int NT, bool LDS_LIGHTS>
+__device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region& rg, const CameraDev& cam,
+                                                 const FeaturesDev& f, uint32_t key, float4* __restrict__ n_t,
+                                                 float4* __restrict__ p_mat, float4* __restrict__ n_t2,
+                                                 float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg) {
+    const uint32_t bvh_f4 = 2u * s.num_nodes + 3u * s.num_tris;
+    const float4* lights = s.lights;
+    if (LDS_LIGHTS) {
+        for (uint32_t i = threadIdx.x; i < 7u * s.num_lights; i += blockDim.x) g_lds[bvh_f4 + i] = s.lights[i];
+        lights = g_lds + bvh_f4;
+    }
+    const Bvh bvh = stage_bvh(s, g_lds);   // ends with the barrier that also covers the light copy
+    const v3 origin = mk(cam.origin[0], cam.origin[1], cam.origin[2]);
+    const uint32_t items = work_items(rg);
+    for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {
+        uint32_t x, y;
+        size_t p;
+        if (!work_pixel(rg, item, x, y, p)) continue;
+        float4 nt, pm;
+        primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, nt, pm);
+        ris_pixel<NT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg);
+    }
+}
+
 // RIS: capped at 96 VGPRs = 5 waves per SIMD (uncapped the allocator takes 100 = 4 waves; 5 waves run the
 // latency-bound candidate loop 9 % faster, 6 waves spill -- scripts/ablate.py, profiles/r1)
 #ifndef ROMIS_RIS_WPE
@@ -609,6 +662,19 @@ ROMIS_RIS_KERNEL(0, false, k_ris_n0, )
 ROMIS_RIS_KERNEL(1, true, k_ris_n1_lds, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL(2, true, k_ris_n2_lds, )
 ROMIS_RIS_KERNEL(0, true, k_ris_n0_lds, )
+
+#define ROMIS_PRIMARY_RIS_KERNEL(NT, LDS, NAME, ATTR)                                                                  \
+    extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, CameraDev cam, FeaturesDev f,   \
+                                                          uint32_t key, float4* n_t, float4* p_mat, float4* n_t2,      \
+                                                          float4* ra, float4* rb, float2* rdbg) {                      \
+        primary_ris_body<NT, LDS>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg);                                  \
+    }
+ROMIS_PRIMARY_RIS_KERNEL(1, true, k_primary_ris_n1_lds, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL(1, false, k_primary_ris_n1, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL(2, true, k_primary_ris_n2_lds, )
+ROMIS_PRIMARY_RIS_KERNEL(2, false, k_primary_ris_n2, )
+ROMIS_PRIMARY_RIS_KERNEL(0, true, k_primary_ris_n0_lds, )
+ROMIS_PRIMARY_RIS_KERNEL(0, false, k_primary_ris_n0, )
 
 // ---------------------------------------------------------------------------------------------------------
 // Combine state shared by temporal and spatial: out[] (Reservoir(N) of the current pixel) + routed M sums.
@@ -1305,6 +1371,23 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f
                        rb, rdbg, wq);
     return hipGetLastError();
 }
+
+hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const CameraDev& cam, const FeaturesDev& f, uint32_t key,
+                              float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,
+                              const Tuning& tu, hipStream_t stream) {
+    if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
+    const Region rg = with_map(rg0, tu.primary_2d);
+    const size_t bvh = bvh_lds_bytes(s), lights = lights_lds_bytes(s);
+    if (bvh > kLdsBudget) return hipErrorInvalidValue;   // caller checks primary_ris_fits()
+    const bool use_lights = tu.ris_lds && s.num_lights > 0 && bvh + lights <= kLdsBudget;
+    auto k = use_lights ? (f.N == 1 ? k_primary_ris_n1_lds : (f.N == 2 ? k_primary_ris_n2_lds : k_primary_ris_n0_lds))
+                        : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
+    ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.ris_blocks), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
+                 cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg);
+    return hipGetLastError();
+}
+
+bool primary_ris_fits(const SceneDev& s) { return bvh_lds_bytes(s) <= kLdsBudget; }
 
 hipError_t launch_temporal(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
                            const float4* n_t, const float4* p_mat, const float4* ca, const float4* cb,

@@ -722,9 +722,15 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     float4* pm = c->p_mat.as<float4>();
     int cur = 0;
 
-    TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, fb.nt(0), pm, fb.nt2(), c->tuning, c->stream));
-    TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, 0), camd.origin, fb.nt(cur),
-                                      pm, fb.ra(cur), fb.rb(cur), nullptr, c->tuning, c->queue, c->stream));
+    const uint32_t ris_key = restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, 0);
+    if (c->tuning.fuse_primary_ris && primary_ris_fits(s)) {   // same region: one kernel (kernels.hip k_primary_ris)
+        TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),
+                                                          fb.rb(cur), nullptr, c->tuning, c->stream));
+    } else {
+        TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, fb.nt(0), pm, fb.nt2(), c->tuning, c->stream));
+        TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, ris_key, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), nullptr,
+                                          c->tuning, c->queue, c->stream));
+    }
     if (temporal) {
         TIMED(c, RESTIR_K_TEMPORAL,
               launch_temporal(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0), camd.origin, fb.nt(cur), pm,
@@ -1185,6 +1191,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.blocks")) t.spatial_blocks = v;
     else if (!std::strcmp(key, "spatial.wave8")) t.spatial_wave8 = v;
     else if (!std::strcmp(key, "spatial.lean")) t.spatial_lean = v;
+    else if (!std::strcmp(key, "fuse.primary_ris")) t.fuse_primary_ris = v;
     else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;
     else if (!std::strcmp(key, "ris.queue")) t.ris_queue = v;
     else if (!std::strcmp(key, "bvh.max_leaf")) t.bvh_max_leaf = v;

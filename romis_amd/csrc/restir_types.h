@@ -69,6 +69,7 @@ struct Tuning {
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
     uint32_t spatial_blocks = 0;
     uint32_t spatial_wave8 = 1;
+    uint32_t fuse_primary_ris = 1; // restir_render: k_primary_ris instead of k_primary + k_ris when the BVH fits LDS
     uint32_t spatial_lean = 1;     // N = 1 biased passes through k_spatial1 (0: the general kernel)    // waves cover 8x8 pixel blocks instead of 32x2 rows (-2..4 %, kbench)
     uint32_t timing_mask = 0xFFFFFFFFu;
     uint32_t records = 0;          // frame path: per-pixel records (1) or SoA planes (0); planes measured faster

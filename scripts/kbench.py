@@ -21,7 +21,7 @@ import numpy as np  # noqa: E402
 from romis_amd import _abi, restir, scene  # noqa: E402
 
 DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 1, "ris.queue": 0,
-            "spatial.xcd": 1, "spatial.blocks": 0, "spatial.wave8": 1, "spatial.lean": 1, "bvh.max_leaf": 2, "final.blocks": 0, "final.lds": 1, "final.2d": 1,
+            "spatial.xcd": 1, "spatial.blocks": 0, "spatial.wave8": 1, "spatial.lean": 1, "fuse.primary_ris": 1, "bvh.max_leaf": 2, "final.blocks": 0, "final.lds": 1, "final.2d": 1,
             "final.sort": 0, "layout.records": 0}
 
 VARIANTS = {
@@ -40,6 +40,7 @@ VARIANTS = {
     "ris_q1024": {"ris.queue": 1024},
     "spatial_noxcd": {"spatial.xcd": 0},
     "spatial_general": {"spatial.lean": 0},
+    "unfused": {"fuse.primary_ris": 0},
     "final_sort": {"final.sort": 1},
     "layout_records": {"layout.records": 1},
     "spatial_rows": {"spatial.wave8": 0},

@@ -29,6 +29,12 @@
  *   RESTIR_STAGE_RIS      (pass 0): candidate c: light 4c, first rand 4c+1, second rand 4c+2, accept 4c+3
  *   RESTIR_STAGE_TEMPORAL (pass 0): accept of the t-th Reservoir::update = t
  *   RESTIR_STAGE_SPATIAL  (pass p): neighbour n: dx 2n, dy 2n+1; accept of the t-th update = 2k + t
+ *   R-MIS / R-OMIS (restir_render with RESTIR_MODE_RMIS / ROMIS):
+ *   RESTIR_STAGE_RIS      (pass i): the i-th MIS iteration's genInitialSamples, slots as above
+ *   RESTIR_STAGE_NEIGHBOURS         generateResampleIndicesGrid (neighbour_selection.cpp:45-122), once per render:
+ *     Random strategy (pass 0): candidate n: x 2n, y 2n+1, U{lo..hi} -> lo + ((uint64(draw) * (hi-lo+1)) >> 32)
+ *     std::sample over the similar list (pass 0) / the dissimilar list (pass 1): selection sampling, the list's
+ *     i-th element is kept iff U{0..len-1-i} (slot i) < the number still needed
  */
 #ifndef RESTIR_C_H
 #define RESTIR_C_H
@@ -40,11 +46,12 @@
 extern "C" {
 #endif
 
-#define RESTIR_ABI_VERSION 1
+#define RESTIR_ABI_VERSION 2   /* 2: restir_features gained the R-MIS / R-OMIS fields */
 
 #define RESTIR_STAGE_RIS      1u
 #define RESTIR_STAGE_TEMPORAL 2u
 #define RESTIR_STAGE_SPATIAL  3u
+#define RESTIR_STAGE_NEIGHBOURS 4u
 #define RESTIR_DEFAULT_SEED   0x5EED0001u
 #define RESTIR_MAX_N          32u   /* numSamplesInReservoir slider range 1..32 (ui.cpp:305) */
 
@@ -54,12 +61,18 @@ typedef enum restir_status {
     RESTIR_ERR_HIP         = 2,  /* HIP runtime failure */
     RESTIR_ERR_NO_DEVICE   = 3,  /* no usable gfx950 device */
     RESTIR_ERR_STATE       = 4,  /* call out of order (e.g. render before set_scene) */
-    RESTIR_ERR_UNSUPPORTED = 5,  /* feature combination not implemented (e.g. RMIS / ROMIS modes) */
+    RESTIR_ERR_UNSUPPORTED = 5,  /* feature combination not implemented (e.g. R-MIS / R-OMIS on a screen tile) */
     RESTIR_ERR_COMM        = 6   /* RCCL failure */
 } restir_status;
 
-/* RayTraceMode (src/utils/common.h:25-29). Only RESTIR is accelerated; the others return UNSUPPORTED. */
+/* RayTraceMode (src/utils/common.h:25-29): renderReSTIR, renderRMIS, renderROMIS (render.cpp:28-265). */
 typedef enum restir_mode { RESTIR_MODE_RESTIR = 0, RESTIR_MODE_RMIS = 1, RESTIR_MODE_ROMIS = 2 } restir_mode;
+/* MISWeightRMIS (common.h:31-34) and NeighbourSelectionStrategy (common.h:36-41) */
+typedef enum restir_mis_weight { RESTIR_MIS_EQUAL = 0, RESTIR_MIS_BALANCE = 1 } restir_mis_weight;
+typedef enum restir_neighbour_strategy {
+    RESTIR_NEIGHBOURS_RANDOM = 0, RESTIR_NEIGHBOURS_SIMILAR = 1, RESTIR_NEIGHBOURS_DISSIMILAR = 2,
+    RESTIR_NEIGHBOURS_EQUAL_SIMILAR_DISSIMILAR = 3
+} restir_neighbour_strategy;
 
 /* std::variant<PointLight, SegmentLight, ParallelogramLight> (common.h:72-87) flattened. 88 bytes. */
 typedef enum restir_light_type {
@@ -130,6 +143,18 @@ typedef struct restir_features {
     uint8_t  enable_tone_mapping;
     float    gamma;
     float    exposure;
+    /* R-MIS / R-OMIS parameters and the neighbour-selection heuristic (common.h:110-121) -- ABI v2 */
+    uint8_t  neighbour_same_geometry;                   /* true */
+    uint8_t  use_progressive_romis;                     /* false */
+    uint8_t  save_alphas_visualisation;                 /* accepted; the per-distribution BMPs are not written */
+    uint8_t  reserved0;
+    float    neighbour_max_depth_difference_fraction;   /* 0.10 */
+    float    neighbour_max_normal_angle_difference_radians; /* 0.436332, compared with the normals' dot product
+                                                           as areSimilar does (neighbour_selection.cpp:16-18) */
+    uint32_t max_iterations_mis;                        /* 5 */
+    uint32_t neighbour_selection_strategy;              /* restir_neighbour_strategy, default SIMILAR */
+    uint32_t mis_weight_rmis;                           /* restir_mis_weight, default EQUAL */
+    uint32_t progressive_update_mod;                    /* 1 */
 } restir_features;
 
 /* Defaults of struct Features (common.h:89-136), rayTraceMode forced to ReSTIR. */
@@ -190,7 +215,13 @@ restir_status restir_set_seed(restir_ctx* ctx, uint32_t seed, uint32_t frame_ind
 restir_status restir_set_scene(restir_ctx* ctx, const restir_mesh* meshes, uint32_t num_meshes,
                                const restir_light* lights, uint32_t num_lights);
 
-/* renderReSTIR (render.cpp:28-62): primary hits -> initial RIS -> [temporal if prev] -> [spatial x P] ->
+/* renderRayTraced (render.cpp:268-290) by features->ray_trace_mode:
+ * RMIS / ROMIS -- renderRMIS / renderROMIS (render.cpp:64-265): primary hits -> neighbour selection grid ->
+ * max_iterations_mis x (initial RIS -> per-pixel MIS combination over the pixel's neighbourhood) -> screen.
+ * Whole images only (tile NULL or covering the image), no temporal predecessor, *out_next = NULL (the reference
+ * returns std::nullopt).  R-OMIS needs k + 1 <= RESTIR_ROMIS_MAX_TECHNIQUES and at least k candidates in every
+ * pixel's window (the reference indexes past the neighbourhood otherwise).
+ * RESTIR -- renderReSTIR (render.cpp:28-62): primary hits -> initial RIS -> [temporal if prev] -> [spatial x P] ->
  * final shading + tone map.  `prev` may be NULL (no temporal predecessor).  `out_next` (nullable) receives
  * a new reference to the frame's final reservoir grid.  `out_rgb` (nullable, host, width*height*3 floats,
  * row 0 = top) -- when NULL the call only enqueues work and returns without synchronising; the image stays
@@ -222,8 +253,18 @@ typedef enum restir_buffer {
     RESTIR_BUF_PREV_A     = 5,   /* reservoir slot 1 (temporal predecessor / spatial ping-pong) */
     RESTIR_BUF_PREV_B     = 6,
     RESTIR_BUF_PREV_DBG   = 7,
-    RESTIR_BUF_RGB        = 8    /* float3 per owned pixel, row 0 = top */
+    RESTIR_BUF_RGB        = 8,   /* float3 per owned pixel, row 0 = top */
+    /* R-MIS / R-OMIS stage buffers (restir_stage_neighbours / restir_stage_mis_accumulate):
+     *   mis_nbr : uint32 [1 + cap][pixels]: row 0 = neighbourhood size c, rows 1..c = the neighbourhood's pixel
+     *             indices y * width + x, the pixel itself first (cap = restir_stage_mis_capacity)
+     *   mis_acc : float [rows][pixels].  R-MIS: colour sum (3 rows).  R-OMIS with T = k + 1: technique matrix A
+     *             (T*T rows, element (i, j) in row i + j*T), contribution vectors b (3*T rows, colour c, technique
+     *             i in row T*T + c*T + i), progressive alphas (3*T rows after b, same order), progressive colour
+     *             (3 rows) */
+    RESTIR_BUF_MIS_NBR    = 9,
+    RESTIR_BUF_MIS_ACC    = 10
 } restir_buffer;
+#define RESTIR_ROMIS_MAX_TECHNIQUES 8u   /* k + 1 distributions per pixel (the technique matrix lives in registers) */
 
 /* Allocates stage buffers for a width x height region with N sub-reservoirs (idempotent). */
 restir_status restir_stage_configure(restir_ctx* ctx, uint32_t width, uint32_t height, uint32_t n);
@@ -245,6 +286,27 @@ restir_status restir_stage_temporal(restir_ctx* ctx, const restir_camera* cam, c
 restir_status restir_stage_spatial(restir_ctx* ctx, const restir_camera* cam, const restir_features* f,
                                    uint32_t rng_key, int debug);
 restir_status restir_stage_final(restir_ctx* ctx, const restir_camera* cam, const restir_features* f);
+
+/* R-MIS / R-OMIS stages (render.cpp:64-265) on the stage buffers (the stage region is the whole image):
+ *   neighbours     : GBUF -> MIS_NBR (generateResampleIndicesGrid); keys = RESTIR_STAGE_NEIGHBOURS passes 0 and 1
+ *   mis_accumulate : iteration i's reservoirs RES_A / RES_B / RES_DBG (restir_stage_ris with debug != 0) + GBUF +
+ *                    MIS_NBR -> MIS_ACC (features->ray_trace_mode selects R-MIS or R-OMIS; MIS_ACC is zeroed
+ *                    when iteration == 0)
+ *   mis_finish     : MIS_ACC -> RGB (combineToScreen, or R-OMIS's per-pixel least-squares solve)
+ * restir_stage_mis_capacity: the neighbourhood capacity `cap` of MIS_NBR for these features. */
+restir_status restir_stage_neighbours(restir_ctx* ctx, const restir_features* f, uint32_t key_similar,
+                                      uint32_t key_dissimilar);
+restir_status restir_stage_mis_accumulate(restir_ctx* ctx, const restir_camera* cam, const restir_features* f,
+                                          uint32_t iteration);
+restir_status restir_stage_mis_finish(restir_ctx* ctx, const restir_features* f);
+restir_status restir_stage_mis_capacity(restir_ctx* ctx, const restir_features* f, uint32_t* out_cap);
+
+/* Batched least squares as renderROMIS solves its systems (Eigen CompleteOrthogonalDecomposition::solve,
+ * render_utils.h:52): for each of `count` systems x = the minimum-norm least-squares solution of A x = b, A n x n
+ * column-major (n*n floats per system), b and x n floats per system; host arrays, n <= RESTIR_ROMIS_MAX_TECHNIQUES.
+ * The device routine of the R-OMIS finish, exposed for the parity tests. */
+restir_status restir_debug_cod_solve(restir_ctx* ctx, uint32_t n, const float* A, const float* b, float* x,
+                                     size_t count);
 
 /* Device portable powf / expf over arrays (parity of the device math with the oracle's). */
 restir_status restir_debug_math(restir_ctx* ctx, const float* x, const float* y, float* out_pow, float* out_exp,
@@ -281,7 +343,8 @@ restir_status restir_measure_read_bandwidth(restir_ctx* ctx, uint64_t bytes, uin
 typedef enum restir_kernel {
     RESTIR_K_PRIMARY = 0, RESTIR_K_RIS = 1, RESTIR_K_TEMPORAL = 2, RESTIR_K_SPATIAL = 3, RESTIR_K_FINAL = 4,
     RESTIR_K_PRIMARY_RIS = 5,   /* primary rays + initial RIS fused (restir_render, tuning "fuse.primary_ris") */
-    RESTIR_K_COUNT = 6
+    RESTIR_K_MIS = 6,           /* R-MIS / R-OMIS neighbour selection, per-iteration combination, finish */
+    RESTIR_K_COUNT = 7
 } restir_kernel;
 restir_status restir_enable_timing(restir_ctx* ctx, int enable);
 /* Launch-shape knobs (never change results): "primary.blocks|lds|2d", "ris.blocks|lds", "spatial.xcd|blocks|lean",

@@ -16,6 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "_build", "liboracle.so")
 
 FP = C.POINTER(C.c_float)
+UP = C.POINTER(C.c_uint32)
 
 
 class Rect(C.Structure):
@@ -59,6 +60,16 @@ def lib() -> C.CDLL:
             "or_final": (None, [P, C.POINTER(_abi.Features), FP, u32, u32, Rect, Rect, FP, FP, FP, FP, FP]),
             "or_render_frame": (C.c_int, [P, C.POINTER(_abi.Camera), C.POINTER(_abi.Features), u32, u32, u32,
                                           u32, Rect, Rect, FP, FP, FP, FP, FP, FP, FP, C.c_int]),
+            "or_mis_capacity": (u32, [C.POINTER(_abi.Features), u32, u32]),
+            "or_mis_acc_rows": (u32, [C.POINTER(_abi.Features)]),
+            "or_neighbours": (None, [P, C.POINTER(_abi.Features), u32, u32, u32, u32, FP, FP, u32, UP]),
+            "or_rmis_accumulate": (None, [P, C.POINTER(_abi.Features), FP, u32, u32, FP, FP, UP, FP, FP, FP]),
+            "or_romis_accumulate": (None, [P, C.POINTER(_abi.Features), FP, u32, u32, FP, FP, UP, FP, FP, FP, u32,
+                                           FP]),
+            "or_mis_finish": (None, [C.POINTER(_abi.Features), u32, u32, FP, FP]),
+            "or_cod_solve": (None, [u32, FP, FP, FP]),
+            "or_render_mis": (C.c_int, [P, C.POINTER(_abi.Camera), C.POINTER(_abi.Features), u32, u32, u32, u32, FP,
+                                        C.c_int]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(l, name)
@@ -170,3 +181,62 @@ def render_frame(osc, cam, f, W, H, seed=_abi.RESTIR_DEFAULT_SEED, frame=0, prev
     if rc != 0:
         raise RuntimeError(f"oracle render_frame failed ({rc})")
     return rgb, (a, b), (n_t, p_mat)
+
+
+# ---- R-MIS / R-OMIS (render.cpp:64-265) -------------------------------------------------------------------
+def up(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.dtype == np.uint32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(UP)
+
+
+def mis_capacity(f, W, H) -> int:
+    return int(lib().or_mis_capacity(C.byref(f), W, H))
+
+
+def mis_acc_rows(f) -> int:
+    return int(lib().or_mis_acc_rows(C.byref(f)))
+
+
+def neighbours(osc, f, key_sim, key_dis, W, H, n_t, p_mat):
+    cap = mis_capacity(f, W, H)
+    nbr = np.zeros(((1 + cap), W * H), np.uint32)
+    lib().or_neighbours(osc.handle, C.byref(f), key_sim, key_dis, W, H, fp(n_t), fp(p_mat), cap, up(nbr))
+    return nbr
+
+
+def rmis_accumulate(osc, f, origin, W, H, n_t, p_mat, nbr, res_a, res_b, acc):
+    o = np.asarray(origin, np.float32)
+    lib().or_rmis_accumulate(osc.handle, C.byref(f), fp(o), W, H, fp(n_t), fp(p_mat), up(nbr), fp(res_a), fp(res_b),
+                             fp(acc))
+
+
+def romis_accumulate(osc, f, origin, W, H, n_t, p_mat, nbr, res_a, res_b, res_dbg, iteration, acc):
+    o = np.asarray(origin, np.float32)
+    lib().or_romis_accumulate(osc.handle, C.byref(f), fp(o), W, H, fp(n_t), fp(p_mat), up(nbr), fp(res_a),
+                              fp(res_b), fp(res_dbg), iteration, fp(acc))
+
+
+def mis_finish(f, W, H, acc):
+    rgb = np.zeros((H, W, 3), np.float32)
+    lib().or_mis_finish(C.byref(f), W, H, fp(acc), fp(rgb))
+    return rgb
+
+
+def cod_solve(A: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """A: [n, n] (row-major numpy; passed column-major), b: [n] -> x"""
+    n = A.shape[0]
+    Ac = np.ascontiguousarray(A.T, np.float32)
+    bc = np.ascontiguousarray(b, np.float32)
+    x = np.zeros(n, np.float32)
+    lib().or_cod_solve(n, fp(Ac), fp(bc), fp(x))
+    return x
+
+
+def render_mis(osc, cam, f, W, H, seed=_abi.RESTIR_DEFAULT_SEED, frame=0, threads=0):
+    rgb = np.zeros((H, W, 3), np.float32)
+    rc = lib().or_render_mis(osc.handle, C.byref(cam), C.byref(f), seed, frame, W, H, fp(rgb), threads)
+    if rc != 0:
+        raise RuntimeError(f"oracle render_mis failed ({rc})")
+    return rgb

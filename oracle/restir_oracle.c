@@ -673,3 +673,490 @@ void or_glm_probe(const float a_[3], const float b_[3], float t, const float e[3
 }
 float or_powf(float x, float y) { return pm_powf(x, y); }
 float or_expf(float x) { return pm_expf(x); }
+
+/* ====================================================================================================== */
+/* R-MIS / R-OMIS (render.cpp:64-265, render_utils.cpp:68-85 / 179-257, neighbour_selection.cpp:7-122,     */
+/* render_utils.h:52).  Whole images only: grids are [H][W] row-major, pixel index p = y * W + x.           */
+
+/* HitInfo::geometryId: the mesh index (rtcAttachGeometry order, embree_interface.cpp:46-47, one material per
+ * mesh); a primary miss keeps the value-initialised HitInfo of genPrimaryRayHits (render_utils.cpp:15): 0. */
+static inline uint32_t geom_id(const or_scene* s, const float* p_mat, size_t p) {
+    uint32_t m = f2u(p_mat[4 * p + 3]);
+    return m + 1u >= s->num_materials ? 0u : m;
+}
+
+/* areSimilar (neighbour_selection.cpp:7-22), lhs = the canonical pixel, rhs = the neighbour.  The normal test
+ * compares the dot product with the RADIANS field (maxDiffCos is computed and unused), as the reference does. */
+static int are_similar(const or_scene* s, const restir_features* f, const float* n_t, const float* p_mat, size_t l,
+                       size_t r) {
+    if (f->neighbour_same_geometry && geom_id(s, p_mat, l) != geom_id(s, p_mat, r)) return 0;
+    float depthFracDiff = fabsf(1.0f - (n_t[4 * l + 3] / n_t[4 * r + 3]));
+    if (depthFracDiff > f->neighbour_max_depth_difference_fraction) return 0;
+    float normalsDotProd = vdot(ld3(&n_t[4 * l]), ld3(&n_t[4 * r]));
+    if (normalsDotProd < f->neighbour_max_normal_angle_difference_radians) return 0;
+    return 1;
+}
+
+typedef struct { int x0, y0, x1, y1; } or_win;
+
+/* Walk pixel p's window in indicesSimilarity's order (y outer, x inner, the pixel itself skipped) and append the
+ * members of one class (similar = 1 / dissimilar = 0): all of them, or std::sample's selection sampling of
+ * `want` of the class's `len` members (member i is kept iff U{0..len-1-i}, keyed slot i, < the number still
+ * needed; the walk stops when none is needed). */
+static uint32_t emit_class(const or_scene* s, const restir_features* f, const float* n_t, const float* p_mat,
+                           uint32_t W, or_win w, size_t p, int cls, uint64_t len, uint64_t want, int take_all,
+                           uint32_t ps, uint32_t* out, size_t npx, uint32_t n) {
+    uint64_t needed = take_all ? len : (want < len ? want : len);
+    uint64_t i = 0;
+    for (int ny = w.y0; ny <= w.y1 && needed; ny++) {
+        for (int nx = w.x0; nx <= w.x1 && needed; nx++) {
+            size_t q = (size_t)ny * W + (size_t)nx;
+            if (q == p || are_similar(s, f, n_t, p_mat, p, q) != cls) continue;
+            int keep = take_all || uniform_index(draw(ps, (uint32_t)i), (uint32_t)(len - i)) < needed;
+            if (keep) { out[(size_t)(1u + n) * npx + p] = (uint32_t)q; n++; needed--; }
+            i++;
+        }
+    }
+    return n;
+}
+
+uint32_t or_mis_capacity(const restir_features* f, uint32_t W, uint32_t H) {
+    uint32_t k1 = f->num_neighbours_to_sample + 1u;
+    if (f->neighbour_selection_strategy == RESTIR_NEIGHBOURS_RANDOM ||
+        f->neighbour_selection_strategy == RESTIR_NEIGHBOURS_SIMILAR)
+        return k1;
+    uint64_t side = 2ull * f->spatial_resample_radius + 1ull;
+    uint64_t win = (side < W ? side : W) * (side < H ? side : H);
+    return win > k1 ? (uint32_t)win : k1;
+}
+
+/* generateResampleIndicesGrid (neighbour_selection.cpp:107-122): nbr[0][p] = neighbourhood size, nbr[1 + i][p] =
+ * its i-th pixel (the pixel itself first).  indicesRandom (:24-43): candidate n draws x then y uniformly in the
+ * clamped window; indicesSimilarity (:45-105): the similar / dissimilar classes of the window, sampled per the
+ * strategy -- including the reference's size arithmetic (Dissimilar takes `k - similar.size()` of the similar
+ * class as size_t, i.e. all of them when that wraps; EqualSimilarDissimilar in uint32_t). */
+void or_neighbours(const or_scene* s, const restir_features* f, uint32_t key_similar, uint32_t key_dissimilar,
+                   uint32_t W, uint32_t H, const float* n_t, const float* p_mat, uint32_t cap, uint32_t* nbr) {
+    const size_t npx = (size_t)W * H;
+    const uint32_t k = f->num_neighbours_to_sample;
+    const int rc = (int)f->spatial_resample_radius;
+#pragma omp parallel for schedule(guided)
+    for (int yy = 0; yy < (int)H; yy++) {
+        for (int x = 0; x < (int)W; x++) {
+            const size_t p = (size_t)yy * W + (size_t)x;
+            const uint32_t ps_s = pix_state(key_similar, (uint32_t)p), ps_d = pix_state(key_dissimilar, (uint32_t)p);
+            or_win w = {x - rc > 0 ? x - rc : 0, yy - rc > 0 ? yy - rc : 0,
+                        x + rc < (int)W - 1 ? x + rc : (int)W - 1, yy + rc < (int)H - 1 ? yy + rc : (int)H - 1};
+            uint32_t n = 0;
+            nbr[npx + p] = (uint32_t)p;
+            n = 1;
+            if (f->neighbour_selection_strategy == RESTIR_NEIGHBOURS_RANDOM) {
+                for (uint32_t c = 0; c < k; c++) {
+                    uint32_t nx = (uint32_t)w.x0 + uniform_index(draw(ps_s, 2u * c), (uint32_t)(w.x1 - w.x0 + 1));
+                    uint32_t ny = (uint32_t)w.y0 + uniform_index(draw(ps_s, 2u * c + 1u), (uint32_t)(w.y1 - w.y0 + 1));
+                    nbr[(size_t)(1u + n) * npx + p] = ny * W + nx;
+                    n++;
+                }
+            } else {
+                uint64_t S = 0, D = 0;
+                for (int ny = w.y0; ny <= w.y1; ny++)
+                    for (int nx = w.x0; nx <= w.x1; nx++) {
+                        size_t q = (size_t)ny * W + (size_t)nx;
+                        if (q == p) continue;
+                        if (are_similar(s, f, n_t, p_mat, p, q)) S++; else D++;
+                    }
+                switch (f->neighbour_selection_strategy) {
+                case RESTIR_NEIGHBOURS_SIMILAR:
+                    if (S < k) {
+                        n = emit_class(s, f, n_t, p_mat, W, w, p, 1, S, 0, 1, ps_s, nbr, npx, n);
+                        n = emit_class(s, f, n_t, p_mat, W, w, p, 0, D, (uint64_t)k - S, 0, ps_d, nbr, npx, n);
+                    } else {
+                        n = emit_class(s, f, n_t, p_mat, W, w, p, 1, S, k, 0, ps_s, nbr, npx, n);
+                    }
+                    break;
+                case RESTIR_NEIGHBOURS_DISSIMILAR:
+                    if (D < k) {
+                        n = emit_class(s, f, n_t, p_mat, W, w, p, 0, D, 0, 1, ps_d, nbr, npx, n);
+                        n = emit_class(s, f, n_t, p_mat, W, w, p, 1, S, (uint64_t)k - S, 0, ps_s, nbr, npx, n);
+                    } else {
+                        n = emit_class(s, f, n_t, p_mat, W, w, p, 0, D, k, 0, ps_d, nbr, npx, n);
+                    }
+                    break;
+                default: {   /* EqualSimilarDissimilar (uint32_t arithmetic as written) */
+                    uint32_t sS = (k / 2u) + 1u < (uint32_t)S ? (k / 2u) + 1u : (uint32_t)S;
+                    uint32_t desired = k - sS;
+                    if ((uint64_t)desired > D) sS = (uint32_t)((uint64_t)sS + ((uint64_t)k - D - sS));
+                    n = emit_class(s, f, n_t, p_mat, W, w, p, 1, S, sS, 0, ps_s, nbr, npx, n);
+                    n = emit_class(s, f, n_t, p_mat, W, w, p, 0, D, (uint32_t)(k - sS), 0, ps_d, nbr, npx, n);
+                } break;
+                }
+            }
+            (void)cap;
+            nbr[p] = n;
+        }
+    }
+}
+
+/* One pixel's reservoir (N sub-reservoirs) with the debug planes (wSum, chosenSampleWeight). */
+static inline void res_load_dbg(or_sub* r, uint32_t N, const float* a, const float* b, const float* dbg, size_t p,
+                                size_t npx) {
+    res_load(r, N, a, b, p, npx);
+    for (uint32_t j = 0; j < N; j++) { r[j].wsum = dbg[2 * (j * npx + p)]; r[j].chosen = dbg[2 * (j * npx + p) + 1]; }
+}
+
+/* One R-MIS iteration's pixel loop (render.cpp:76-112): acc[3][W*H] += the pixel's MIS estimate over its
+ * neighbourhood's reservoirs (this iteration's genInitialSamples). */
+void or_rmis_accumulate(const or_scene* s, const restir_features* f, const float origin_[3], uint32_t W, uint32_t H,
+                        const float* n_t, const float* p_mat, const uint32_t* nbr, const float* res_a,
+                        const float* res_b, float* acc) {
+    const size_t npx = (size_t)W * H;
+    const uint32_t N = f->num_samples_in_reservoir;
+    const v3 origin = ld3(origin_);
+#pragma omp parallel for schedule(guided)
+    for (int yy = 0; yy < (int)H; yy++) {
+        or_sub r[RESTIR_MAX_N];
+        for (uint32_t x = 0; x < W; x++) {
+            const size_t p = (size_t)yy * W + x;
+            or_px cur = load_px(s, n_t, p_mat, p, origin);
+            const uint32_t c = nbr[p];
+            v3 finalColor = mk(0.0f, 0.0f, 0.0f);
+            for (uint32_t i = 0; i < c; i++) {
+                const size_t q = nbr[(size_t)(1u + i) * npx + p];
+                res_load(r, N, res_a, res_b, q, npx);
+                for (uint32_t j = 0; j < N; j++) {
+                    float misWeight;
+                    if (f->mis_weight_rmis == RESTIR_MIS_EQUAL) {
+                        misWeight = 1.0f / (float)c;
+                    } else {   /* generalisedBalanceHeuristic (render_utils.cpp:179-187) */
+                        float numerator = target_pdf(f, &cur, r[j].pos, r[j].col);
+                        float denominator = FLT_MIN;
+                        for (uint32_t i2 = 0; i2 < c; i2++) {
+                            or_px px2 = load_px(s, n_t, p_mat, nbr[(size_t)(1u + i2) * npx + p], origin);
+                            denominator += target_pdf(f, &px2, r[j].pos, r[j].col);
+                        }
+                        misWeight = numerator / denominator;
+                    }
+                    v3 sc = visible(s, cur.P, r[j].pos) ? shade(f, &cur, r[j].pos, r[j].col) : mk(0.0f, 0.0f, 0.0f);
+                    v3 t = vscale(vscale(sc, misWeight), r[j].W);   /* misWeight * sampleColor * outputWeight */
+                    finalColor = vadd(finalColor, vdivs(t, (float)N));
+                }
+            }
+            acc[p] += finalColor.x; acc[npx + p] += finalColor.y; acc[2 * npx + p] += finalColor.z;
+        }
+    }
+}
+
+/* ---- Eigen 3 CompleteOrthogonalDecomposition<MatrixXf>::solve (render_utils.h:52), scalar restatement ---- *
+ * ColPivHouseholderQR::computeInPlace (ColPivHouseholderQR.h:482-571), CompleteOrthogonalDecomposition::
+ * computeInPlace / _solve_impl / applyZAdjointOnTheLeftInPlace (CompleteOrthogonalDecomposition.h:430-560),
+ * makeHouseholder / applyHouseholderOnTheLeft / OnTheRight (Householder.h, HouseholderSequence.h:361-412), the
+ * upper-triangular back substitution (TriangularSolverVector.h, one panel for n <= 16).  Reductions (norms, the
+ * Householder dot products) are evaluated in index order; Eigen evaluates them with SIMD packets, so the two
+ * agree to rounding (tests/golden/cod_fixtures.json, generated by oracle/_ref/cod_ref against the reference's
+ * vendored Eigen) while oracle and device agree bit for bit. */
+#define OR_COD_MAX 8
+static float or_sqnorm(const float* v, int n, int stride) {
+    float s = 0.0f;
+    for (int i = 0; i < n; i++) s = i == 0 ? v[0] * v[0] : s + v[i * stride] * v[i * stride];
+    return s;
+}
+/* makeHouseholder on v[0], v[stride], ... (m entries): essential written over v[stride..], returns tau, beta */
+static void or_make_householder(float* v, int m, int stride, float* tau, float* beta) {
+    float tailSqNorm = m == 1 ? 0.0f : or_sqnorm(v + stride, m - 1, stride);
+    float c0 = v[0];
+    if (tailSqNorm <= FLT_MIN) {
+        *tau = 0.0f;
+        *beta = c0;
+        for (int i = 1; i < m; i++) v[i * stride] = 0.0f;
+    } else {
+        float b = sqrtf(c0 * c0 + tailSqNorm);
+        if (c0 >= 0.0f) b = -b;
+        for (int i = 1; i < m; i++) v[i * stride] = v[i * stride] / (c0 - b);
+        *tau = (b - c0) / b;
+        *beta = b;
+    }
+}
+/* H = I - tau [1 e][1 e]^T from the left on the rows r0..r0+m-1 of columns c0..c0+nc-1 of column-major M (ld) */
+static void or_householder_left(float* M, int ld, int r0, int c0, int m, int nc, const float* e, int estride, float tau) {
+    if (m == 1) {
+        for (int j = 0; j < nc; j++) M[r0 + (c0 + j) * ld] *= 1.0f - tau;
+        return;
+    }
+    if (tau == 0.0f) return;
+    for (int j = 0; j < nc; j++) {
+        float* col = &M[(c0 + j) * ld + r0];
+        float t = 0.0f;
+        for (int i = 0; i < m - 1; i++) t = i == 0 ? e[0] * col[1] : t + e[i * estride] * col[1 + i];
+        t += col[0];
+        col[0] -= tau * t;
+        for (int i = 0; i < m - 1; i++) col[1 + i] -= (tau * e[i * estride]) * t;
+    }
+}
+/* H from the right on rows r0..r0+nr-1 of columns c0..c0+m-1 */
+static void or_householder_right(float* M, int ld, int r0, int c0, int nr, int m, const float* e, int estride, float tau) {
+    if (m == 1) {
+        for (int i = 0; i < nr; i++) M[r0 + i + c0 * ld] *= 1.0f - tau;
+        return;
+    }
+    if (tau == 0.0f) return;
+    for (int i = 0; i < nr; i++) {
+        float t = 0.0f;
+        for (int j = 0; j < m - 1; j++) t = j == 0 ? M[r0 + i + (c0 + 1) * ld] * e[0] : t + M[r0 + i + (c0 + 1 + j) * ld] * e[j * estride];
+        t += M[r0 + i + c0 * ld];
+        M[r0 + i + c0 * ld] -= tau * t;
+        for (int j = 0; j < m - 1; j++) M[r0 + i + (c0 + 1 + j) * ld] -= (tau * t) * e[j * estride];
+    }
+}
+
+void or_cod_solve(uint32_t n_, const float* A, const float* b, float* x) {
+    const int n = (int)n_;
+    float qr[OR_COD_MAX * OR_COD_MAX], hc[OR_COD_MAX], zc[OR_COD_MAX], nU[OR_COD_MAX], nD[OR_COD_MAX];
+    int tr[OR_COD_MAX], perm[OR_COD_MAX];
+    memcpy(qr, A, (size_t)n * n * sizeof(float));
+    for (int k = 0; k < n; k++) { nD[k] = sqrtf(or_sqnorm(&qr[k * n], n, 1)); nU[k] = nD[k]; }
+    float mx = nU[0];
+    for (int k = 1; k < n; k++) if (nU[k] > mx) mx = nU[k];
+    const float eps = FLT_EPSILON;
+    const float threshold_helper = (mx * eps) * (mx * eps) / (float)n;
+    const float norm_downdate_threshold = sqrtf(eps);
+    int nonzero = n;
+    float maxpivot = 0.0f;
+    for (int k = 0; k < n; k++) {
+        int bi = k;
+        float bv = nU[k];
+        for (int j = k + 1; j < n; j++) if (nU[j] > bv) { bv = nU[j]; bi = j; }
+        if (nonzero == n && bv * bv < threshold_helper * (float)(n - k)) nonzero = k;
+        tr[k] = bi;
+        if (k != bi) {
+            for (int i = 0; i < n; i++) { float t = qr[i + k * n]; qr[i + k * n] = qr[i + bi * n]; qr[i + bi * n] = t; }
+            float t = nU[k]; nU[k] = nU[bi]; nU[bi] = t;
+            t = nD[k]; nD[k] = nD[bi]; nD[bi] = t;
+        }
+        float beta;
+        or_make_householder(&qr[k + k * n], n - k, 1, &hc[k], &beta);
+        qr[k + k * n] = beta;
+        if (fabsf(beta) > maxpivot) maxpivot = fabsf(beta);
+        or_householder_left(qr, n, k, k + 1, n - k, n - k - 1, &qr[k + 1 + k * n], 1, hc[k]);
+        for (int j = k + 1; j < n; j++) {
+            if (nU[j] != 0.0f) {
+                float temp = fabsf(qr[k + j * n]) / nU[j];
+                temp = (1.0f + temp) * (1.0f - temp);
+                temp = temp < 0.0f ? 0.0f : temp;
+                float ratio = nU[j] / nD[j];
+                float temp2 = temp * (ratio * ratio);
+                if (temp2 <= norm_downdate_threshold) {
+                    nD[j] = sqrtf(or_sqnorm(&qr[k + 1 + j * n], n - k - 1, 1));
+                    nU[j] = nD[j];
+                } else {
+                    nU[j] *= sqrtf(temp);
+                }
+            }
+        }
+    }
+    for (int k = 0; k < n; k++) perm[k] = k;
+    for (int k = 0; k < n; k++) { int t = perm[k]; perm[k] = perm[tr[k]]; perm[tr[k]] = t; }
+    /* ColPivHouseholderQR::rank() (ColPivHouseholderQR.h:255-264), threshold() = epsilon * diagonalSize */
+    const float pre = fabsf(maxpivot) * (eps * (float)n);
+    int rank = 0;
+    for (int i = 0; i < nonzero; i++) rank += fabsf(qr[i + i * n]) > pre;
+    /* CompleteOrthogonalDecomposition::computeInPlace: zero R12 from the right */
+    if (rank < n) {
+        for (int k = rank - 1; k >= 0; k--) {
+            if (k != rank - 1)
+                for (int i = 0; i <= k; i++) { float t = qr[i + k * n]; qr[i + k * n] = qr[i + (rank - 1) * n]; qr[i + (rank - 1) * n] = t; }
+            float beta;
+            or_make_householder(&qr[k + (rank - 1) * n], n - rank + 1, n, &zc[k], &beta);
+            qr[k + (rank - 1) * n] = beta;
+            if (k > 0) or_householder_right(qr, n, 0, rank - 1, k, n - rank + 1, &qr[k + rank * n], n, zc[k]);
+            if (k != rank - 1)
+                for (int i = 0; i <= k; i++) { float t = qr[i + k * n]; qr[i + k * n] = qr[i + (rank - 1) * n]; qr[i + (rank - 1) * n] = t; }
+        }
+    }
+    /* _solve_impl: rank() again, now over the decomposition's T11 diagonal (|beta| >= the old pivot: the same
+     * count, re-evaluated as the reference does) */
+    {
+        int r2 = 0;
+        for (int i = 0; i < nonzero; i++) r2 += fabsf(qr[i + i * n]) > pre;
+        rank = r2;
+    }
+    float c[OR_COD_MAX], y[OR_COD_MAX];
+    if (rank == 0) { for (int i = 0; i < n; i++) x[i] = 0.0f; return; }
+    for (int i = 0; i < n; i++) c[i] = b[i];
+    for (int k = 0; k < rank; k++)   /* Q^* c: H_0 first */
+        or_householder_left(c, n, k, 0, n - k, 1, &qr[k + 1 + k * n], 1, hc[k]);
+    for (int i = 0; i < n; i++) y[i] = i < rank ? c[i] : 0.0f;
+    for (int i = rank - 1; i >= 0; i--) {   /* upper-triangular back substitution, column sweep */
+        if (y[i] != 0.0f) {
+            y[i] /= qr[i + i * n];
+            for (int j = 0; j < i; j++) y[j] -= y[i] * qr[j + i * n];
+        }
+    }
+    if (rank < n) {   /* applyZAdjointOnTheLeftInPlace */
+        for (int k = 0; k < rank; k++) {
+            if (k != rank - 1) { float t = y[k]; y[k] = y[rank - 1]; y[rank - 1] = t; }
+            or_householder_left(y, n, rank - 1, 0, n - rank + 1, 1, &qr[k + rank * n], n, zc[k]);
+            if (k != rank - 1) { float t = y[k]; y[k] = y[rank - 1]; y[rank - 1] = t; }
+        }
+    }
+    for (int i = 0; i < n; i++) x[perm[i]] = y[i];
+}
+
+/* arbitraryUnbiasedContributionWeightReciprocal (render_utils.cpp:245-257) for sample (pos, col) against
+ * distribution pixel q's reservoir sub sampleIdx */
+static inline float aucw_reciprocal(const or_scene* s, const restir_features* f, const or_px* qpx, const or_sub* qr,
+                                    v3 pos, v3 col) {
+    float targetPdfValue = target_pdf(f, qpx, pos, col);
+    if (targetPdfValue == 0.0f) return 0.0f;
+    float mockSampleWeight = targetPdfValue / (1.0f / (float)s->num_lights);
+    float arbitraryWeight = ((1.0f / targetPdfValue) * (1.0f / (float)qr->M)) * ((qr->wsum - qr->chosen) + mockSampleWeight);
+    return 1.0f / arbitraryWeight;
+}
+
+/* One R-OMIS iteration's pixel loop (render.cpp:139-231): the technique matrix / contribution vectors (and the
+ * progressive estimator's alphas and colour) of acc, layout as RESTIR_BUF_MIS_ACC. */
+void or_romis_accumulate(const or_scene* s, const restir_features* f, const float origin_[3], uint32_t W, uint32_t H,
+                         const float* n_t, const float* p_mat, const uint32_t* nbr, const float* res_a,
+                         const float* res_b, const float* res_dbg, uint32_t iteration, float* acc) {
+    const size_t npx = (size_t)W * H;
+    const uint32_t N = f->num_samples_in_reservoir;
+    const uint32_t T = f->num_neighbours_to_sample + 1u;
+    const int32_t totalSamples = (int32_t)(T * N);
+    const int32_t fractionOfTotalSamples = (int32_t)N / (int32_t)T;
+    const v3 origin = ld3(origin_);
+    float* Am = acc;
+    float* Bv = acc + (size_t)T * T * npx;
+    float* Al = Bv + (size_t)3 * T * npx;
+    float* Col = Al + (size_t)3 * T * npx;
+#pragma omp parallel for schedule(guided)
+    for (int yy = 0; yy < (int)H; yy++) {
+        or_sub r[RESTIR_MAX_N], rd[RESTIR_MAX_N];
+        for (uint32_t x = 0; x < W; x++) {
+            const size_t p = (size_t)yy * W + x;
+            or_px cur = load_px(s, n_t, p_mat, p, origin);
+            float A[OR_COD_MAX * OR_COD_MAX], bb[3][OR_COD_MAX], al[3][OR_COD_MAX];
+            for (uint32_t e = 0; e < T * T; e++) A[e] = Am[e * npx + p];
+            for (uint32_t c = 0; c < 3; c++)
+                for (uint32_t i = 0; i < T; i++) { bb[c][i] = Bv[(c * T + i) * npx + p]; al[c][i] = Al[(c * T + i) * npx + p]; }
+            v3 fc = mk(Col[p], Col[npx + p], Col[2 * npx + p]);
+            if (f->use_progressive_romis && iteration >= 1u && iteration % f->progressive_update_mod == 0u)
+                for (uint32_t c = 0; c < 3; c++) or_cod_solve(T, A, bb[c], al[c]);
+            for (uint32_t pi = 0; pi < T; pi++) {
+                if (f->use_progressive_romis) fc = vadd(fc, mk(al[0][pi], al[1][pi], al[2][pi]));
+                const size_t q = nbr[(size_t)(1u + pi) * npx + p];
+                res_load(r, N, res_a, res_b, q, npx);
+                for (uint32_t si = 0; si < N; si++) {
+                    float v[OR_COD_MAX];
+                    for (uint32_t d = 0; d < T; d++) {
+                        const size_t qd = nbr[(size_t)(1u + d) * npx + p];
+                        or_px dpx = load_px(s, n_t, p_mat, qd, origin);
+                        res_load_dbg(rd, N, res_a, res_b, res_dbg, qd, npx);
+                        v[d] = aucw_reciprocal(s, f, &dpx, &rd[si], r[si].pos, r[si].col);
+                    }
+                    v3 sc = visible(s, cur.P, r[si].pos) ? shade(f, &cur, r[si].pos, r[si].col) : mk(0.0f, 0.0f, 0.0f);
+                    if (f->use_progressive_romis) {
+                        v3 sa = mk(0.0f, 0.0f, 0.0f);
+                        float sf = FLT_MIN;
+                        for (uint32_t d = 0; d < T; d++) {
+                            sa = vadd(sa, vscale(mk(al[0][d], al[1][d], al[2][d]), v[d]));
+                            sf += (float)fractionOfTotalSamples * v[d];
+                        }
+                        v3 term = vsub(vdivs(sc, sf), vdivs(sa, sf));
+                        float inv = 1.0f / (float)totalSamples;
+                        fc = vadd(fc, mk(inv * term.x, inv * term.y, inv * term.z));
+                    }
+                    float scaleFactor = FLT_MIN;
+                    for (uint32_t d = 0; d < T; d++) scaleFactor += (float)N * v[d];
+                    scaleFactor = 1.0f / scaleFactor;
+                    for (uint32_t d = 0; d < T; d++) v[d] *= scaleFactor;
+                    for (uint32_t j = 0; j < T; j++)
+                        for (uint32_t i = 0; i < T; i++) A[i + j * T] += v[i] * v[j];
+                    for (uint32_t row = 0; row < T; row++) {
+                        float scaleColVecConst = scaleFactor * v[row];
+                        bb[0][row] += sc.x * scaleColVecConst;
+                        bb[1][row] += sc.y * scaleColVecConst;
+                        bb[2][row] += sc.z * scaleColVecConst;
+                    }
+                }
+            }
+            for (uint32_t e = 0; e < T * T; e++) Am[e * npx + p] = A[e];
+            for (uint32_t c = 0; c < 3; c++)
+                for (uint32_t i = 0; i < T; i++) { Bv[(c * T + i) * npx + p] = bb[c][i]; Al[(c * T + i) * npx + p] = al[c][i]; }
+            Col[p] = fc.x; Col[npx + p] = fc.y; Col[2 * npx + p] = fc.z;
+        }
+    }
+}
+
+/* Screen output of R-MIS / progressive R-OMIS (combineToScreen, render_utils.cpp:68-85) or the direct R-OMIS
+ * estimator (render.cpp:234-263: per-pixel solves, component sums, tone map).  rgb [H][W][3], row 0 = top. */
+void or_mis_finish(const restir_features* f, uint32_t W, uint32_t H, const float* acc, float* rgb) {
+    const size_t npx = (size_t)W * H;
+    const uint32_t T = f->num_neighbours_to_sample + 1u;
+    const int romis = f->ray_trace_mode == RESTIR_MODE_ROMIS;
+    const int direct = romis && !f->use_progressive_romis;
+    const float* col = romis ? acc + (size_t)(T * T + 6u * T) * npx : acc;
+#pragma omp parallel for schedule(guided)
+    for (int yy = 0; yy < (int)H; yy++) {
+        for (uint32_t x = 0; x < W; x++) {
+            const size_t p = (size_t)yy * W + x;
+            v3 c;
+            if (direct) {
+                float A[OR_COD_MAX * OR_COD_MAX], bb[OR_COD_MAX], xs[3][OR_COD_MAX];
+                for (uint32_t e = 0; e < T * T; e++) A[e] = acc[e * npx + p];
+                for (uint32_t ch = 0; ch < 3; ch++) {
+                    for (uint32_t i = 0; i < T; i++) bb[i] = acc[(T * T + ch * T + i) * npx + p];
+                    or_cod_solve(T, A, bb, xs[ch]);
+                }
+                c = mk(0.0f, 0.0f, 0.0f);
+                for (uint32_t row = 0; row < T; row++) { c.x += xs[0][row]; c.y += xs[1][row]; c.z += xs[2][row]; }
+            } else {
+                c = vdivs(mk(col[p], col[npx + p], col[2 * npx + p]), (float)f->max_iterations_mis);
+            }
+            if (f->enable_tone_mapping) c = tonemap(c, f->exposure, f->gamma);
+            st3(&rgb[3 * ((size_t)(H - 1u - (uint32_t)yy) * W + x)], c);
+        }
+    }
+}
+
+uint32_t or_mis_acc_rows(const restir_features* f) {
+    const uint32_t T = f->num_neighbours_to_sample + 1u;
+    return f->ray_trace_mode == RESTIR_MODE_ROMIS ? T * T + 6u * T + 3u : 3u;
+}
+
+/* renderRMIS / renderROMIS (render.cpp:64-265) over the whole W x H image; rgb [H][W][3], row 0 = top. */
+int or_render_mis(const or_scene* s, const restir_camera* cam, const restir_features* f, uint32_t seed, uint32_t frame,
+                  uint32_t W, uint32_t H, float* rgb, int threads) {
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+    const uint32_t N = f->num_samples_in_reservoir;
+    if (N == 0 || N > RESTIR_MAX_N) return -2;
+    const size_t npx = (size_t)W * H;
+    restir_camera_frame cf;
+    or_camera_derive(cam, &cf);
+    float* n_t = (float*)malloc(npx * 16);
+    float* p_mat = (float*)malloc(npx * 16);
+    or_rect view = {0, 0, W, H};
+    or_primary(s, &cf, W, H, view, view, n_t, p_mat);
+    const uint32_t cap = or_mis_capacity(f, W, H);
+    uint32_t* nbr = (uint32_t*)calloc((size_t)(1u + cap) * npx, 4);
+    or_neighbours(s, f, or_rng_key(seed, frame, RESTIR_STAGE_NEIGHBOURS, 0), or_rng_key(seed, frame, RESTIR_STAGE_NEIGHBOURS, 1),
+                  W, H, n_t, p_mat, cap, nbr);
+    const size_t rows = or_mis_acc_rows(f);
+    float* acc = (float*)calloc(rows * npx, 4);
+    float* a = (float*)malloc(npx * N * 16);
+    float* b = (float*)malloc(npx * N * 16);
+    float* d = (float*)malloc(npx * N * 8);
+    int rc = 0;
+    for (uint32_t it = 0; it < f->max_iterations_mis; it++) {
+        or_ris(s, f, or_rng_key(seed, frame, RESTIR_STAGE_RIS, it), cf.origin, W, H, view, view, n_t, p_mat, a, b, d);
+        if (f->ray_trace_mode == RESTIR_MODE_ROMIS)
+            or_romis_accumulate(s, f, cf.origin, W, H, n_t, p_mat, nbr, a, b, d, it, acc);
+        else
+            or_rmis_accumulate(s, f, cf.origin, W, H, n_t, p_mat, nbr, a, b, acc);
+    }
+    or_mis_finish(f, W, H, acc, rgb);
+    free(n_t); free(p_mat); free(nbr); free(acc); free(a); free(b); free(d);
+    return rc;
+}

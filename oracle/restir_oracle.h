@@ -80,6 +80,24 @@ int or_render_frame(const or_scene* s, const restir_camera* cam, const restir_fe
                     const float* prev_b, float* n_t, float* p_mat, float* out_a, float* out_b, float* rgb,
                     int threads);
 
+/* R-MIS / R-OMIS (render.cpp:64-265) over a whole W x H image (pixel index p = y * W + x).  Buffer layouts are
+ * RESTIR_BUF_MIS_NBR ([1 + cap][W*H] uint32) and RESTIR_BUF_MIS_ACC ([or_mis_acc_rows][W*H] float). */
+uint32_t or_mis_capacity(const restir_features* f, uint32_t W, uint32_t H);
+uint32_t or_mis_acc_rows(const restir_features* f);
+void or_neighbours(const or_scene* s, const restir_features* f, uint32_t key_similar, uint32_t key_dissimilar,
+                   uint32_t W, uint32_t H, const float* n_t, const float* p_mat, uint32_t cap, uint32_t* nbr);
+void or_rmis_accumulate(const or_scene* s, const restir_features* f, const float origin[3], uint32_t W, uint32_t H,
+                        const float* n_t, const float* p_mat, const uint32_t* nbr, const float* res_a,
+                        const float* res_b, float* acc);
+void or_romis_accumulate(const or_scene* s, const restir_features* f, const float origin[3], uint32_t W, uint32_t H,
+                         const float* n_t, const float* p_mat, const uint32_t* nbr, const float* res_a,
+                         const float* res_b, const float* res_dbg, uint32_t iteration, float* acc);
+void or_mis_finish(const restir_features* f, uint32_t W, uint32_t H, const float* acc, float* rgb);
+/* Eigen CompleteOrthogonalDecomposition<MatrixXf>(A).solve(b), n <= 8, A column-major (scalar restatement). */
+void or_cod_solve(uint32_t n, const float* A, const float* b, float* x);
+int  or_render_mis(const or_scene* s, const restir_camera* cam, const restir_features* f, uint32_t seed,
+                   uint32_t frame, uint32_t W, uint32_t H, float* rgb, int threads);
+
 #ifdef __cplusplus
 }
 #endif

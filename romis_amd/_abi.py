@@ -14,17 +14,22 @@ LIB_PATH = os.path.join(HERE, "_build", "libromis_amd.so")
 RESTIR_STAGE_RIS = 1
 RESTIR_STAGE_TEMPORAL = 2
 RESTIR_STAGE_SPATIAL = 3
+RESTIR_STAGE_NEIGHBOURS = 4
 RESTIR_DEFAULT_SEED = 0x5EED0001
 RESTIR_MAX_N = 32
+RESTIR_ROMIS_MAX_TECHNIQUES = 8
 
 LIGHT_POINT, LIGHT_SEGMENT, LIGHT_PARALLELOGRAM = 0, 1, 2
 MODE_RESTIR, MODE_RMIS, MODE_ROMIS = 0, 1, 2
+MIS_EQUAL, MIS_BALANCE = 0, 1
+NEIGHBOURS_RANDOM, NEIGHBOURS_SIMILAR, NEIGHBOURS_DISSIMILAR, NEIGHBOURS_EQUAL_SIMILAR_DISSIMILAR = 0, 1, 2, 3
 
 BUF_GBUF_N_T, BUF_GBUF_P_MAT, BUF_RES_A, BUF_RES_B, BUF_RES_DBG = 0, 1, 2, 3, 4
 BUF_PREV_A, BUF_PREV_B, BUF_PREV_DBG, BUF_RGB = 5, 6, 7, 8
+BUF_MIS_NBR, BUF_MIS_ACC = 9, 10
 
-K_PRIMARY, K_RIS, K_TEMPORAL, K_SPATIAL, K_FINAL, K_PRIMARY_RIS, K_COUNT = 0, 1, 2, 3, 4, 5, 6
-KERNEL_NAMES = ["primary", "ris", "temporal", "spatial", "final", "primary_ris"]
+K_PRIMARY, K_RIS, K_TEMPORAL, K_SPATIAL, K_FINAL, K_PRIMARY_RIS, K_MIS, K_COUNT = 0, 1, 2, 3, 4, 5, 6, 7
+KERNEL_NAMES = ["primary", "ris", "temporal", "spatial", "final", "primary_ris", "mis"]
 
 STATUS_NAMES = {0: "OK", 1: "INVALID", 2: "HIP", 3: "NO_DEVICE", 4: "STATE", 5: "UNSUPPORTED", 6: "COMM"}
 
@@ -64,7 +69,13 @@ class Features(C.Structure):
                 ("spatial_reuse", C.c_uint8), ("spatial_reuse_visibility_check", C.c_uint8),
                 ("temporal_reuse", C.c_uint8), ("enable_shading", C.c_uint8),
                 ("enable_texture_mapping", C.c_uint8), ("enable_tone_mapping", C.c_uint8),
-                ("gamma", C.c_float), ("exposure", C.c_float)]
+                ("gamma", C.c_float), ("exposure", C.c_float),
+                ("neighbour_same_geometry", C.c_uint8), ("use_progressive_romis", C.c_uint8),
+                ("save_alphas_visualisation", C.c_uint8), ("reserved0", C.c_uint8),
+                ("neighbour_max_depth_difference_fraction", C.c_float),
+                ("neighbour_max_normal_angle_difference_radians", C.c_float),
+                ("max_iterations_mis", C.c_uint32), ("neighbour_selection_strategy", C.c_uint32),
+                ("mis_weight_rmis", C.c_uint32), ("progressive_update_mod", C.c_uint32)]
 
 
 class HaloSegment(C.Structure):
@@ -80,7 +91,7 @@ class Tile(C.Structure):
 
 assert C.sizeof(Light) == 88
 assert C.sizeof(Material) == 32
-assert C.sizeof(Features) == 44
+assert C.sizeof(Features) == 72
 
 
 def default_features(**overrides) -> Features:
@@ -89,7 +100,11 @@ def default_features(**overrides) -> Features:
                  num_neighbours_to_sample=5, spatial_resample_radius=10, spatial_resampling_passes=2,
                  temporal_clamp_m=20, initial_samples_visibility_check=0, unbiased_combination=0,
                  spatial_reuse=1, spatial_reuse_visibility_check=0, temporal_reuse=1, enable_shading=1,
-                 enable_texture_mapping=1, enable_tone_mapping=1, gamma=1.0, exposure=1.5)
+                 enable_texture_mapping=1, enable_tone_mapping=1, gamma=1.0, exposure=1.5,
+                 neighbour_same_geometry=1, use_progressive_romis=0, save_alphas_visualisation=1,
+                 neighbour_max_depth_difference_fraction=0.10, neighbour_max_normal_angle_difference_radians=0.436332,
+                 max_iterations_mis=5, neighbour_selection_strategy=NEIGHBOURS_SIMILAR, mis_weight_rmis=MIS_EQUAL,
+                 progressive_update_mod=1)
     for k, v in overrides.items():
         if not hasattr(f, k):
             raise AttributeError(f"Features has no field {k!r}")
@@ -129,6 +144,12 @@ SIGNATURES = {
     "restir_stage_final": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Features)]),
     "restir_debug_math": (C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                     C.POINTER(C.c_float), C.c_size_t]),
+    "restir_stage_neighbours": (C.c_int, [_P, C.POINTER(Features), C.c_uint32, C.c_uint32]),
+    "restir_stage_mis_accumulate": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Features), C.c_uint32]),
+    "restir_stage_mis_finish": (C.c_int, [_P, C.POINTER(Features)]),
+    "restir_stage_mis_capacity": (C.c_int, [_P, C.POINTER(Features), C.POINTER(C.c_uint32)]),
+    "restir_debug_cod_solve": (C.c_int, [_P, C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                         C.POINTER(C.c_float), C.c_size_t]),
     "restir_halo_plan": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                    C.c_uint32, C.POINTER(HaloSegment), C.POINTER(HaloSegment),
                                    C.POINTER(C.c_uint32)]),

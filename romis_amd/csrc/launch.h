@@ -35,6 +35,15 @@ hipError_t launch_halo_unpack(const Region& rg, const HaloSegs& hs, uint32_t N, 
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 bool launch_events_used();
 hipError_t launch_read_stream(const float4* buf, size_t n4, float* sink, hipStream_t stream);
+// R-MIS / R-OMIS over a whole W x H image (stage / frame buffers in the RESTIR_BUF_MIS_* layouts)
+hipError_t launch_mis_neighbours(const SceneDev& s, uint32_t W, uint32_t H, const FeaturesDev& f, uint32_t key_s, uint32_t key_d,
+                                 const float4* n_t, const float4* p_mat, uint32_t* nbr, hipStream_t stream);
+hipError_t launch_mis_accumulate(const SceneDev& s, uint32_t W, uint32_t H, const FeaturesDev& f, const float* origin,
+                                 const float4* n_t, const float4* p_mat, const uint32_t* nbr, const float4* ra,
+                                 const float4* rb, const float2* rdbg, uint32_t iteration, float* acc, const Tuning& tu,
+                                 hipStream_t stream);
+hipError_t launch_mis_finish(uint32_t W, uint32_t H, const FeaturesDev& f, const float* acc, float* rgb, hipStream_t stream);
+hipError_t launch_debug_cod(uint32_t n, const float* A, const float* b, float* x, uint32_t count, hipStream_t stream);
 hipError_t launch_debug_math(const float* x, const float* y, float* pw, float* ex, uint32_t n, hipStream_t stream);
 
 }  // namespace romis

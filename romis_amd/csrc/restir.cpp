@@ -139,6 +139,10 @@ struct restir_ctx {
     Region stage_rg{};
     bool stage_ok = false;
 
+    // R-MIS / R-OMIS: neighbourhoods [1 + cap][pixels] and accumulators [rows][pixels] (RESTIR_BUF_MIS_*)
+    DevBuf mis_nbr, mis_acc;
+    uint32_t mis_cap = 0, mis_rows = 0;
+
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -174,6 +178,15 @@ void restir_features_default(restir_features* out) {
     out->enable_tone_mapping = 1;
     out->gamma = 1.0f;
     out->exposure = 1.5f;
+    out->neighbour_same_geometry = 1;
+    out->use_progressive_romis = 0;
+    out->save_alphas_visualisation = 1;
+    out->neighbour_max_depth_difference_fraction = 0.10f;
+    out->neighbour_max_normal_angle_difference_radians = 0.436332f;
+    out->max_iterations_mis = 5;
+    out->neighbour_selection_strategy = RESTIR_NEIGHBOURS_SIMILAR;
+    out->mis_weight_rmis = RESTIR_MIS_EQUAL;
+    out->progressive_update_mod = 1;
 }
 
 uint32_t restir_rng_key(uint32_t seed, uint32_t frame, uint32_t stage, uint32_t pass) {
@@ -297,9 +310,19 @@ namespace {
 
 restir_status check_features(const restir_features* f) {
     if (!f) return fail(RESTIR_ERR_INVALID, "features is NULL");
-    if (f->ray_trace_mode != RESTIR_MODE_RESTIR)
-        return fail(RESTIR_ERR_UNSUPPORTED, "rayTraceMode %u: only ReSTIR is implemented on this path (RMIS/ROMIS are out "
-                                            "of scope, SURVEY.md §2 #12)", f->ray_trace_mode);
+    if (f->ray_trace_mode > RESTIR_MODE_ROMIS)
+        return fail(RESTIR_ERR_INVALID, "Unsupported ray-tracing render mode %u requested from entry point", f->ray_trace_mode);
+    if (f->ray_trace_mode != RESTIR_MODE_RESTIR) {
+        if (f->neighbour_selection_strategy > RESTIR_NEIGHBOURS_EQUAL_SIMILAR_DISSIMILAR)
+            return fail(RESTIR_ERR_INVALID, "neighbourSelectionStrategy %u", f->neighbour_selection_strategy);
+        if (f->ray_trace_mode == RESTIR_MODE_RMIS && f->mis_weight_rmis > RESTIR_MIS_BALANCE)   // render.cpp:94
+            return fail(RESTIR_ERR_INVALID, "Unhandled MIS weight type: %u", f->mis_weight_rmis);
+        if (f->ray_trace_mode == RESTIR_MODE_ROMIS && f->num_neighbours_to_sample + 1u > RESTIR_ROMIS_MAX_TECHNIQUES)
+            return fail(RESTIR_ERR_UNSUPPORTED, "R-OMIS with %u neighbours: at most %u techniques per pixel",
+                        f->num_neighbours_to_sample, RESTIR_ROMIS_MAX_TECHNIQUES);
+        if (f->ray_trace_mode == RESTIR_MODE_ROMIS && f->use_progressive_romis && f->progressive_update_mod == 0)
+            return fail(RESTIR_ERR_INVALID, "progressiveUpdateMod 0 (iteration %% 0)");
+    }
     if (f->num_samples_in_reservoir < 1 || f->num_samples_in_reservoir > RESTIR_MAX_N)
         return fail(RESTIR_ERR_INVALID, "numSamplesInReservoir %u outside 1..%u", f->num_samples_in_reservoir, RESTIR_MAX_N);
     if (f->spatial_resample_radius > 4096) return fail(RESTIR_ERR_INVALID, "spatialResampleRadius too large");
@@ -322,7 +345,51 @@ FeaturesDev to_dev(const restir_features* f) {
     d.tone_map = f->enable_tone_mapping;
     d.gamma = f->gamma;
     d.exposure = f->exposure;
+    d.mode = f->ray_trace_mode;
+    d.strategy = f->neighbour_selection_strategy;
+    d.same_geom = f->neighbour_same_geometry;
+    d.depth_frac = f->neighbour_max_depth_difference_fraction;
+    d.normal_rad = f->neighbour_max_normal_angle_difference_radians;
+    d.mis_weight = f->mis_weight_rmis;
+    d.progressive = f->use_progressive_romis;
+    d.prog_mod = f->progressive_update_mod;
+    d.iterations = f->max_iterations_mis;
     return d;
+}
+
+// neighbourhood capacity of generateResampleIndicesGrid's output (neighbour_selection.cpp:45-105): k + 1, or the
+// whole window for the strategies whose size arithmetic can take every member of a class
+uint32_t mis_capacity(const restir_features* f, uint32_t W, uint32_t H) {
+    const uint32_t k1 = f->num_neighbours_to_sample + 1u;
+    if (f->neighbour_selection_strategy == RESTIR_NEIGHBOURS_RANDOM || f->neighbour_selection_strategy == RESTIR_NEIGHBOURS_SIMILAR)
+        return k1;
+    const uint64_t side = 2ull * f->spatial_resample_radius + 1ull;
+    const uint64_t win = std::min<uint64_t>(side, W) * std::min<uint64_t>(side, H);
+    return win > k1 ? (uint32_t)win : k1;
+}
+uint32_t mis_acc_rows(const restir_features* f) {
+    const uint32_t T = f->num_neighbours_to_sample + 1u;
+    return f->ray_trace_mode == RESTIR_MODE_ROMIS ? T * T + 6u * T + 3u : 3u;
+}
+restir_status ensure_mis(restir_ctx* c, const restir_features* f, uint32_t W, uint32_t H) {
+    if (f->ray_trace_mode == RESTIR_MODE_RESTIR) return fail(RESTIR_ERR_INVALID, "the MIS stages need rayTraceMode RMIS or ROMIS");
+    const size_t npx = (size_t)W * H;
+    c->mis_cap = mis_capacity(f, W, H);
+    c->mis_rows = mis_acc_rows(f);
+    ST_TRY(c->mis_nbr.ensure((size_t)(1u + c->mis_cap) * npx * 4));
+    ST_TRY(c->mis_acc.ensure((size_t)c->mis_rows * npx * 4));
+    return RESTIR_OK;
+}
+// renderROMIS reads neighborhood[0..k] (render.cpp:155-181): every pixel's window must hold k candidates
+restir_status check_romis_window(const restir_features* f, uint32_t W, uint32_t H) {
+    if (f->ray_trace_mode != RESTIR_MODE_ROMIS || f->neighbour_selection_strategy == RESTIR_NEIGHBOURS_RANDOM) return RESTIR_OK;
+    const uint64_t corner = std::min<uint64_t>((uint64_t)f->spatial_resample_radius + 1u, W) *
+                            std::min<uint64_t>((uint64_t)f->spatial_resample_radius + 1u, H);
+    if (corner - 1u < f->num_neighbours_to_sample)
+        return fail(RESTIR_ERR_INVALID, "R-OMIS: a %ux%u image with radius %u leaves fewer than k = %u candidates in a corner window "
+                                        "(the reference indexes past the neighbourhood)", W, H, f->spatial_resample_radius,
+                    f->num_neighbours_to_sample);
+    return RESTIR_OK;
 }
 
 restir_status ensure_work(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N, bool debug) {
@@ -655,6 +722,44 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
     return RESTIR_OK;
 }
 
+// renderRMIS / renderROMIS (render.cpp:64-265) over the whole image; the caller holds c->mu.
+static restir_status render_mis(restir_ctx* c, const restir_camera* cam, const restir_features* features, uint32_t W,
+                                uint32_t H, float* out_rgb) {
+    if (W == 0 || H == 0) return fail(RESTIR_ERR_INVALID, "empty image %ux%u", W, H);
+    ST_TRY(check_romis_window(features, W, H));
+    const FeaturesDev f = to_dev(features);
+    ST_TRY(ensure_work(c, W, H, f.N, true));
+    ST_TRY(ensure_mis(c, features, W, H));
+    ST_TRY(c->rgb.ensure((size_t)W * H * 12));
+    c->rgb_w = W; c->rgb_h = H;
+    c->stage_ok = false;   // the stage buffers now hold this render's state
+    const CameraDev camd = camera_dev(cam);
+    const Region view = make_region(W, H, 0, 0, W, H, 0, 0, W, H);
+    const uint32_t frame = c->frame_index++;
+    const SceneDev& s = c->sdev;
+    float4* nt = c->n_t.as<float4>();
+    float4* pm = c->p_mat.as<float4>();
+    TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, nt, pm, nullptr, c->tuning, c->stream));
+    TIMED(c, RESTIR_K_MIS, launch_mis_neighbours(s, W, H, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_NEIGHBOURS, 0),
+                                                 restir_rng_key(c->seed, frame, RESTIR_STAGE_NEIGHBOURS, 1), nt, pm,
+                                                 c->mis_nbr.as<uint32_t>(), c->stream));
+    HIP_TRY(hipMemsetAsync(c->mis_acc.p, 0, (size_t)c->mis_rows * W * H * 4, c->stream));
+    for (uint32_t it = 0; it < features->max_iterations_mis; it++) {
+        TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, it), camd.origin, nt, pm,
+                                          c->ra[0].as<float4>(), c->rb[0].as<float4>(), c->dbg[0].as<float2>(), c->tuning,
+                                          c->queue, c->stream));
+        TIMED(c, RESTIR_K_MIS, launch_mis_accumulate(s, W, H, f, camd.origin, nt, pm, c->mis_nbr.as<uint32_t>(),
+                                                     c->ra[0].as<float4>(), c->rb[0].as<float4>(), c->dbg[0].as<float2>(), it,
+                                                     c->mis_acc.as<float>(), c->tuning, c->stream));
+    }
+    TIMED(c, RESTIR_K_MIS, launch_mis_finish(W, H, f, c->mis_acc.as<float>(), c->rgb.as<float>(), c->stream));
+    if (out_rgb) {
+        HIP_TRY(hipMemcpyAsync(out_rgb, c->rgb.p, (size_t)W * H * 12, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return RESTIR_OK;
+}
+
 // renderReSTIR (render.cpp:28-62)
 restir_status restir_render(restir_ctx* c, const restir_camera* cam, const restir_features* features, uint32_t width,
                             uint32_t height, const restir_tile* tile, const restir_frame* prev, restir_frame** out_next,
@@ -666,6 +771,12 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     std::lock_guard<std::mutex> lk(c->mu);
     if (!c->has_scene) return fail(RESTIR_ERR_STATE, "restir_render before restir_set_scene");
     HIP_TRY(hipSetDevice(c->device));
+    if (features->ray_trace_mode != RESTIR_MODE_RESTIR) {   // renderRayTraced's switch (render.cpp:274-279)
+        if (tile && (tile->global_width != width || tile->global_height != height || tile->x0 || tile->y0 ||
+                     tile->width != width || tile->height != height))
+            return fail(RESTIR_ERR_UNSUPPORTED, "R-MIS / R-OMIS render whole images only (no screen tiles)");
+        return render_mis(c, cam, features, width, height, out_rgb);
+    }
 
     restir_tile t{};
     if (tile) {
@@ -829,6 +940,12 @@ static restir_status stage_buffer(restir_ctx* c, restir_buffer which, DevBuf** o
         case RESTIR_BUF_PREV_B: *out = &c->rb[prv]; *bytes = npx * c->N * 16; break;
         case RESTIR_BUF_PREV_DBG: *out = &c->dbg[prv]; *bytes = npx * c->N * 8; break;
         case RESTIR_BUF_RGB: *out = &c->rgb; *bytes = (size_t)c->rgb_w * c->rgb_h * 12; break;
+        case RESTIR_BUF_MIS_NBR:
+            if (!c->mis_cap) return fail(RESTIR_ERR_STATE, "MIS buffers: call restir_stage_mis_capacity first");
+            *out = &c->mis_nbr; *bytes = (size_t)(1u + c->mis_cap) * npx * 4; break;
+        case RESTIR_BUF_MIS_ACC:
+            if (!c->mis_cap) return fail(RESTIR_ERR_STATE, "MIS buffers: call restir_stage_mis_capacity first");
+            *out = &c->mis_acc; *bytes = (size_t)c->mis_rows * npx * 4; break;
         default: return fail(RESTIR_ERR_INVALID, "unknown buffer %d", (int)which);
     }
     return RESTIR_OK;
@@ -945,6 +1062,73 @@ restir_status restir_stage_final(restir_ctx* c, const restir_camera* cam, const 
     TIMED(c, RESTIR_K_FINAL, launch_final(c->sdev, c->stage_rg, d, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                                           c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->rgb.as<float>(), c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return RESTIR_OK;
+}
+
+restir_status restir_stage_mis_capacity(restir_ctx* c, const restir_features* f, uint32_t* out_cap) {
+    if (!out_cap) return fail(RESTIR_ERR_INVALID, "out_cap is NULL");
+    STAGE_PRELUDE();
+    FeaturesDev d;
+    ST_TRY(stage_features(c, f, d));
+    ST_TRY(ensure_mis(c, f, c->vw, c->vh));
+    *out_cap = c->mis_cap;
+    return RESTIR_OK;
+}
+
+restir_status restir_stage_neighbours(restir_ctx* c, const restir_features* f, uint32_t key_similar, uint32_t key_dissimilar) {
+    STAGE_PRELUDE();
+    FeaturesDev d;
+    ST_TRY(stage_features(c, f, d));
+    ST_TRY(ensure_mis(c, f, c->vw, c->vh));
+    TIMED(c, RESTIR_K_MIS, launch_mis_neighbours(c->sdev, c->vw, c->vh, d, key_similar, key_dissimilar, c->n_t.as<float4>(),
+                                                 c->p_mat.as<float4>(), c->mis_nbr.as<uint32_t>(), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RESTIR_OK;
+}
+
+restir_status restir_stage_mis_accumulate(restir_ctx* c, const restir_camera* cam, const restir_features* f, uint32_t iteration) {
+    if (!cam) return fail(RESTIR_ERR_INVALID, "camera is NULL");
+    STAGE_PRELUDE();
+    FeaturesDev d;
+    ST_TRY(stage_features(c, f, d));
+    ST_TRY(check_romis_window(f, c->vw, c->vh));
+    ST_TRY(ensure_mis(c, f, c->vw, c->vh));
+    const CameraDev camd = camera_dev(cam);
+    const int cur = c->cur;
+    if (iteration == 0) HIP_TRY(hipMemsetAsync(c->mis_acc.p, 0, (size_t)c->mis_rows * c->vw * c->vh * 4, c->stream));
+    TIMED(c, RESTIR_K_MIS, launch_mis_accumulate(c->sdev, c->vw, c->vh, d, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
+                                                 c->mis_nbr.as<uint32_t>(), c->ra[cur].as<float4>(), c->rb[cur].as<float4>(),
+                                                 c->dbg[cur].as<float2>(), iteration, c->mis_acc.as<float>(), c->tuning,
+                                                 c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RESTIR_OK;
+}
+
+restir_status restir_stage_mis_finish(restir_ctx* c, const restir_features* f) {
+    STAGE_PRELUDE();
+    FeaturesDev d;
+    ST_TRY(stage_features(c, f, d));
+    if (!c->mis_cap) return fail(RESTIR_ERR_STATE, "MIS buffers: run restir_stage_mis_accumulate first");
+    TIMED(c, RESTIR_K_MIS, launch_mis_finish(c->vw, c->vh, d, c->mis_acc.as<float>(), c->rgb.as<float>(), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RESTIR_OK;
+}
+
+restir_status restir_debug_cod_solve(restir_ctx* c, uint32_t n, const float* A, const float* b, float* x, size_t count) {
+    if (!c || (count && (!A || !b || !x))) return fail(RESTIR_ERR_INVALID, "null argument");
+    if (n < 1 || n > RESTIR_ROMIS_MAX_TECHNIQUES) return fail(RESTIR_ERR_INVALID, "n = %u outside 1..%u", n, RESTIR_ROMIS_MAX_TECHNIQUES);
+    if (count > 0xFFFFFFFFull) return fail(RESTIR_ERR_INVALID, "count too large");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    DevBuf bA, bb, bx;
+    ST_TRY(bA.upload(A, count * n * n * 4, c->stream));
+    ST_TRY(bb.upload(b, count * n * 4, c->stream));
+    ST_TRY(bx.ensure(count * n * 4));
+    hipError_t e = launch_debug_cod(n, bA.as<float>(), bb.as<float>(), bx.as<float>(), (uint32_t)count, c->stream);
+    if (e != hipSuccess) return fail(RESTIR_ERR_HIP, "debug cod launch: %s", hipGetErrorString(e));
+    HIP_TRY(hipMemcpyAsync(x, bx.p, count * n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    bA.release(); bb.release(); bx.release();
     return RESTIR_OK;
 }
 

@@ -114,6 +114,13 @@ struct FeaturesDev {
     uint32_t clamp_m;
     uint32_t initial_vis, unbiased, spatial_vis, shading, tone_map;
     float gamma, exposure;
+    // R-MIS / R-OMIS and the neighbour-selection heuristic (common.h:110-121)
+    uint32_t mode;            // restir_mode
+    uint32_t strategy;        // restir_neighbour_strategy
+    uint32_t same_geom;
+    float depth_frac, normal_rad;
+    uint32_t mis_weight;      // restir_mis_weight
+    uint32_t progressive, prog_mod, iterations;
 };
 
 }  // namespace romis

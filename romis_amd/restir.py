@@ -178,6 +178,65 @@ class Renderer:
         check(self.lib, self.lib.restir_stage_final(self.ctx, C.byref(camera), C.byref(features)),
               "restir_stage_final")
 
+    # ---- R-MIS / R-OMIS (render.cpp:64-265) ------------------------------------------------------------
+    def render_mis(self, camera, width: int, height: int, features) -> np.ndarray:
+        """renderRMIS / renderROMIS by features.ray_trace_mode: the screen image (row 0 = top).  No grid is
+        returned, as renderRayTraced returns std::nullopt for these modes (render.cpp:274-279)."""
+        rgb, _ = self.render_restir(None, camera, width, height, features, want_grid=False)
+        return rgb
+
+    def mis_capacity(self, features) -> int:
+        cap = C.c_uint32()
+        check(self.lib, self.lib.restir_stage_mis_capacity(self.ctx, C.byref(features), C.byref(cap)),
+              "restir_stage_mis_capacity")
+        return cap.value
+
+    def stage_neighbours(self, features, key_similar: int, key_dissimilar: int) -> None:
+        check(self.lib, self.lib.restir_stage_neighbours(self.ctx, C.byref(features), key_similar, key_dissimilar),
+              "restir_stage_neighbours")
+
+    def stage_mis_accumulate(self, camera, features, iteration: int) -> None:
+        check(self.lib, self.lib.restir_stage_mis_accumulate(self.ctx, C.byref(camera), C.byref(features), iteration),
+              "restir_stage_mis_accumulate")
+
+    def stage_mis_finish(self, features) -> None:
+        check(self.lib, self.lib.restir_stage_mis_finish(self.ctx, C.byref(features)), "restir_stage_mis_finish")
+
+    def mis_buffers(self, features, nbr: np.ndarray | None = None, acc: np.ndarray | None = None):
+        """Upload (when given) and download the MIS_NBR (uint32 [1 + cap][pixels]) and MIS_ACC (float
+        [rows][pixels]) stage buffers."""
+        w, h, _ = self.stage_shape
+        cap = self.mis_capacity(features)
+        T = features.num_neighbours_to_sample + 1
+        rows = T * T + 6 * T + 3 if features.ray_trace_mode == _abi.MODE_ROMIS else 3
+        for which, arr, dt, shape in [(_abi.BUF_MIS_NBR, nbr, np.uint32, (1 + cap, w * h)),
+                                      (_abi.BUF_MIS_ACC, acc, np.float32, (rows, w * h))]:
+            if arr is not None:
+                a = np.ascontiguousarray(arr, dtype=dt).reshape(shape)
+                check(self.lib, self.lib.restir_stage_upload(self.ctx, which, a.ctypes.data, a.nbytes),
+                      "restir_stage_upload")
+        out = []
+        for which, dt, shape in [(_abi.BUF_MIS_NBR, np.uint32, (1 + cap, w * h)),
+                                 (_abi.BUF_MIS_ACC, np.float32, (rows, w * h))]:
+            a = np.zeros(shape, dt)
+            check(self.lib, self.lib.restir_stage_download(self.ctx, which, a.ctypes.data, a.nbytes),
+                  "restir_stage_download")
+            out.append(a)
+        return tuple(out)
+
+    def debug_cod_solve(self, A: np.ndarray, b: np.ndarray) -> np.ndarray:
+        """Batched least squares (A [count][n][n] row-major numpy, b [count][n]) with the device routine of the
+        R-OMIS finish (Eigen CompleteOrthogonalDecomposition::solve, render_utils.h:52)."""
+        A = np.asarray(A, np.float32)
+        count, n, _ = A.shape
+        Ac = np.ascontiguousarray(np.transpose(A, (0, 2, 1)), np.float32)   # column-major per system
+        bc = np.ascontiguousarray(b, np.float32).reshape(count, n)
+        x = np.zeros((count, n), np.float32)
+        FP = C.POINTER(C.c_float)
+        check(self.lib, self.lib.restir_debug_cod_solve(self.ctx, n, Ac.ctypes.data_as(FP), bc.ctypes.data_as(FP),
+                                                        x.ctypes.data_as(FP), count), "restir_debug_cod_solve")
+        return x
+
     def debug_math(self, x: np.ndarray, y: np.ndarray):
         x = np.ascontiguousarray(x, np.float32)
         y = np.ascontiguousarray(y, np.float32)

@@ -1,0 +1,153 @@
+"""GPU parity of R-MIS / R-OMIS (renderRMIS / renderROMIS, render.cpp:64-265) against the oracle, through the C ABI.
+Stage-isolated like test_gpu_parity.py: each stage gets the oracle's inputs, so a mismatch points at one kernel.
+Bar: bit-exact (neighbourhood indices, accumulators, least-squares solutions, RGB) -- device and oracle evaluate
+the same float operations in the same order.  Against the reference's own Eigen the solve agrees to COD_TOL
+(tests/test_mis_oracle.py).
+"""
+import numpy as np
+import pytest
+
+from romis_amd import _abi, scene
+
+pytestmark = pytest.mark.gpu
+
+W, H = 48, 32
+SEED = _abi.RESTIR_DEFAULT_SEED
+COD_TOL = 2e-4
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    from romis_amd import build, restir
+    build.build()
+    r = restir.Renderer(0)
+    yield r
+    r.close()
+
+
+def key(oracle, stage, p=0, frame=0):
+    return oracle.lib().or_rng_key(SEED, frame, stage, p)
+
+
+def bits_equal(got, want, what):
+    g = np.ascontiguousarray(got).reshape(-1).view(np.uint32)
+    w = np.ascontiguousarray(want).reshape(-1).view(np.uint32)
+    assert g.shape == w.shape, what
+    bad = np.flatnonzero(g != w)
+    assert bad.size == 0, f"{what}: {bad.size}/{g.size} words differ, first {bad[:4].tolist()}"
+
+
+def setup(gpu, oracle, name, f):
+    sc = scene.bench_scene(name)
+    gpu.set_scene(sc)
+    osc = oracle.OracleScene(sc)
+    cam = scene.camera_for(name, W, H)
+    gpu.stage_configure(W, H, f.num_samples_in_reservoir)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    gpu.upload(_abi.BUF_GBUF_N_T, n_t)
+    gpu.upload(_abi.BUF_GBUF_P_MAT, p_mat)
+    origin = np.asarray(list(oracle.camera_frame(cam).origin), np.float32)
+    return osc, cam, n_t, p_mat, origin
+
+
+def test_cod_solve_bit_exact_with_oracle(gpu, oracle):
+    from tests.test_mis_oracle import load_cod_fixtures
+    cases = load_cod_fixtures()
+    by_n = {}
+    for kind, A, b, xe, rank in cases:
+        by_n.setdefault(A.shape[0], []).append((A, b, xe))
+    for n, cs in by_n.items():
+        A = np.stack([c[0] for c in cs])
+        b = np.stack([c[1] for c in cs])
+        xg = gpu.debug_cod_solve(A, b)
+        for i, (Ai, bi, xe) in enumerate(cs):
+            bits_equal(xg[i], oracle.cod_solve(Ai, bi), f"n={n} case {i}")
+            assert np.abs(xg[i] - xe).max() <= COD_TOL * max(float(np.abs(xe).max()), 1e-30)
+
+
+@pytest.mark.parametrize("name", ["nightclub_128pt", "cornell_parallelogram"])
+@pytest.mark.parametrize("strategy,radius", [(0, 10), (1, 10), (1, 3), (2, 3), (3, 3), (3, 10)])
+def test_neighbours_bit_exact(gpu, oracle, name, strategy, radius):
+    f = _abi.default_features(ray_trace_mode=_abi.MODE_RMIS, neighbour_selection_strategy=strategy,
+                              spatial_resample_radius=radius, num_samples_in_reservoir=1)
+    osc, cam, n_t, p_mat, origin = setup(gpu, oracle, name, f)
+    ks, kd = key(oracle, _abi.RESTIR_STAGE_NEIGHBOURS, 0), key(oracle, _abi.RESTIR_STAGE_NEIGHBOURS, 1)
+    gpu.stage_neighbours(f, ks, kd)
+    got, _ = gpu.mis_buffers(f)
+    want = oracle.neighbours(osc, f, ks, kd, W, H, n_t, p_mat)
+    assert got.shape == want.shape
+    bits_equal(got[0], want[0], "neighbourhood sizes")
+    for p in range(W * H):
+        c = int(want[0, p])
+        if not np.array_equal(got[1:1 + c, p], want[1:1 + c, p]):
+            raise AssertionError(f"pixel {p}: {got[1:1 + c, p].tolist()} != {want[1:1 + c, p].tolist()}")
+
+
+MIS_CASES = {
+    "rmis_equal": dict(ray_trace_mode=_abi.MODE_RMIS, num_samples_in_reservoir=2),
+    "rmis_balance": dict(ray_trace_mode=_abi.MODE_RMIS, num_samples_in_reservoir=2, mis_weight_rmis=_abi.MIS_BALANCE),
+    "rmis_dissimilar": dict(ray_trace_mode=_abi.MODE_RMIS, num_samples_in_reservoir=1, spatial_resample_radius=2,
+                            neighbour_selection_strategy=_abi.NEIGHBOURS_DISSIMILAR),
+    "romis_direct": dict(ray_trace_mode=_abi.MODE_ROMIS, num_samples_in_reservoir=2),
+    "romis_random_k2": dict(ray_trace_mode=_abi.MODE_ROMIS, num_samples_in_reservoir=1, num_neighbours_to_sample=2,
+                            neighbour_selection_strategy=_abi.NEIGHBOURS_RANDOM),
+    "romis_k7": dict(ray_trace_mode=_abi.MODE_ROMIS, num_samples_in_reservoir=1, num_neighbours_to_sample=7),
+    "romis_progressive": dict(ray_trace_mode=_abi.MODE_ROMIS, num_samples_in_reservoir=6, use_progressive_romis=1),
+    "romis_progressive_mod2": dict(ray_trace_mode=_abi.MODE_ROMIS, num_samples_in_reservoir=6,
+                                   use_progressive_romis=1, progressive_update_mod=2),
+}
+
+
+@pytest.mark.parametrize("case", sorted(MIS_CASES))
+def test_mis_accumulate_and_finish_bit_exact(gpu, oracle, case):
+    f = _abi.default_features(**MIS_CASES[case])
+    f.max_iterations_mis = 3
+    osc, cam, n_t, p_mat, origin = setup(gpu, oracle, "nightclub_128pt", f)
+    nbr = oracle.neighbours(osc, f, key(oracle, 4, 0), key(oracle, 4, 1), W, H, n_t, p_mat)
+    gpu.mis_buffers(f, nbr=nbr)
+    acc = np.zeros((oracle.mis_acc_rows(f), W * H), np.float32)
+    for it in range(f.max_iterations_mis):
+        a, b, d = oracle.ris(osc, f, key(oracle, _abi.RESTIR_STAGE_RIS, it), origin, W, H, n_t, p_mat)
+        gpu.upload(_abi.BUF_RES_A, a)
+        gpu.upload(_abi.BUF_RES_B, b)
+        gpu.upload(_abi.BUF_RES_DBG, d)
+        gpu.stage_mis_accumulate(cam, f, it)
+        if f.ray_trace_mode == _abi.MODE_ROMIS:
+            oracle.romis_accumulate(osc, f, origin, W, H, n_t, p_mat, nbr, a, b, d, it, acc)
+        else:
+            oracle.rmis_accumulate(osc, f, origin, W, H, n_t, p_mat, nbr, a, b, acc)
+        _, got = gpu.mis_buffers(f)
+        bits_equal(got, acc, f"{case}: accumulators after iteration {it}")
+    gpu.stage_mis_finish(f)
+    bits_equal(gpu.download(_abi.BUF_RGB), oracle.mis_finish(f, W, H, acc), f"{case}: screen")
+
+
+@pytest.mark.parametrize("name,case", [("nightclub_128pt", "rmis_equal"), ("nightclub_128pt", "romis_direct"),
+                                       ("cornell_parallelogram", "rmis_balance"),
+                                       ("cornell_parallelogram", "romis_progressive"),
+                                       ("nightclub_512", "romis_random_k2")])
+def test_render_mis_matches_oracle(gpu, oracle, name, case):
+    f = _abi.default_features(**MIS_CASES[case])
+    sc = scene.bench_scene(name)
+    gpu.set_scene(sc)
+    cam = scene.camera_for(name, W, H)
+    gpu.set_seed(SEED, 0)
+    got = gpu.render_mis(cam, W, H, f)
+    want = oracle.render_mis(oracle.OracleScene(sc), cam, f, W, H, SEED, 0)
+    bits_equal(got, want, f"{name} {case}")
+    assert np.isfinite(got).all() and got.max() > 0.0
+
+
+def test_mis_errors(gpu, oracle):
+    sc = scene.bench_scene("nightclub_128pt")
+    gpu.set_scene(sc)
+    cam = scene.camera_for("nightclub_128pt", W, H)
+    f = _abi.default_features(ray_trace_mode=_abi.MODE_ROMIS, num_neighbours_to_sample=8)
+    with pytest.raises(_abi.RestirError, match="UNSUPPORTED"):
+        gpu.render_mis(cam, W, H, f)
+    f = _abi.default_features(ray_trace_mode=3)
+    with pytest.raises(_abi.RestirError, match="INVALID"):
+        gpu.render_mis(cam, W, H, f)
+    f = _abi.default_features(ray_trace_mode=_abi.MODE_ROMIS, spatial_resample_radius=1)   # 2x2 corner < k
+    with pytest.raises(_abi.RestirError, match="INVALID"):
+        gpu.render_mis(cam, W, H, f)

@@ -459,7 +459,10 @@ def test_measured_read_bandwidth_is_plausible(gpu):
 def test_errors_are_reported(gpu):
     from romis_amd._abi import RestirError
     cam = scene.nightclub_camera(W, H)
-    with pytest.raises(RestirError, match="UNSUPPORTED"):
-        gpu.render_restir(None, cam, W, H, _abi.default_features(ray_trace_mode=_abi.MODE_ROMIS))
+    with pytest.raises(RestirError, match="UNSUPPORTED"):   # R-MIS / R-OMIS render whole images only
+        tile = _abi.Tile(W, H, 0, 0, W // 2, H, 0, 0, W // 2 + 10, H)
+        gpu.render_restir(None, cam, W, H, _abi.default_features(ray_trace_mode=_abi.MODE_ROMIS), tile=tile)
+    with pytest.raises(RestirError, match="INVALID"):
+        gpu.render_restir(None, cam, W, H, _abi.default_features(ray_trace_mode=7))
     with pytest.raises(RestirError, match="INVALID"):
         gpu.render_restir(None, cam, W, H, _abi.default_features(num_samples_in_reservoir=0))

@@ -1614,14 +1614,16 @@ __device__ __forceinline__ float aucw_reciprocal(const SceneDev& s, const Featur
     return 1.0f / arbitraryWeight;
 }
 
-// One R-OMIS iteration (render.cpp:139-231): technique matrix A, contribution vectors b and, when progressive, the
-// alphas and colour estimate, held in registers for the pixel (T = k + 1 techniques, a compile-time constant).
-template <int T, bool LDS_BVH>
+// One R-OMIS iteration (render.cpp:139-231): technique matrix A and contribution vectors b held in registers for
+// the pixel (T = k + 1 techniques, a compile-time constant; every index static, so nothing spills to scratch), plus
+// the progressive estimator's colour (PROG).  The progressive alphas are solved beforehand by k_romis_alphas and only
+// read here.
+template <int T, bool LDS_BVH, bool PROG>
 __device__ __forceinline__ void romis_body(const SceneDev& s, uint32_t W, uint32_t H, const FeaturesDev& f, v3 origin,
                                            const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                            const uint32_t* __restrict__ nbr, const float4* __restrict__ ra,
                                            const float4* __restrict__ rb, const float2* __restrict__ rdbg,
-                                           uint32_t iteration, float* __restrict__ acc) {
+                                           float* __restrict__ acc) {
     const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= W * H) return;
@@ -1631,8 +1633,8 @@ __device__ __forceinline__ void romis_body(const SceneDev& s, uint32_t W, uint32
     const int32_t fractionOfTotalSamples = (int32_t)N / (int32_t)T;
     float* Am = acc;
     float* Bv = acc + (size_t)T * T * npx;
-    float* Al = Bv + (size_t)3 * T * npx;
-    float* Col = Al + (size_t)3 * T * npx;
+    const float* Al = Bv + (size_t)3 * T * npx;
+    float* Col = Bv + (size_t)6 * T * npx;
     const Px cur = make_px(s, n_t[p], p_mat[p], origin);
     float A[T * T], bb[3][T], al[3][T];
 #pragma unroll
@@ -1640,30 +1642,34 @@ __device__ __forceinline__ void romis_body(const SceneDev& s, uint32_t W, uint32
 #pragma unroll
     for (int ch = 0; ch < 3; ch++)
 #pragma unroll
-        for (int i = 0; i < T; i++) { bb[ch][i] = Bv[(size_t)(ch * T + i) * npx + p]; al[ch][i] = Al[(size_t)(ch * T + i) * npx + p]; }
-    v3 fc = mk(Col[p], Col[npx + p], Col[2 * npx + p]);
-    if (f.progressive && iteration >= 1u && iteration % f.prog_mod == 0u)
-        for (int ch = 0; ch < 3; ch++) cod_solve_dev<T>(A, bb[ch], al[ch]);
-    uint32_t qd[T];
-#pragma unroll
-    for (int d = 0; d < T; d++) qd[d] = nbr[(size_t)(1 + d) * npx + p];
+        for (int i = 0; i < T; i++) {
+            bb[ch][i] = Bv[(size_t)(ch * T + i) * npx + p];
+            if (PROG) al[ch][i] = Al[(size_t)(ch * T + i) * npx + p];
+        }
+    v3 fc = mk(0.0f, 0.0f, 0.0f);
+    if (PROG) fc = mk(Col[p], Col[npx + p], Col[2 * npx + p]);
     for (int pi = 0; pi < T; pi++) {
-        if (f.progressive) fc = vadd(fc, mk(al[0][pi], al[1][pi], al[2][pi]));
+        if (PROG)
+            fc = vadd(fc, mk(Al[(size_t)pi * npx + p], Al[(size_t)(T + pi) * npx + p], Al[(size_t)(2 * T + pi) * npx + p]));
         const uint32_t q = nbr[(size_t)(1 + pi) * npx + p];
         for (uint32_t si = 0; si < N; si++) {
             const float4 a = ra[(size_t)si * npx + q], b4 = rb[(size_t)si * npx + q];
             const v3 pos = xyz(a), col = xyz(b4);
+            // the T target-pdf evaluations run as one rolled loop (one inlined copy: 4x fewer VGPRs than unrolled);
+            // each result lands in its static register slot by selects
             float v[T];
-#pragma unroll
+#pragma unroll 1
             for (int d = 0; d < T; d++) {
-                const uint32_t qq = qd[d];
+                const uint32_t qq = nbr[(size_t)(1 + d) * npx + p];
                 const float4 db = rb[(size_t)si * npx + qq];
                 const float2 dd = rdbg[(size_t)si * npx + qq];
-                v[d] = aucw_reciprocal(s, f, make_px(s, n_t[qq], p_mat[qq], origin), (float)__float_as_uint(db.w), dd.x,
-                                       dd.y, pos, col);
+                const float val = aucw_reciprocal(s, f, make_px(s, n_t[qq], p_mat[qq], origin), (float)__float_as_uint(db.w),
+                                                  dd.x, dd.y, pos, col);
+#pragma unroll
+                for (int e = 0; e < T; e++) v[e] = e == d ? val : v[e];
             }
             const v3 sc = visible(bvh, cur.P, pos) ? shade(s, f, cur, pos, col) : mk(0.0f, 0.0f, 0.0f);
-            if (f.progressive) {
+            if (PROG) {
                 v3 sa = mk(0.0f, 0.0f, 0.0f);
                 float sf = ROMIS_FLT_MIN;
 #pragma unroll
@@ -1699,22 +1705,40 @@ __device__ __forceinline__ void romis_body(const SceneDev& s, uint32_t W, uint32
 #pragma unroll
     for (int ch = 0; ch < 3; ch++)
 #pragma unroll
-        for (int i = 0; i < T; i++) { Bv[(size_t)(ch * T + i) * npx + p] = bb[ch][i]; Al[(size_t)(ch * T + i) * npx + p] = al[ch][i]; }
-    Col[p] = fc.x; Col[npx + p] = fc.y; Col[2 * npx + p] = fc.z;
+        for (int i = 0; i < T; i++) Bv[(size_t)(ch * T + i) * npx + p] = bb[ch][i];
+    if (PROG) { Col[p] = fc.x; Col[npx + p] = fc.y; Col[2 * npx + p] = fc.z; }
 }
 
+// Progressive R-OMIS (render.cpp:148-152): at the start of iteration i >= 1 with i % progressiveUpdateMod == 0, each
+// colour's alpha vector = the least-squares solution over the technique matrix and contribution vector so far.
+template <int T>
+__device__ __forceinline__ void romis_alphas_body(uint32_t W, uint32_t H, float* __restrict__ acc) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= W * H) return;
+    const size_t npx = (size_t)W * H;
+    float A[T * T], bv[T], xv[T];
+    for (int e = 0; e < T * T; e++) A[e] = acc[(size_t)e * npx + p];
+    for (int ch = 0; ch < 3; ch++) {
+        for (int i = 0; i < T; i++) bv[i] = acc[(size_t)(T * T + ch * T + i) * npx + p];
+        cod_solve_dev<T>(A, bv, xv);
+        for (int i = 0; i < T; i++) acc[(size_t)(T * T + 3 * T + ch * T + i) * npx + p] = xv[i];
+    }
+}
+
+#define ROMIS_ROMIS_ACCUM(T, LDS, PROG, NAME)                                                                        \
+    extern "C" __global__ __launch_bounds__(256) void NAME(SceneDev s, uint32_t W, uint32_t H, FeaturesDev f, float ox,  \
+                                                          float oy, float oz, const float4* n_t, const float4* p_mat,  \
+                                                          const uint32_t* nbr, const float4* ra, const float4* rb,      \
+                                                          const float2* rdbg, float* acc) {                             \
+        romis_body<T, LDS, PROG>(s, W, H, f, mk(ox, oy, oz), n_t, p_mat, nbr, ra, rb, rdbg, acc);                       \
+    }
 #define ROMIS_ROMIS_KERNELS(T)                                                                                        \
-    extern "C" __global__ __launch_bounds__(256) void k_romis_accum_t##T(                                             \
-        SceneDev s, uint32_t W, uint32_t H, FeaturesDev f, float ox, float oy, float oz, const float4* n_t,             \
-        const float4* p_mat, const uint32_t* nbr, const float4* ra, const float4* rb, const float2* rdbg, uint32_t it, \
-        float* acc) {                                                                                                 \
-        romis_body<T, false>(s, W, H, f, mk(ox, oy, oz), n_t, p_mat, nbr, ra, rb, rdbg, it, acc);                     \
-    }                                                                                                                 \
-    extern "C" __global__ __launch_bounds__(256) void k_romis_accum_lds_t##T(                                         \
-        SceneDev s, uint32_t W, uint32_t H, FeaturesDev f, float ox, float oy, float oz, const float4* n_t,             \
-        const float4* p_mat, const uint32_t* nbr, const float4* ra, const float4* rb, const float2* rdbg, uint32_t it, \
-        float* acc) {                                                                                                 \
-        romis_body<T, true>(s, W, H, f, mk(ox, oy, oz), n_t, p_mat, nbr, ra, rb, rdbg, it, acc);                      \
+    ROMIS_ROMIS_ACCUM(T, false, false, k_romis_accum_t##T)                                                            \
+    ROMIS_ROMIS_ACCUM(T, true, false, k_romis_accum_lds_t##T)                                                         \
+    ROMIS_ROMIS_ACCUM(T, false, true, k_romis_accum_prog_t##T)                                                        \
+    ROMIS_ROMIS_ACCUM(T, true, true, k_romis_accum_prog_lds_t##T)                                                     \
+    extern "C" __global__ __launch_bounds__(256) void k_romis_alphas_t##T(uint32_t W, uint32_t H, float* acc) {         \
+        romis_alphas_body<T>(W, H, acc);                                                                              \
     }                                                                                                                 \
     extern "C" __global__ __launch_bounds__(256) void k_romis_solve_t##T(uint32_t W, uint32_t H, FeaturesDev f,         \
                                                                         const float* acc, float* rgb) {               \
@@ -1964,12 +1988,16 @@ hipError_t launch_debug_math(const float* x, const float* y, float* pw, float* e
 // ---- R-MIS / R-OMIS ---------------------------------------------------------------------------------------
 namespace {
 typedef void (*RomisAccumFn)(SceneDev, uint32_t, uint32_t, FeaturesDev, float, float, float, const float4*, const float4*,
-                             const uint32_t*, const float4*, const float4*, const float2*, uint32_t, float*);
+                             const uint32_t*, const float4*, const float4*, const float2*, float*);
+typedef void (*RomisAlphasFn)(uint32_t, uint32_t, float*);
 typedef void (*RomisSolveFn)(uint32_t, uint32_t, FeaturesDev, const float*, float*);
 typedef void (*DebugCodFn)(const float*, const float*, float*, uint32_t);
 #define ROMIS_T_TABLE(PFX) {PFX##1, PFX##2, PFX##3, PFX##4, PFX##5, PFX##6, PFX##7, PFX##8}
 const RomisAccumFn kRomisAccum[8] = ROMIS_T_TABLE(k_romis_accum_t);
 const RomisAccumFn kRomisAccumLds[8] = ROMIS_T_TABLE(k_romis_accum_lds_t);
+const RomisAccumFn kRomisAccumProg[8] = ROMIS_T_TABLE(k_romis_accum_prog_t);
+const RomisAccumFn kRomisAccumProgLds[8] = ROMIS_T_TABLE(k_romis_accum_prog_lds_t);
+const RomisAlphasFn kRomisAlphas[8] = ROMIS_T_TABLE(k_romis_alphas_t);
 const RomisSolveFn kRomisSolve[8] = ROMIS_T_TABLE(k_romis_solve_t);
 const DebugCodFn kDebugCod[8] = ROMIS_T_TABLE(k_debug_cod_t);
 inline dim3 px_grid(size_t npx) { return dim3((uint32_t)((npx + kBlock - 1) / kBlock)); }
@@ -1994,8 +2022,12 @@ hipError_t launch_mis_accumulate(const SceneDev& s, uint32_t W, uint32_t H, cons
     } else {
         const uint32_t T = f.K + 1u;
         if (T < 1u || T > 8u) return hipErrorInvalidValue;
-        ROMIS_LAUNCH(use_lds ? kRomisAccumLds[T - 1] : kRomisAccum[T - 1], grid, dim3(kBlock), use_lds ? lds : 0, stream, s,
-                     W, H, f, o[0], o[1], o[2], n_t, p_mat, nbr, ra, rb, rdbg, iteration, acc);
+        if (f.progressive && iteration >= 1u && iteration % f.prog_mod == 0u)   // alphas from the sums so far
+            ROMIS_LAUNCH(kRomisAlphas[T - 1], grid, dim3(kBlock), 0, stream, W, H, acc);
+        const RomisAccumFn k = f.progressive ? (use_lds ? kRomisAccumProgLds[T - 1] : kRomisAccumProg[T - 1])
+                                             : (use_lds ? kRomisAccumLds[T - 1] : kRomisAccum[T - 1]);
+        ROMIS_LAUNCH(k, grid, dim3(kBlock), use_lds ? lds : 0, stream, s, W, H, f, o[0], o[1], o[2], n_t, p_mat, nbr, ra,
+                     rb, rdbg, acc);
     }
     return hipGetLastError();
 }

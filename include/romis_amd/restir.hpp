@@ -122,12 +122,24 @@ inline std::shared_ptr<ReservoirGrid> renderReSTIR(Renderer& r, const std::share
     return std::make_shared<ReservoirGrid>(next);
 }
 
-// renderRayTraced (render.cpp:268-290): only the ReSTIR mode is accelerated here; R-MIS / R-OMIS throw.
+// renderRMIS / renderROMIS (render.cpp:64-265): maxIterationsMIS rounds of initial samples combined over each
+// pixel's neighbourhood into `screen` (features.ray_trace_mode selects the estimator).
+inline void renderMIS(Renderer& r, const Camera& camera, Screen& screen, const Features& features) {
+    check(restir_render(r.handle(), &camera, &features, uint32_t(screen.width), uint32_t(screen.height), nullptr, nullptr,
+                        nullptr, screen.rgb.data()),
+          "restir_render");
+}
+
+// renderRayTraced (render.cpp:268-290): the grid for temporal reuse in ReSTIR mode, nullptr (std::nullopt) for
+// R-MIS / R-OMIS.
 inline std::shared_ptr<ReservoirGrid> renderRayTraced(Renderer& r, const std::shared_ptr<ReservoirGrid>& prev,
                                                       const Camera& camera, Screen& screen, const Features& features) {
-    if (features.ray_trace_mode != RESTIR_MODE_RESTIR)
-        throw RestirError("Unsupported ray-tracing render mode requested from entry point");
-    return renderReSTIR(r, prev, camera, screen, features);
+    switch (features.ray_trace_mode) {
+        case RESTIR_MODE_RESTIR: return renderReSTIR(r, prev, camera, screen, features);
+        case RESTIR_MODE_RMIS:
+        case RESTIR_MODE_ROMIS: renderMIS(r, camera, screen, features); return nullptr;
+        default: throw RestirError("Unsupported ray-tracing render mode requested from entry point");
+    }
 }
 
 }  // namespace romis

@@ -62,3 +62,23 @@ def test_wrapper_frames_match_oracle(tmp_path, frames, N, passes, temporal):
     for fr in range(frames):
         want, prev, _ = pyoracle.render_frame(osc, cam, f, W, H, _abi.RESTIR_DEFAULT_SEED, fr, prev=prev)
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [_abi.MODE_RMIS, _abi.MODE_ROMIS])
+def test_wrapper_mis_matches_oracle(tmp_path, mode):
+    """renderRayTraced in R-MIS / R-OMIS mode through the C++ wrapper (render.cpp:268-290)."""
+    from oracle import pyoracle
+    W, H = 64, 40
+    name = "nightclub_128pt"
+    sc = scene.bench_scene(name)
+    cam = scene.camera_for(name, W, H)
+    write_scene(tmp_path / "s.bin", sc, cam)
+    out = tmp_path / "o.rgb"
+    subprocess.check_call([build_cpp(), str(tmp_path / "s.bin"), str(out), str(W), str(H), "1", "1", "0", "0",
+                           str(mode)], timeout=120)
+    got = np.fromfile(out, np.float32).reshape(H, W, 3)
+    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=0, temporal_reuse=0,
+                              ray_trace_mode=mode)
+    want = pyoracle.render_mis(pyoracle.OracleScene(sc), cam, f, W, H)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))

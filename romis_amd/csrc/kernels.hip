@@ -1030,7 +1030,11 @@ __device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& 
     // instead of 40 for the whole batch, which keeps the kernel at 91 VGPRs = 5 waves per SIMD)
     if (ok[0]) { na[0] = ld_at(ia, qo[0]); nb[0] = ld_at(ib, qo[0]); }
     // the pixel's own sample is consumed last; its target pdf does not depend on the stream
+#if defined(ROMIS_ABL_PDCUR)
+    const float pd_cur = ca.w;
+#else
     const float pd_cur = target_pdf(s, f, cur, xyz(ca), xyz(cb));
+#endif
     Comb1 cmb;
     cmb.pos = mk(0.0f, 0.0f, 0.0f); cmb.col = mk(0.0f, 0.0f, 0.0f);
     cmb.wsum = ROMIS_FLT_MIN; cmb.chosen = 0.0f; cmb.pd = 0.0f; cmb.macc = 0u; cmb.has_pd = false;
@@ -1614,17 +1618,53 @@ __device__ __forceinline__ float aucw_reciprocal(const SceneDev& s, const Featur
     return 1.0f / arbitraryWeight;
 }
 
-// One R-OMIS iteration (render.cpp:139-231): technique matrix A and contribution vectors b held in registers for
-// the pixel (T = k + 1 techniques, a compile-time constant; every index static, so nothing spills to scratch), plus
-// the progressive estimator's colour (PROG).  The progressive alphas are solved beforehand by k_romis_alphas and only
-// read here.
-template <int T, bool LDS_BVH, bool PROG>
-__device__ __forceinline__ void romis_body(const SceneDev& s, uint32_t W, uint32_t H, const FeaturesDev& f, v3 origin,
-                                           const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
-                                           const uint32_t* __restrict__ nbr, const float4* __restrict__ ra,
-                                           const float4* __restrict__ rb, const float2* __restrict__ rdbg,
-                                           float* __restrict__ acc) {
+// One R-OMIS iteration (render.cpp:139-231), split in two launches per chunk of the pixel's T x N samples (the
+// one-lane-per-pixel form held A, b and every sample's per-distribution state at once: 251-260 VGPRs = 1-2 waves per
+// SIMD, its loads a dependent chain per distribution; 24-44 % VALU busy):
+//  - k_romis_samples_t{T}: one lane per (sample, pixel), wave = 64 pixels of one sample slot: the sample's column
+//    vector over the T distributions (arbitraryUnbiasedContributionWeightReciprocal at each distribution pixel) and
+//    its visibility-tested shaded colour -> smp rows [sample][T + 3][pixels];
+//  - k_romis_accum_t{T}[_prog]: one lane per pixel: the progressive colour, scale factor, technique matrix and
+//    contribution vector updates of those samples, in the reference's order, reading them back from smp.
+// Every value is computed by the same operations as in one pass, so the split is bit-exact.
+template <int T, bool LDS_BVH>
+__device__ __forceinline__ void romis_samples_body(const SceneDev& s, uint32_t W, uint32_t H, const FeaturesDev& f,
+                                                   v3 origin, const float4* __restrict__ n_t,
+                                                   const float4* __restrict__ p_mat, const uint32_t* __restrict__ nbr,
+                                                   const float4* __restrict__ ra, const float4* __restrict__ rb,
+                                                   const float2* __restrict__ rdbg, uint32_t s0, uint32_t ns,
+                                                   float* __restrict__ smp) {
     const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
+    const uint32_t npx = W * H;   // launcher: ns * npx < 2^31
+    const uint32_t N = f.N;
+    const uint32_t items = ns * npx;
+    for (uint32_t it = blockIdx.x * blockDim.x + threadIdx.x; it < items; it += gridDim.x * blockDim.x) {
+        const uint32_t sl = it / npx, p = it - sl * npx;
+        const uint32_t sg = s0 + sl, pi = sg / N, si = sg - pi * N;
+        const uint32_t q = nbr[(size_t)(1u + pi) * npx + p];
+        const float4 a = ra[(size_t)si * npx + q], b4 = rb[(size_t)si * npx + q];
+        const v3 pos = xyz(a), col = xyz(b4);
+        float* out = smp + (size_t)sl * (T + 3) * npx + p;
+        // the T target-pdf evaluations as one rolled loop (one inlined copy of target_pdf)
+#pragma unroll 1
+        for (int d = 0; d < T; d++) {
+            const uint32_t qq = nbr[(size_t)(1 + d) * npx + p];
+            const float4 db = rb[(size_t)si * npx + qq];
+            const float2 dd = rdbg[(size_t)si * npx + qq];
+            out[(size_t)d * npx] = aucw_reciprocal(s, f, make_px(s, n_t[qq], p_mat[qq], origin),
+                                                   (float)__float_as_uint(db.w), dd.x, dd.y, pos, col);
+        }
+        const Px cur = make_px(s, n_t[p], p_mat[p], origin);
+        const v3 sc = visible(bvh, cur.P, pos) ? shade(s, f, cur, pos, col) : mk(0.0f, 0.0f, 0.0f);
+        out[(size_t)T * npx] = sc.x;
+        out[(size_t)(T + 1) * npx] = sc.y;
+        out[(size_t)(T + 2) * npx] = sc.z;
+    }
+}
+
+template <int T, bool PROG>
+__device__ __forceinline__ void romis_accum_body(uint32_t W, uint32_t H, const FeaturesDev& f, uint32_t s0, uint32_t ns,
+                                                 const float* __restrict__ smp, float* __restrict__ acc) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= W * H) return;
     const size_t npx = (size_t)W * H;
@@ -1635,7 +1675,6 @@ __device__ __forceinline__ void romis_body(const SceneDev& s, uint32_t W, uint32
     float* Bv = acc + (size_t)T * T * npx;
     const float* Al = Bv + (size_t)3 * T * npx;
     float* Col = Bv + (size_t)6 * T * npx;
-    const Px cur = make_px(s, n_t[p], p_mat[p], origin);
     float A[T * T], bb[3][T], al[3][T];
 #pragma unroll
     for (int e = 0; e < T * T; e++) A[e] = Am[(size_t)e * npx + p];
@@ -1648,56 +1687,43 @@ __device__ __forceinline__ void romis_body(const SceneDev& s, uint32_t W, uint32
         }
     v3 fc = mk(0.0f, 0.0f, 0.0f);
     if (PROG) fc = mk(Col[p], Col[npx + p], Col[2 * npx + p]);
-    for (int pi = 0; pi < T; pi++) {
-        if (PROG)
+    for (uint32_t sl = 0; sl < ns; sl++) {
+        const uint32_t sg = s0 + sl, pi = sg / N, si = sg - pi * N;
+        if (PROG && si == 0u)   // the start of neighbourhood entry pi (render.cpp:156-160)
             fc = vadd(fc, mk(Al[(size_t)pi * npx + p], Al[(size_t)(T + pi) * npx + p], Al[(size_t)(2 * T + pi) * npx + p]));
-        const uint32_t q = nbr[(size_t)(1 + pi) * npx + p];
-        for (uint32_t si = 0; si < N; si++) {
-            const float4 a = ra[(size_t)si * npx + q], b4 = rb[(size_t)si * npx + q];
-            const v3 pos = xyz(a), col = xyz(b4);
-            // the T target-pdf evaluations run as one rolled loop (one inlined copy: 4x fewer VGPRs than unrolled);
-            // each result lands in its static register slot by selects
-            float v[T];
-#pragma unroll 1
+        const float* in = smp + (size_t)sl * (T + 3) * npx + p;
+        float v[T];
+#pragma unroll
+        for (int d = 0; d < T; d++) v[d] = in[(size_t)d * npx];
+        const v3 sc = mk(in[(size_t)T * npx], in[(size_t)(T + 1) * npx], in[(size_t)(T + 2) * npx]);
+        if (PROG) {
+            v3 sa = mk(0.0f, 0.0f, 0.0f);
+            float sf = ROMIS_FLT_MIN;
+#pragma unroll
             for (int d = 0; d < T; d++) {
-                const uint32_t qq = nbr[(size_t)(1 + d) * npx + p];
-                const float4 db = rb[(size_t)si * npx + qq];
-                const float2 dd = rdbg[(size_t)si * npx + qq];
-                const float val = aucw_reciprocal(s, f, make_px(s, n_t[qq], p_mat[qq], origin), (float)__float_as_uint(db.w),
-                                                  dd.x, dd.y, pos, col);
-#pragma unroll
-                for (int e = 0; e < T; e++) v[e] = e == d ? val : v[e];
+                sa = vadd(sa, vscale(mk(al[0][d], al[1][d], al[2][d]), v[d]));
+                sf += (float)fractionOfTotalSamples * v[d];
             }
-            const v3 sc = visible(bvh, cur.P, pos) ? shade(s, f, cur, pos, col) : mk(0.0f, 0.0f, 0.0f);
-            if (PROG) {
-                v3 sa = mk(0.0f, 0.0f, 0.0f);
-                float sf = ROMIS_FLT_MIN;
+            const v3 term = vsub(mk(sc.x / sf, sc.y / sf, sc.z / sf), mk(sa.x / sf, sa.y / sf, sa.z / sf));
+            const float inv = 1.0f / (float)totalSamples;
+            fc = vadd(fc, mk(inv * term.x, inv * term.y, inv * term.z));
+        }
+        float scaleFactor = ROMIS_FLT_MIN;
 #pragma unroll
-                for (int d = 0; d < T; d++) {
-                    sa = vadd(sa, vscale(mk(al[0][d], al[1][d], al[2][d]), v[d]));
-                    sf += (float)fractionOfTotalSamples * v[d];
-                }
-                const v3 term = vsub(mk(sc.x / sf, sc.y / sf, sc.z / sf), mk(sa.x / sf, sa.y / sf, sa.z / sf));
-                const float inv = 1.0f / (float)totalSamples;
-                fc = vadd(fc, mk(inv * term.x, inv * term.y, inv * term.z));
-            }
-            float scaleFactor = ROMIS_FLT_MIN;
+        for (int d = 0; d < T; d++) scaleFactor += (float)N * v[d];
+        scaleFactor = 1.0f / scaleFactor;
 #pragma unroll
-            for (int d = 0; d < T; d++) scaleFactor += (float)N * v[d];
-            scaleFactor = 1.0f / scaleFactor;
+        for (int d = 0; d < T; d++) v[d] *= scaleFactor;
 #pragma unroll
-            for (int d = 0; d < T; d++) v[d] *= scaleFactor;
+        for (int j = 0; j < T; j++)
 #pragma unroll
-            for (int j = 0; j < T; j++)
+            for (int i = 0; i < T; i++) A[i + j * T] += v[i] * v[j];
 #pragma unroll
-                for (int i = 0; i < T; i++) A[i + j * T] += v[i] * v[j];
-#pragma unroll
-            for (int row = 0; row < T; row++) {
-                const float scaleColVecConst = scaleFactor * v[row];
-                bb[0][row] += sc.x * scaleColVecConst;
-                bb[1][row] += sc.y * scaleColVecConst;
-                bb[2][row] += sc.z * scaleColVecConst;
-            }
+        for (int row = 0; row < T; row++) {
+            const float scaleColVecConst = scaleFactor * v[row];
+            bb[0][row] += sc.x * scaleColVecConst;
+            bb[1][row] += sc.y * scaleColVecConst;
+            bb[2][row] += sc.z * scaleColVecConst;
         }
     }
 #pragma unroll
@@ -1725,18 +1751,23 @@ __device__ __forceinline__ void romis_alphas_body(uint32_t W, uint32_t H, float*
     }
 }
 
-#define ROMIS_ROMIS_ACCUM(T, LDS, PROG, NAME)                                                                        \
+#define ROMIS_ROMIS_SAMPLES(T, LDS, NAME)                                                                           \
     extern "C" __global__ __launch_bounds__(256) void NAME(SceneDev s, uint32_t W, uint32_t H, FeaturesDev f, float ox,  \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,  \
                                                           const uint32_t* nbr, const float4* ra, const float4* rb,      \
-                                                          const float2* rdbg, float* acc) {                             \
-        romis_body<T, LDS, PROG>(s, W, H, f, mk(ox, oy, oz), n_t, p_mat, nbr, ra, rb, rdbg, acc);                       \
+                                                          const float2* rdbg, uint32_t s0, uint32_t ns, float* smp) {   \
+        romis_samples_body<T, LDS>(s, W, H, f, mk(ox, oy, oz), n_t, p_mat, nbr, ra, rb, rdbg, s0, ns, smp);             \
+    }
+#define ROMIS_ROMIS_ACCUM(T, PROG, NAME)                                                                             \
+    extern "C" __global__ __launch_bounds__(256) void NAME(uint32_t W, uint32_t H, FeaturesDev f, uint32_t s0,           \
+                                                          uint32_t ns, const float* smp, float* acc) {                 \
+        romis_accum_body<T, PROG>(W, H, f, s0, ns, smp, acc);                                                          \
     }
 #define ROMIS_ROMIS_KERNELS(T)                                                                                        \
-    ROMIS_ROMIS_ACCUM(T, false, false, k_romis_accum_t##T)                                                            \
-    ROMIS_ROMIS_ACCUM(T, true, false, k_romis_accum_lds_t##T)                                                         \
-    ROMIS_ROMIS_ACCUM(T, false, true, k_romis_accum_prog_t##T)                                                        \
-    ROMIS_ROMIS_ACCUM(T, true, true, k_romis_accum_prog_lds_t##T)                                                     \
+    ROMIS_ROMIS_SAMPLES(T, false, k_romis_samples_t##T)                                                               \
+    ROMIS_ROMIS_SAMPLES(T, true, k_romis_samples_lds_t##T)                                                            \
+    ROMIS_ROMIS_ACCUM(T, false, k_romis_accum_t##T)                                                                   \
+    ROMIS_ROMIS_ACCUM(T, true, k_romis_accum_prog_t##T)                                                               \
     extern "C" __global__ __launch_bounds__(256) void k_romis_alphas_t##T(uint32_t W, uint32_t H, float* acc) {         \
         romis_alphas_body<T>(W, H, acc);                                                                              \
     }                                                                                                                 \
@@ -1833,7 +1864,9 @@ bool launch_events_used() { return g_launched; }
 
 #define ROMIS_LAUNCH(kernel, grid, block, lds, stream, ...)                                                    \
     do {                                                                                                      \
-        hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, g_ev_start, g_ev_stop, 0, __VA_ARGS__);      \
+        /* a multi-launch stage: start event on its first kernel, stop event after its last */              \
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, g_launched ? nullptr : g_ev_start, g_ev_stop, 0, \
+                              __VA_ARGS__);                                                                   \
         g_launched = true;                                                                                    \
     } while (0)
 
@@ -1987,16 +2020,17 @@ hipError_t launch_debug_math(const float* x, const float* y, float* pw, float* e
 
 // ---- R-MIS / R-OMIS ---------------------------------------------------------------------------------------
 namespace {
-typedef void (*RomisAccumFn)(SceneDev, uint32_t, uint32_t, FeaturesDev, float, float, float, const float4*, const float4*,
-                             const uint32_t*, const float4*, const float4*, const float2*, float*);
+typedef void (*RomisSamplesFn)(SceneDev, uint32_t, uint32_t, FeaturesDev, float, float, float, const float4*, const float4*,
+                               const uint32_t*, const float4*, const float4*, const float2*, uint32_t, uint32_t, float*);
+typedef void (*RomisAccumFn)(uint32_t, uint32_t, FeaturesDev, uint32_t, uint32_t, const float*, float*);
 typedef void (*RomisAlphasFn)(uint32_t, uint32_t, float*);
 typedef void (*RomisSolveFn)(uint32_t, uint32_t, FeaturesDev, const float*, float*);
 typedef void (*DebugCodFn)(const float*, const float*, float*, uint32_t);
 #define ROMIS_T_TABLE(PFX) {PFX##1, PFX##2, PFX##3, PFX##4, PFX##5, PFX##6, PFX##7, PFX##8}
+const RomisSamplesFn kRomisSamples[8] = ROMIS_T_TABLE(k_romis_samples_t);
+const RomisSamplesFn kRomisSamplesLds[8] = ROMIS_T_TABLE(k_romis_samples_lds_t);
 const RomisAccumFn kRomisAccum[8] = ROMIS_T_TABLE(k_romis_accum_t);
-const RomisAccumFn kRomisAccumLds[8] = ROMIS_T_TABLE(k_romis_accum_lds_t);
 const RomisAccumFn kRomisAccumProg[8] = ROMIS_T_TABLE(k_romis_accum_prog_t);
-const RomisAccumFn kRomisAccumProgLds[8] = ROMIS_T_TABLE(k_romis_accum_prog_lds_t);
 const RomisAlphasFn kRomisAlphas[8] = ROMIS_T_TABLE(k_romis_alphas_t);
 const RomisSolveFn kRomisSolve[8] = ROMIS_T_TABLE(k_romis_solve_t);
 const DebugCodFn kDebugCod[8] = ROMIS_T_TABLE(k_debug_cod_t);
@@ -2011,8 +2045,8 @@ hipError_t launch_mis_neighbours(const SceneDev& s, uint32_t W, uint32_t H, cons
 
 hipError_t launch_mis_accumulate(const SceneDev& s, uint32_t W, uint32_t H, const FeaturesDev& f, const float* o,
                                  const float4* n_t, const float4* p_mat, const uint32_t* nbr, const float4* ra,
-                                 const float4* rb, const float2* rdbg, uint32_t iteration, float* acc, const Tuning& tu,
-                                 hipStream_t stream) {
+                                 const float4* rb, const float2* rdbg, uint32_t iteration, float* acc, float* smp,
+                                 uint32_t smp_samples, const Tuning& tu, hipStream_t stream) {
     const size_t lds = bvh_lds_bytes(s);
     const bool use_lds = tu.final_lds && lds <= kLdsBudget;   // shadow rays: the BVH staged like k_final's
     const dim3 grid = px_grid((size_t)W * H);
@@ -2024,10 +2058,18 @@ hipError_t launch_mis_accumulate(const SceneDev& s, uint32_t W, uint32_t H, cons
         if (T < 1u || T > 8u) return hipErrorInvalidValue;
         if (f.progressive && iteration >= 1u && iteration % f.prog_mod == 0u)   // alphas from the sums so far
             ROMIS_LAUNCH(kRomisAlphas[T - 1], grid, dim3(kBlock), 0, stream, W, H, acc);
-        const RomisAccumFn k = f.progressive ? (use_lds ? kRomisAccumProgLds[T - 1] : kRomisAccumProg[T - 1])
-                                             : (use_lds ? kRomisAccumLds[T - 1] : kRomisAccum[T - 1]);
-        ROMIS_LAUNCH(k, grid, dim3(kBlock), use_lds ? lds : 0, stream, s, W, H, f, o[0], o[1], o[2], n_t, p_mat, nbr, ra,
-                     rb, rdbg, acc);
+        // the T x N samples in chunks of smp_samples (the scratch rows ensure_mis sized), in the reference's order
+        const RomisSamplesFn ks = use_lds ? kRomisSamplesLds[T - 1] : kRomisSamples[T - 1];
+        const RomisAccumFn ka = f.progressive ? kRomisAccumProg[T - 1] : kRomisAccum[T - 1];
+        const uint32_t npx = W * H, S = T * f.N;
+        if (smp_samples == 0u || (uint64_t)smp_samples * npx >= (1ull << 31)) return hipErrorInvalidValue;
+        for (uint32_t s0 = 0; s0 < S; s0 += smp_samples) {
+            const uint32_t ns = std::min(smp_samples, S - s0);
+            const uint32_t blocks = std::min<uint32_t>((ns * npx + kBlock - 1u) / kBlock, 8192u);
+            ROMIS_LAUNCH(ks, dim3(blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, W, H, f, o[0], o[1], o[2], n_t,
+                         p_mat, nbr, ra, rb, rdbg, s0, ns, smp);
+            ROMIS_LAUNCH(ka, grid, dim3(kBlock), 0, stream, W, H, f, s0, ns, smp, acc);
+        }
     }
     return hipGetLastError();
 }

@@ -140,8 +140,8 @@ struct restir_ctx {
     bool stage_ok = false;
 
     // R-MIS / R-OMIS: neighbourhoods [1 + cap][pixels] and accumulators [rows][pixels] (RESTIR_BUF_MIS_*)
-    DevBuf mis_nbr, mis_acc;
-    uint32_t mis_cap = 0, mis_rows = 0;
+    DevBuf mis_nbr, mis_acc, mis_smp;
+    uint32_t mis_cap = 0, mis_rows = 0, mis_smp_samples = 0;
 
     // timing
     bool timing = false;
@@ -371,6 +371,7 @@ uint32_t mis_acc_rows(const restir_features* f) {
     const uint32_t T = f->num_neighbours_to_sample + 1u;
     return f->ray_trace_mode == RESTIR_MODE_ROMIS ? T * T + 6u * T + 3u : 3u;
 }
+constexpr uint64_t kMisSampleBudget = 4ull << 30;   // bytes of R-OMIS per-sample scratch
 restir_status ensure_mis(restir_ctx* c, const restir_features* f, uint32_t W, uint32_t H) {
     if (f->ray_trace_mode == RESTIR_MODE_RESTIR) return fail(RESTIR_ERR_INVALID, "the MIS stages need rayTraceMode RMIS or ROMIS");
     const size_t npx = (size_t)W * H;
@@ -378,6 +379,18 @@ restir_status ensure_mis(restir_ctx* c, const restir_features* f, uint32_t W, ui
     c->mis_rows = mis_acc_rows(f);
     ST_TRY(c->mis_nbr.ensure((size_t)(1u + c->mis_cap) * npx * 4));
     ST_TRY(c->mis_acc.ensure((size_t)c->mis_rows * npx * 4));
+    c->mis_smp_samples = 0;
+    if (f->ray_trace_mode == RESTIR_MODE_ROMIS) {
+        // R-OMIS per-sample scratch (k_romis_samples -> k_romis_accum): T + 3 rows per sample, as many of the T x N
+        // samples as fit kMisSampleBudget (or the mis.chunk knob) and keep one launch's items below 2^31
+        const uint64_t T = f->num_neighbours_to_sample + 1ull, S = T * f->num_samples_in_reservoir;
+        const uint64_t per = (T + 3ull) * npx * 4ull;
+        uint64_t n = std::max<uint64_t>(1, std::min<uint64_t>(S, kMisSampleBudget / per));
+        if (c->tuning.mis_chunk) n = std::min<uint64_t>(n, c->tuning.mis_chunk);
+        n = std::min<uint64_t>(n, std::max<uint64_t>(1, ((1ull << 31) - 1ull) / std::max<uint64_t>(npx, 1)));
+        c->mis_smp_samples = (uint32_t)n;
+        ST_TRY(c->mis_smp.ensure((size_t)(n * per)));
+    }
     return RESTIR_OK;
 }
 // renderROMIS reads neighborhood[0..k] (render.cpp:155-181): every pixel's window must hold k candidates
@@ -750,7 +763,8 @@ static restir_status render_mis(restir_ctx* c, const restir_camera* cam, const r
                                           c->queue, c->stream));
         TIMED(c, RESTIR_K_MIS, launch_mis_accumulate(s, W, H, f, camd.origin, nt, pm, c->mis_nbr.as<uint32_t>(),
                                                      c->ra[0].as<float4>(), c->rb[0].as<float4>(), c->dbg[0].as<float2>(), it,
-                                                     c->mis_acc.as<float>(), c->tuning, c->stream));
+                                                     c->mis_acc.as<float>(), c->mis_smp.as<float>(), c->mis_smp_samples,
+                                                     c->tuning, c->stream));
     }
     TIMED(c, RESTIR_K_MIS, launch_mis_finish(W, H, f, c->mis_acc.as<float>(), c->rgb.as<float>(), c->stream));
     if (out_rgb) {
@@ -1098,8 +1112,8 @@ restir_status restir_stage_mis_accumulate(restir_ctx* c, const restir_camera* ca
     if (iteration == 0) HIP_TRY(hipMemsetAsync(c->mis_acc.p, 0, (size_t)c->mis_rows * c->vw * c->vh * 4, c->stream));
     TIMED(c, RESTIR_K_MIS, launch_mis_accumulate(c->sdev, c->vw, c->vh, d, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                                                  c->mis_nbr.as<uint32_t>(), c->ra[cur].as<float4>(), c->rb[cur].as<float4>(),
-                                                 c->dbg[cur].as<float2>(), iteration, c->mis_acc.as<float>(), c->tuning,
-                                                 c->stream));
+                                                 c->dbg[cur].as<float2>(), iteration, c->mis_acc.as<float>(),
+                                                 c->mis_smp.as<float>(), c->mis_smp_samples, c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
@@ -1380,6 +1394,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "ris.queue")) t.ris_queue = v;
     else if (!std::strcmp(key, "bvh.max_leaf")) t.bvh_max_leaf = v;
     else if (!std::strcmp(key, "final.sort")) t.final_sort = v;
+    else if (!std::strcmp(key, "mis.chunk")) t.mis_chunk = v;   // applies from the next ensure_mis
     else if (!std::strcmp(key, "layout.records")) t.records = v;   // frame-path buffer layout   // applies from the next restir_set_scene
     else if (!std::strcmp(key, "final.blocks")) t.final_blocks = v;
     else if (!std::strcmp(key, "final.lds")) t.final_lds = v;

@@ -78,6 +78,7 @@ struct Tuning {
     uint32_t final_lds = 1;
     uint32_t final_2d = 1;
     uint32_t final_sort = 0;       // N = 1: bin each tile's shadow rays by target before tracing
+    uint32_t mis_chunk = 0;        // R-OMIS samples per k_romis_samples / k_romis_accum pair; 0 = the scratch budget
 };
 
 // Dynamic tile queue for persistent grids: a never-reset ticket counter; a launch hands out tickets

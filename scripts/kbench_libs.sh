@@ -16,5 +16,5 @@ python3 - "$REPO/gpurun_out/$TAG" <<'PY'
 import json, glob, os, sys
 for f in sorted(glob.glob(os.path.join(sys.argv[1], "*.json"))):
     d = json.load(open(f))
-    print(os.path.basename(f)[:-5].ljust(12), "  ".join(f"{k}:{v.get('spatial')}/{v.get('ris')}" for k, v in d.items()))
+    print(os.path.basename(f)[:-5].ljust(12), "  ".join(f"{k}:{v.get('spatial')}/{v.get('primary_ris')}/{v.get('final')}" for k, v in d.items()))
 PY

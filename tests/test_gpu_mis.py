@@ -122,6 +122,31 @@ def test_mis_accumulate_and_finish_bit_exact(gpu, oracle, case):
     bits_equal(gpu.download(_abi.BUF_RGB), oracle.mis_finish(f, W, H, acc), f"{case}: screen")
 
 
+@pytest.mark.parametrize("case,chunk", [("romis_direct", 5), ("romis_progressive", 5), ("romis_progressive", 1)])
+def test_romis_sample_chunks_bit_exact(gpu, oracle, case, chunk):
+    """k_romis_samples / k_romis_accum over chunks of the T x N samples (mis.chunk; chunk boundaries inside a
+    neighbourhood entry) give the accumulators of the one-chunk launch and of the oracle."""
+    f = _abi.default_features(**MIS_CASES[case])
+    f.max_iterations_mis = 2
+    osc, cam, n_t, p_mat, origin = setup(gpu, oracle, "nightclub_128pt", f)
+    nbr = oracle.neighbours(osc, f, key(oracle, 4, 0), key(oracle, 4, 1), W, H, n_t, p_mat)
+    gpu.set_tuning("mis.chunk", chunk)
+    try:
+        gpu.mis_buffers(f, nbr=nbr)
+        acc = np.zeros((oracle.mis_acc_rows(f), W * H), np.float32)
+        for it in range(f.max_iterations_mis):
+            a, b, d = oracle.ris(osc, f, key(oracle, _abi.RESTIR_STAGE_RIS, it), origin, W, H, n_t, p_mat)
+            gpu.upload(_abi.BUF_RES_A, a)
+            gpu.upload(_abi.BUF_RES_B, b)
+            gpu.upload(_abi.BUF_RES_DBG, d)
+            gpu.stage_mis_accumulate(cam, f, it)
+            oracle.romis_accumulate(osc, f, origin, W, H, n_t, p_mat, nbr, a, b, d, it, acc)
+            _, got = gpu.mis_buffers(f)
+            bits_equal(got, acc, f"{case} chunk {chunk}: accumulators after iteration {it}")
+    finally:
+        gpu.set_tuning("mis.chunk", 0)
+
+
 @pytest.mark.parametrize("name,case", [("nightclub_128pt", "rmis_equal"), ("nightclub_128pt", "romis_direct"),
                                        ("cornell_parallelogram", "rmis_balance"),
                                        ("cornell_parallelogram", "romis_progressive"),

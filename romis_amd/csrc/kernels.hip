@@ -1347,6 +1347,30 @@ __device__ uint32_t mis_emit_class(const SceneDev& s, const FeaturesDev& f, cons
     return n;
 }
 
+// The same walk over the count pass's similarity bits (window member m = bit m, LDS word m / 32 of the lane, stride
+// 256): windows of up to kMisMaskBits members skip re-evaluating areSimilar in the emit passes.
+constexpr uint32_t kMisMaskWords = 14, kMisMaskBits = 32u * kMisMaskWords;   // 448 >= (2 * 10 + 1)^2 - 1
+__device__ uint32_t mis_emit_class_mask(const uint32_t* __restrict__ mask, uint32_t W, MisWin w, uint32_t p, int cls,
+                                        uint64_t len, uint64_t want, bool take_all, uint32_t ps,
+                                        uint32_t* __restrict__ nbr, size_t npx, uint32_t n) {
+    uint64_t needed = take_all ? len : (want < len ? want : len);
+    uint64_t i = 0;
+    uint32_t m = 0;
+    for (int ny = w.y0; ny <= w.y1 && needed; ny++) {
+        for (int nx = w.x0; nx <= w.x1 && needed; nx++) {
+            const uint32_t q = (uint32_t)ny * W + (uint32_t)nx;
+            if (q == p) continue;
+            const int sim = (int)((mask[(m >> 5) * 256u] >> (m & 31u)) & 1u);
+            m++;
+            if (sim != cls) continue;
+            const bool keep = take_all || (uint64_t)uniform_index(draw(ps, (uint32_t)i), (uint32_t)(len - i)) < needed;
+            if (keep) { nbr[(size_t)(1u + n) * npx + p] = q; n++; needed--; }
+            i++;
+        }
+    }
+    return n;
+}
+
 // generateResampleIndicesGrid (neighbour_selection.cpp:107-122): nbr[0][p] = neighbourhood size, nbr[1 + i][p] = its
 // i-th pixel (the pixel itself first).  indicesRandom (:24-43) / indicesSimilarity (:45-105) with the reference's
 // size arithmetic (Dissimilar: `k - similar.size()` as size_t; EqualSimilarDissimilar in uint32_t).
@@ -1355,6 +1379,7 @@ extern "C" __global__ __launch_bounds__(256) void k_mis_neighbours(SceneDev s, u
                                                                   const float4* __restrict__ n_t,
                                                                   const float4* __restrict__ p_mat,
                                                                   uint32_t* __restrict__ nbr) {
+    __shared__ uint32_t s_mask[kMisMaskWords * 256u];
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= W * H) return;
     const size_t npx = (size_t)W * H;
@@ -1374,33 +1399,48 @@ extern "C" __global__ __launch_bounds__(256) void k_mis_neighbours(SceneDev s, u
     } else {
         const float4 cn = n_t[p];
         const uint32_t cg = geom_id_of(s, p_mat[p]);
+        uint32_t* mask = s_mask + threadIdx.x;
+        const bool use_mask = (uint32_t)((w.x1 - w.x0 + 1) * (w.y1 - w.y0 + 1)) - 1u <= kMisMaskBits;
         uint64_t S = 0, D = 0;
+        uint32_t m = 0, word = 0;
         for (int ny = w.y0; ny <= w.y1; ny++)
             for (int nx = w.x0; nx <= w.x1; nx++) {
                 const uint32_t q = (uint32_t)ny * W + (uint32_t)nx;
                 if (q == p) continue;
-                if (are_similar(s, f, cn, cg, n_t[q], p_mat[q])) S++; else D++;
+                const bool sim = are_similar(s, f, cn, cg, n_t[q], p_mat[q]);
+                if (sim) S++; else D++;
+                if (use_mask) {
+                    word |= (uint32_t)sim << (m & 31u);
+                    if ((m & 31u) == 31u) { mask[(m >> 5) * 256u] = word; word = 0; }
+                }
+                m++;
             }
+        if (use_mask && (m & 31u)) mask[(m >> 5) * 256u] = word;
+        // emit one class: from the stored bits, or by re-evaluating areSimilar for windows past kMisMaskBits
+        auto emit = [&](int cls, uint64_t len, uint64_t want, bool take_all, uint32_t ps, uint32_t n0) {
+            return use_mask ? mis_emit_class_mask(mask, W, w, p, cls, len, want, take_all, ps, nbr, npx, n0)
+                            : mis_emit_class(s, f, n_t, p_mat, W, w, p, cn, cg, cls, len, want, take_all, ps, nbr, npx, n0);
+        };
         if (f.strategy == RESTIR_NEIGHBOURS_SIMILAR) {
             if (S < k) {
-                n = mis_emit_class(s, f, n_t, p_mat, W, w, p, cn, cg, 1, S, 0, true, ps_s, nbr, npx, n);
-                n = mis_emit_class(s, f, n_t, p_mat, W, w, p, cn, cg, 0, D, (uint64_t)k - S, false, ps_d, nbr, npx, n);
+                n = emit(1, S, 0, true, ps_s, n);
+                n = emit(0, D, (uint64_t)k - S, false, ps_d, n);
             } else {
-                n = mis_emit_class(s, f, n_t, p_mat, W, w, p, cn, cg, 1, S, k, false, ps_s, nbr, npx, n);
+                n = emit(1, S, k, false, ps_s, n);
             }
         } else if (f.strategy == RESTIR_NEIGHBOURS_DISSIMILAR) {
             if (D < k) {
-                n = mis_emit_class(s, f, n_t, p_mat, W, w, p, cn, cg, 0, D, 0, true, ps_d, nbr, npx, n);
-                n = mis_emit_class(s, f, n_t, p_mat, W, w, p, cn, cg, 1, S, (uint64_t)k - S, false, ps_s, nbr, npx, n);
+                n = emit(0, D, 0, true, ps_d, n);
+                n = emit(1, S, (uint64_t)k - S, false, ps_s, n);
             } else {
-                n = mis_emit_class(s, f, n_t, p_mat, W, w, p, cn, cg, 0, D, k, false, ps_d, nbr, npx, n);
+                n = emit(0, D, k, false, ps_d, n);
             }
         } else {   // EqualSimilarDissimilar (uint32_t arithmetic as written, neighbour_selection.cpp:87-95)
             uint32_t sS = min((k / 2u) + 1u, (uint32_t)S);
             const uint32_t desired = k - sS;
             if ((uint64_t)desired > D) sS = (uint32_t)((uint64_t)sS + ((uint64_t)k - D - sS));
-            n = mis_emit_class(s, f, n_t, p_mat, W, w, p, cn, cg, 1, S, sS, false, ps_s, nbr, npx, n);
-            n = mis_emit_class(s, f, n_t, p_mat, W, w, p, cn, cg, 0, D, (uint32_t)(k - sS), false, ps_d, nbr, npx, n);
+            n = emit(1, S, sS, false, ps_s, n);
+            n = emit(0, D, (uint32_t)(k - sS), false, ps_d, n);
         }
     }
     nbr[p] = n;

@@ -21,16 +21,6 @@ struct v3 { float x, y, z; };
 // (v_sqrt_f32, then pick s-1ulp / s / s+1ulp by the sign of the fma residuals) without its denormal rescaling
 // and +-0 / inf fix-ups, which are identities for q in [2^-96, FLT_MAX].
 __device__ __forceinline__ bool sqrt_fast_ok(float q) { return q >= 0x1p-96f && q <= 3.402823466e+38F; }
-#if defined(ROMIS_SQRT_PK)
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float sqrt_rn_core(float q) {
-    const float s = __builtin_amdgcn_sqrtf(q);
-    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
-    const f32x2 r = __builtin_elementwise_fma((f32x2){-sm, -sp}, (f32x2){s, s}, (f32x2){q, q});
-    float o = (r.x <= 0.0f) ? sm : s;
-    return (r.y > 0.0f) ? sp : o;
-}
-#else
 __device__ __forceinline__ float sqrt_rn_core(float q) {
     const float s = __builtin_amdgcn_sqrtf(q);
     const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
@@ -38,7 +28,6 @@ __device__ __forceinline__ float sqrt_rn_core(float q) {
     float r = (rm <= 0.0f) ? sm : s;
     return (rp > 0.0f) ? sp : r;
 }
-#endif
 // reciprocal: v_rcp_f32 (< 1 ulp) + one Newton step with exact fma residual (Markstein); the exhaustive check
 // pins it to 1.0f / b for every |b| in [2^-125, 2^125].
 __device__ __forceinline__ bool rcp_fast_ok(float b) { const float a = fabsf(b); return a >= 0x1p-125f && a <= 0x1p125f; }

@@ -21,6 +21,7 @@ VARIANTS = {
     "light0": ["ROMIS_ABL_LIGHT0"],           # every candidate reads light 0 (no LDS bank conflicts)
     "spatial_self": ["ROMIS_ABL_SPATIAL_SELF"],  # spatial neighbours = the pixel itself (no gathers)
     "spatial_copy": ["ROMIS_ABL_SPATIAL_COPY"],  # spatial = copy own reservoir (memory floor)
+    "pdcur": ["ROMIS_ABL_PDCUR"],             # k_spatial1: the pixel's own target pdf not evaluated (W stand-in)
 }
 
 

@@ -49,6 +49,8 @@ def lib() -> C.CDLL:
             "or_tonemap": (None, [FP, C.c_float, C.c_float, FP]),
             "or_powf": (C.c_float, [C.c_float, C.c_float]),
             "or_expf": (C.c_float, [C.c_float]),
+            "or_powf_n": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+            "or_expf_n": (None, [C.c_void_p, C.c_void_p, C.c_size_t]),
             "or_camera_derive": (None, [C.POINTER(_abi.Camera), C.POINTER(_abi.CameraFrame)]),
             "or_target_pdf": (C.c_float, [P, C.POINTER(_abi.Features), FP, FP, FP, FP, FP]),
             "or_primary": (None, [P, C.POINTER(_abi.CameraFrame), u32, u32, Rect, Rect, FP, FP]),

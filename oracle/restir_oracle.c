@@ -673,6 +673,12 @@ void or_glm_probe(const float a_[3], const float b_[3], float t, const float e[3
 }
 float or_powf(float x, float y) { return pm_powf(x, y); }
 float or_expf(float x) { return pm_expf(x); }
+void or_powf_n(const float* x, const float* y, float* out, size_t n) {
+    for (size_t i = 0; i < n; i++) out[i] = pm_powf(x[i], y[i]);
+}
+void or_expf_n(const float* x, float* out, size_t n) {
+    for (size_t i = 0; i < n; i++) out[i] = pm_expf(x[i]);
+}
 
 /* ====================================================================================================== */
 /* R-MIS / R-OMIS (render.cpp:64-265, render_utils.cpp:68-85 / 179-257, neighbour_selection.cpp:7-122,     */

@@ -48,6 +48,8 @@ void  or_glm_probe(const float a[3], const float b[3], float t, const float e[3]
 void  or_tonemap(const float c[3], float exposure, float gamma, float out[3]);
 float or_powf(float x, float y);
 float or_expf(float x);
+void or_powf_n(const float* x, const float* y, float* out, size_t n);
+void or_expf_n(const float* x, float* out, size_t n);
 void  or_camera_derive(const restir_camera* cam, restir_camera_frame* out);
 float or_target_pdf(const or_scene* s, const restir_features* f, const float origin[3],
                     const float n_t[4], const float p_mat[4], const float lpos[3], const float lcol[3]);

@@ -81,8 +81,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 
 def build_variant(name: str, defines: list[str]) -> str:
-    """Build _build/variants/<name>/libromis_amd.so with kernels.hip compiled under extra -D defines (the
-    ablation study, scripts/ablate.py).  The host objects are the shipped ones."""
+    """Build _build/variants/<name>/libromis_amd.so with kernels.hip compiled under extra -D defines (launch-bound
+    knobs such as ROMIS_SPATIAL_WPE).  The host objects are the shipped ones."""
     build()
     vdir = os.path.join(OUT, "variants", name)
     os.makedirs(vdir, exist_ok=True)

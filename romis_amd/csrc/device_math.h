@@ -109,11 +109,7 @@ __device__ __host__ __forceinline__ uint32_t mix32(uint32_t h) {
 __device__ __host__ __forceinline__ uint32_t pix_state(uint32_t key, uint32_t g) {
     return mix32(key ^ mix32(g * 0x9E3779B1u + 0x7F4A7C15u));
 }
-#if defined(ROMIS_ABL_RNG)
-__device__ __host__ __forceinline__ uint32_t draw(uint32_t ps, uint32_t slot) { uint32_t h = ps + slot * 0x9E3779B9u; return h ^ (h >> 15); }
-#else
 __device__ __host__ __forceinline__ uint32_t draw(uint32_t ps, uint32_t slot) { return mix32(ps + slot * 0x9E3779B9u); }
-#endif
 // rand() + linearMap(float(rand()), 0, RAND_MAX, 0, 1) (utils.cpp:26-31): exact (power-of-two scale)
 __device__ __forceinline__ float rand01(uint32_t d) {
     float val = (float)(d >> 1);
@@ -124,108 +120,164 @@ __device__ __forceinline__ float rand01(uint32_t d) {
 __device__ __forceinline__ uint32_t uniform_index(uint32_t d, uint32_t n) { return __umulhi(d, n); }
 __device__ __forceinline__ int uniform_offset(uint32_t d, uint32_t r) { return (int)__umulhi(d, 2u * r + 1u) - (int)r; }
 
-// ---- portable powf / expf (same algorithm as oracle/portable_math.h, evaluated in double) -----------------
-__device__ __forceinline__ double pm_ldexp1(int n) { return __longlong_as_double((long long)(n + 1023) << 52); }
+// ---- powf / expf: glibc 2.35's flt-32 algorithms, FMA objects (oracle/portable_math.h is the CPU side) -------
+// The reference's std::pow(float, float) (shading.cpp:26, tone_mapping.cpp:10) and expf (tone_mapping.cpp:9)
+// resolve to glibc's __powf_fma / __expf_fma on x86-64: log2 through a 16-entry {1/c, log2 c} table and a
+// degree-5 polynomial, exp2 through a 32-entry 2^(i/32) table and a degree-3 polynomial, all in double with the
+// fused multiply-adds of the FMA objects.  v_fma_f64 is the same single-rounding operation as vfmadd*sd, so
+// the sequence below returns glibc's bits (oracle/check_libm.c: every 32-bit base for the scenes' exponents and
+// every expf input, 0 mismatches; tests/test_gpu_parity.py::test_device_math_matches_oracle pins GPU = CPU).
+__constant__ double kGlLog2Tab[32] = {
+    0x1.661ec79f8f3bep+0, -0x1.efec65b963019p-2, 0x1.571ed4aaf883dp+0, -0x1.b0b6832d4fca4p-2,
+    0x1.49539f0f010bp+0,  -0x1.7418b0a1fb77bp-2, 0x1.3c995b0b80385p+0, -0x1.39de91a6dcf7bp-2,
+    0x1.30d190c8864a5p+0, -0x1.01d9bf3f2b631p-2, 0x1.25e227b0b8eap+0,  -0x1.97c1d1b3b7afp-3,
+    0x1.1bb4a4a1a343fp+0, -0x1.2f9e393af3c9fp-3, 0x1.12358f08ae5bap+0, -0x1.960cbbf788d5cp-4,
+    0x1.0953f419900a7p+0, -0x1.a6f9db6475fcep-5, 0x1p+0,               0x0p+0,
+    0x1.e608cfd9a47acp-1, 0x1.338ca9f24f53dp-4,  0x1.ca4b31f026aap-1,  0x1.476a9543891bap-3,
+    0x1.b2036576afce6p-1, 0x1.e840b4ac4e4d2p-3,  0x1.9c2d163a1aa2dp-1, 0x1.40645f0c6651cp-2,
+    0x1.886e6037841edp-1, 0x1.88e9c2c1b9ff8p-2,  0x1.767dcf5534862p-1, 0x1.ce0a44eb17bccp-2,
+};
+__constant__ unsigned long long kGlExp2Tab[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull,
+};
 
-__device__ __forceinline__ double pm_log_d(double a) {
-    unsigned long long b = (unsigned long long)__double_as_longlong(a);
-    int e = (int)((b >> 52) & 0x7FF) - 1023;
-    double m = __longlong_as_double((long long)((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull));
-    if (m > 1.4142135623730951) { m = m * 0.5; e = e + 1; }
-    double s = (m - 1.0) / (m + 1.0);
-    double s2 = s * s;
-    double p = 1.0 / 23.0;
-    p = 1.0 / 21.0 + s2 * p;
-    p = 1.0 / 19.0 + s2 * p;
-    p = 1.0 / 17.0 + s2 * p;
-    p = 1.0 / 15.0 + s2 * p;
-    p = 1.0 / 13.0 + s2 * p;
-    p = 1.0 / 11.0 + s2 * p;
-    p = 1.0 / 9.0 + s2 * p;
-    p = 1.0 / 7.0 + s2 * p;
-    p = 1.0 / 5.0 + s2 * p;
-    p = 1.0 / 3.0 + s2 * p;
-    double lnm = (2.0 * s) + (2.0 * s) * (s2 * p);
-    return (double)e * 0.69314718055994530942 + lnm;
+// where a kernel keeps the two tables: the __constant__ copies, or a workgroup's LDS copy (gl_stage_tables)
+struct GlTabs {
+    const double* log2;                 // [16][2] {invc, logc}
+    const unsigned long long* exp2;     // [32]
+};
+__device__ __forceinline__ GlTabs gl_global_tabs() { GlTabs t; t.log2 = kGlLog2Tab; t.exp2 = kGlExp2Tab; return t; }
+
+__device__ __forceinline__ float gl_xflowf(uint32_t sign, float y) { return (sign ? -y : y) * y; }
+__device__ __forceinline__ int gl_checkint(uint32_t iy) {
+    const int e = (int)(iy >> 23 & 0xff);
+    if (e < 0x7f) return 0;
+    if (e > 0x7f + 23) return 2;
+    if (iy & ((1u << (0x7f + 23 - e)) - 1)) return 0;
+    if (iy & (1u << (0x7f + 23 - e))) return 1;
+    return 2;
+}
+__device__ __forceinline__ bool gl_zeroinfnan(uint32_t i) { return 2u * i - 1u >= 2u * 0x7f800000u - 1u; }
+__device__ __forceinline__ bool gl_issignaling(uint32_t i) { return 2u * (i ^ 0x00400000u) > 2u * 0x7fc00000u; }
+// x86 x + y with a NaN operand: the first NaN operand, quieted
+__device__ __forceinline__ float gl_nan_add(float x, float y) {
+    const uint32_t ix = __float_as_uint(x), iy = __float_as_uint(y);
+    if ((ix & 0x7fffffffu) > 0x7f800000u) return __uint_as_float(ix | 0x00400000u);
+    if ((iy & 0x7fffffffu) > 0x7f800000u) return __uint_as_float(iy | 0x00400000u);
+    return x + y;
 }
 
-__device__ __forceinline__ double pm_exp_d(double z) {
-    double kf = floor(z * 1.4426950408889634074 + 0.5);
-    int k = (int)kf;
-    double r = (z - kf * 0.693147180369123816490) - kf * 1.90821492927058770002e-10;
-    double p = 1.0 / 6227020800.0;
-    p = 1.0 / 479001600.0 + r * p;
-    p = 1.0 / 39916800.0 + r * p;
-    p = 1.0 / 3628800.0 + r * p;
-    p = 1.0 / 362880.0 + r * p;
-    p = 1.0 / 40320.0 + r * p;
-    p = 1.0 / 5040.0 + r * p;
-    p = 1.0 / 720.0 + r * p;
-    p = 1.0 / 120.0 + r * p;
-    p = 1.0 / 24.0 + r * p;
-    p = 1.0 / 6.0 + r * p;
-    p = 0.5 + r * p;
-    p = 1.0 + r * p;
-    p = 1.0 + r * p;
-    int k1 = k / 2, k2 = k - k / 2;
-    return (p * pm_ldexp1(k1)) * pm_ldexp1(k2);
+__device__ __forceinline__ double gl_log2_inline(const GlTabs& tb, uint32_t ix) {
+    const uint32_t tmp = ix - 0x3f330000u;
+    const uint32_t i = (tmp >> 19) & 15u;
+    const uint32_t top = tmp & 0xff800000u;
+    const uint32_t iz = ix - top;
+    const int k = (int32_t)top >> 23;
+    const double2 c = reinterpret_cast<const double2*>(tb.log2)[i];   // {invc, logc}
+    const double z = (double)__uint_as_float(iz);
+    const double r = __builtin_fma(z, c.x, -1.0);
+    const double y0 = c.y + (double)k;
+    const double r2 = r * r;
+    const double y = __builtin_fma(r, 0x1.27616c9496e0bp-2, -0x1.71969a075c67ap-2);
+    const double p = __builtin_fma(r, 0x1.ec70a6ca7baddp-2, -0x1.7154748bef6c8p-1);
+    const double r4 = r2 * r2;
+    double q = __builtin_fma(r, 0x1.71547652ab82bp+0, y0);
+    q = __builtin_fma(r2, p, q);
+    return __builtin_fma(y, r4, q);
 }
 
-__device__ __forceinline__ bool pm_is_int(float y) { return y == truncf(y); }
-__device__ __forceinline__ bool pm_is_odd_int(float y) {
-    if (!pm_is_int(y) || fabsf(y) >= 16777216.0f) return false;
-    long long i = (long long)y;
-    return (i & 1) != 0;
+__device__ __forceinline__ double gl_exp2_scaled(const GlTabs& tb, unsigned long long ki, double r, double c0, double c1,
+                                                 double c2) {
+    unsigned long long t = tb.exp2[ki & 31u];
+    t += ki << 47;
+    const double s = __longlong_as_double((long long)t);
+    const double z = __builtin_fma(r, c0, c1);
+    const double r2 = r * r;
+    double y = __builtin_fma(r, c2, 1.0);
+    y = __builtin_fma(z, r2, y);
+    return y * s;
 }
 
-__device__ __noinline__ float pm_powf_general(float x, float y) {
-    if (y == 0.0f) return 1.0f;
-    if (x == 1.0f) return 1.0f;
-    if (__builtin_isnan(x) || __builtin_isnan(y)) return x + y;
-    bool yint = pm_is_int(y), yodd = pm_is_odd_int(y);
-    if (x == 0.0f) {
-        if (y < 0.0f) return yodd ? copysignf(__builtin_inff(), x) : __builtin_inff();
-        return yodd ? x : 0.0f;
-    }
-    if (__builtin_isinf(y)) {
-        float ax = fabsf(x);
-        if (ax == 1.0f) return 1.0f;
-        return ((ax < 1.0f) == (y < 0.0f)) ? __builtin_inff() : 0.0f;
-    }
-    if (__builtin_isinf(x)) {
-        if (x > 0.0f) return y < 0.0f ? 0.0f : __builtin_inff();
-        if (yodd) return y < 0.0f ? -0.0f : -__builtin_inff();
-        return y < 0.0f ? 0.0f : __builtin_inff();
-    }
-    if (x < 0.0f && !yint) return __builtin_nanf("");
-    double sign = (x < 0.0f && yodd) ? -1.0 : 1.0;
-    double ax = fabs((double)x);
-    double r;
-    if (yint && fabsf(y) <= 1048576.0f) {
-        uint32_t n = (uint32_t)fabsf(y);
-        double base = ax, acc = 1.0;
-        while (n) {
-            if (n & 1u) acc = acc * base;
-            n >>= 1;
-            if (n) base = base * base;
+// exp2_inline (e_powf.c) rounded to float: kd = ylogx + SHIFT rounds ylogx to k/32
+__device__ __forceinline__ float gl_exp2_inline(const GlTabs& tb, double ylogx, uint32_t sign_bias) {
+    double kd = ylogx + 0x1.8p+47;
+    const unsigned long long ki = (unsigned long long)__double_as_longlong(kd);
+    kd -= 0x1.8p+47;
+    const double r = ylogx - kd;
+    return (float)gl_exp2_scaled(tb, ki + sign_bias, r, 0x1.c6af84b912394p-5, 0x1.ebfce50fac4f3p-3,
+                                 0x1.62e42ff0c52d6p-1);
+}
+
+// __powf (e_powf.c) with the caller's table location
+__device__ __forceinline__ float gl_powf(const GlTabs& tb, float x, float y) {
+    uint32_t sign_bias = 0;
+    uint32_t ix = __float_as_uint(x);
+    const uint32_t iy = __float_as_uint(y);
+    if (__builtin_expect(ix - 0x00800000u >= 0x7f800000u - 0x00800000u || gl_zeroinfnan(iy), 0)) {
+        if (gl_zeroinfnan(iy)) {
+            if (2u * iy == 0u) return gl_issignaling(ix) ? gl_nan_add(x, y) : 1.0f;
+            if (ix == 0x3f800000u) return gl_issignaling(iy) ? gl_nan_add(x, y) : 1.0f;
+            if (2u * ix > 2u * 0x7f800000u || 2u * iy > 2u * 0x7f800000u) return gl_nan_add(x, y);
+            if (2u * ix == 2u * 0x3f800000u) return 1.0f;
+            if ((2u * ix < 2u * 0x3f800000u) == !(iy & 0x80000000u)) return 0.0f;
+            return y * y;
         }
-        r = (y < 0.0f) ? 1.0 / acc : acc;
-    } else {
-        double z = (double)y * pm_log_d(ax);
-        if (z > 89.0) r = __builtin_inf();
-        else if (z < -104.0) r = 0.0;
-        else r = pm_exp_d(z);
+        if (gl_zeroinfnan(ix)) {
+            float x2 = x * x;
+            if ((ix & 0x80000000u) && gl_checkint(iy) == 1) x2 = -x2;
+            return (iy & 0x80000000u) ? 1.0f / x2 : x2;
+        }
+        if (ix & 0x80000000u) {
+            const int yint = gl_checkint(iy);
+            if (yint == 0) return __uint_as_float(0xffc00000u);
+            if (yint == 1) sign_bias = 0x10000u;
+            ix &= 0x7fffffffu;
+        }
+        if (ix < 0x00800000u) {
+            ix = __float_as_uint(__uint_as_float(ix) * 0x1p23f);
+            ix &= 0x7fffffffu;
+            ix -= 23u << 23;
+        }
     }
-    return (float)(sign * r);
+    const double logx = gl_log2_inline(tb, ix);
+    const double ylogx = (double)y * logx;
+    if (__builtin_expect(((unsigned long long)__double_as_longlong(ylogx) >> 47 & 0xffffu) >= 0x80bfu, 0)) {
+        if (ylogx > 0x1.fffffffd1d571p+6) return gl_xflowf(sign_bias, 0x1p97f);
+        if (ylogx <= -150.0) return gl_xflowf(sign_bias, 0x1p-95f);
+        if (ylogx < -149.0) return gl_xflowf(sign_bias, 0x1.4p-75f);
+    }
+    return gl_exp2_inline(tb, ylogx, sign_bias);
 }
 
-__device__ __forceinline__ float pm_powf(float x, float y) { return pm_powf_general(x, y); }
-
-__device__ __forceinline__ float pm_expf(float x) {
-    if (__builtin_isnan(x)) return x;
-    if (x > 89.0f) return __builtin_inff();
-    if (x < -104.0f) return 0.0f;
-    return (float)pm_exp_d((double)x);
+// __expf (e_expf.c)
+__device__ __forceinline__ float gl_expf(const GlTabs& tb, float x) {
+    const uint32_t ux = __float_as_uint(x);
+    const double xd = (double)x;
+    const uint32_t abstop = (ux >> 20) & 0x7ffu;
+    if (__builtin_expect(abstop >= 0x42au, 0)) {
+        if (ux == 0xff800000u) return 0.0f;
+        if (abstop >= 0x7f8u) return gl_nan_add(x, x);
+        if (x > 0x1.62e42ep6f) return gl_xflowf(0, 0x1p97f);
+        if (x < -0x1.9fe368p6f) return gl_xflowf(0, 0x1p-95f);
+        if (x < -0x1.9d1d9ep6f) return gl_xflowf(0, 0x1.4p-75f);
+    }
+    double kd = __builtin_fma(0x1.71547652b82fep+5, xd, 0x1.8p+52);
+    const unsigned long long ki = (unsigned long long)__double_as_longlong(kd);
+    kd -= 0x1.8p+52;
+    const double r = __builtin_fma(0x1.71547652b82fep+5, xd, -kd);
+    return (float)gl_exp2_scaled(tb, ki, r, 0x1.c6af84b912394p-20, 0x1.ebfce50fac4f3p-13, 0x1.62e42ff0c52d6p-6);
 }
+
+// the call sites that do not stage the tables
+__device__ __noinline__ float pm_powf_general(float x, float y) { return gl_powf(gl_global_tabs(), x, y); }
+__device__ __forceinline__ float pm_powf(float x, float y) { return gl_powf(gl_global_tabs(), x, y); }
+__device__ __forceinline__ float pm_expf(float x) { return gl_expf(gl_global_tabs(), x); }
 
 }  // namespace romis

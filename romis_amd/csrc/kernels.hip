@@ -196,54 +196,51 @@ __device__ __forceinline__ Px load_px(const SceneDev& s, const Region& rg, const
     return make_px(s, n_t[gidx(rg, p)], p_mat[p], origin);
 }
 
-// |x|^n (n >= 1) by binary powering in double: exactly the product sequence of pm_powf's integer branch
-// (oracle/portable_math.h: acc = 1, acc *= base at each set bit, base squared between bits), started at the
-// lowest set bit since 1 * base == base.  With a wave-uniform n the bit tests are scalar branches (the empty
-// volatile asm keeps the compiler from turning them into per-lane selects), leaving only the f64 multiplies.
-template <bool UNIFORM>
-__device__ __forceinline__ double pow_int_chain(double base, uint32_t k) {
-    if (k == 0u) return 1.0;
-    while (!(k & 1u)) { base = base * base; k >>= 1; }
-    double acc = base;
-    k >>= 1;
-    while (k) {
-        base = base * base;
-        if (k & 1u) {
-            if (UNIFORM) asm volatile("");
-            acc = acc * base;
-        }
-        k >>= 1;
-    }
-    return acc;
-}
-
-// std::pow(cosTheta, shininess) (shading.cpp:26) specialised per material; every branch returns exactly what
-// pm_powf(x, shininess) returns (or, for ks == 0, a value whose product with ks is the same +-0 the reference
-// gets after its NaN clean-up -- see DESIGN.md "Floating point").
-__device__ __forceinline__ float material_pow(float x, const Px& px) {
-#if defined(ROMIS_ABL_POW)
-    return x * px.kd_sh.w;
-#endif
+// std::pow(cosTheta, shininess) (shading.cpp:26) = glibc's powf (device_math.h gl_powf), specialised per
+// material with the exponent's classes precomputed on the host (restir.cpp put_material, ROMIS_PWC_*):
+//  - ks == 0 skips it (the product with ks is the same +-0 the reference gets after its NaN clean-up --
+//    DESIGN.md "Floating point");
+//  - |x| below the material's threshold is glibc's own underflow exit (+-0, negative for a negative base and an
+//    odd integer exponent), decided before the log2 / exp2 evaluation;
+//  - y = +-0 / NaN / +-inf are glibc's zeroinfnan(y) returns; otherwise of its special cases only a NaN base
+//    (whose NaN the caller's clean-up zeroes whatever its payload: cosTheta is never a signalling NaN), a
+//    negative base (invalid unless y is an integer, sign from y's parity) and a zero / subnormal base remain.
+__device__ __forceinline__ float material_pow(const GlTabs& tb, float x, const Px& px) {
     const uint32_t mode = __float_as_uint(px.ks_pm.w);
     if (mode == ROMIS_POW_SKIP) return 1.0f;
-    if (mode == ROMIS_POW_INT) {
-        const uint32_t n = __float_as_uint(px.pw.y);
-        const float ax = fabsf(x);
-        if (ax < px.pw.x) return (__builtin_signbit(x) && (n & 1u)) ? -0.0f : 0.0f;   // |x|^n < 2^-151: underflow
-        if (ax <= 3.402823466e+38F) {
-            // the same multiplication chain either way; a wave whose lanes share the exponent (one material)
-            // runs it under scalar loop control instead of a per-lane divergent loop
-            const uint32_t n0 = __builtin_amdgcn_readfirstlane(n);
-            const double acc = __all(n == n0) ? pow_int_chain<true>((double)ax, n0) : pow_int_chain<false>((double)ax, n);
-            const double sign = (x < 0.0f && (n & 1u)) ? -1.0 : 1.0;
-            return (float)(sign * acc);
-        }
+    const uint32_t cls = __float_as_uint(px.pw.y);
+    const float ax = fabsf(x);
+    if (__builtin_expect(cls & ROMIS_PWC_SPECIAL, 0)) {
+        if (cls & ROMIS_PWC_ZERO) return 1.0f;
+        if (cls & ROMIS_PWC_NAN) return x == 1.0f ? 1.0f : __builtin_nanf("");
+        if (__builtin_isnan(x)) return x;
+        if (ax == 1.0f) return 1.0f;
+        return ((ax < 1.0f) == ((cls & ROMIS_PWC_PINF) != 0u)) ? 0.0f : __builtin_inff();
     }
-    return pm_powf_general(x, px.kd_sh.w);
+    const bool neg_odd = __builtin_signbit(x) && (cls & ROMIS_PWC_ODD);
+    if (!(ax >= px.pw.x)) return __builtin_isnan(x) ? x : (neg_odd ? -0.0f : 0.0f);
+    if (x < 0.0f && !(cls & ROMIS_PWC_INT)) return __uint_as_float(0xffc00000u);
+    uint32_t ix = __float_as_uint(ax);
+    if (__builtin_expect(ix < 0x00800000u, 0)) {
+        if (ix == 0u) {
+            const float z = neg_odd ? -0.0f : 0.0f;
+            return (cls & ROMIS_PWC_NEG) ? 1.0f / z : z;
+        }
+        ix = (__float_as_uint(ax * 0x1p23f) & 0x7fffffffu) - (23u << 23);
+    }
+    const double ylogx = (double)px.kd_sh.w * gl_log2_inline(tb, ix);
+    const uint32_t sign_bias = neg_odd ? 0x10000u : 0u;
+    if (__builtin_expect(((unsigned long long)__double_as_longlong(ylogx) >> 47 & 0xffffu) >= 0x80bfu, 0)) {
+        if (ylogx > 0x1.fffffffd1d571p+6) return gl_xflowf(sign_bias, 0x1p97f);
+        if (ylogx <= -150.0) return gl_xflowf(sign_bias, 0x1p-95f);
+        if (ylogx < -149.0) return gl_xflowf(sign_bias, 0x1.4p-75f);
+    }
+    return gl_exp2_inline(tb, ylogx, sign_bias);
 }
 
 // computeShading (shading.cpp:7-34), general form: every IEEE special case, any material
-__device__ __forceinline__ v3 shade_ref(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
+__device__ __forceinline__ v3 shade_ref(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,
+                                        const GlTabs& tb = gl_global_tabs()) {
     v3 kd = xyz(px.kd_sh);
     if (!f.shading) return kd;
     float d;   // glm::distance(hitPos, lightPos) == |lightPos - hitPos|, the length normalize() takes
@@ -252,7 +249,7 @@ __device__ __forceinline__ v3 shade_ref(const SceneDev& s, const FeaturesDev& f,
     if (dotNL < 0.0f) return mk(0.0f, 0.0f, 0.0f);
     v3 R = vnormalize(vsub(vscale(px.N, 2.0f * dotNL), L));
     float cosTheta = vdot(R, px.V);
-    const float pw = material_pow(cosTheta, px);
+    const float pw = material_pow(tb, cosTheta, px);
     v3 diffuse = vscale(vmul(lcol, kd), dotNL);
     v3 specular = vscale(vmul(lcol, xyz(px.ks_pm)), pw);
     // The reference zeroes a term holding a NaN.  When every colour x reflectance product is finite (host
@@ -266,15 +263,13 @@ __device__ __forceinline__ v3 shade_ref(const SceneDev& s, const FeaturesDev& f,
     return vdivs(vadd(diffuse, specular), d * d);
 }
 
-__device__ __forceinline__ v3 shade(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
-    return shade_ref(s, f, px, lpos, lcol);
+__device__ __forceinline__ v3 shade(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,
+                                    const GlTabs& tb = gl_global_tabs()) {
+    return shade_ref(s, f, px, lpos, lcol, tb);
 }
 
 // target pdf = glm::length(computeShading(...)) (light.cpp:84, reservoir.cpp:49)
 __device__ __forceinline__ float target_pdf(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
-#if defined(ROMIS_ABL_SHADE)
-    return fabsf(vdot(vsub(lpos, px.P), px.N)) * (lcol.x + lcol.y);
-#endif
     return vlength(shade_ref(s, f, px, lpos, lcol));
 }
 
@@ -552,11 +547,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 }
             };
             auto record = [&](uint32_t c) {
-#if defined(ROMIS_ABL_LIGHT0)
-                return lights + 7u * (draw(ps, 4u * c) == 0x12345u ? 1u : 0u);
-#else
                 return lights + 7u * uniform_index(draw(ps, 4u * c), L);
-#endif
             };
             auto sample = [&](uint32_t c, v3& pos, v3& col) {
                 const float4* lt = record(c);
@@ -564,18 +555,6 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
             };
             auto weight = [&](float pd) { return s.light_scale != 0.0f ? pd * s.light_scale : pd / invL; };  // light.cpp:80
             uint32_t c = 0;
-#if defined(ROMIS_RIS_U2)
-            // two independent target pdfs per iteration (more ILP per wave); updates stay in candidate order
-            for (; c + 1 < c_end; c += 2) {
-                v3 pos0, col0, pos1, col1;
-                sample(c, pos0, col0);
-                sample(c + 1, pos1, col1);
-                const float pd0 = target_pdf(s, f, px, pos0, col0);
-                const float pd1 = target_pdf(s, f, px, pos1, col1);
-                res_update<NT>(r, N, pos0, col0, weight(pd0), rand01(draw(ps, 4u * c + 3u)), pd0);
-                res_update<NT>(r, N, pos1, col1, weight(pd1), rand01(draw(ps, 4u * c + 7u)), pd1);
-            }
-#endif
             for (; c < c_end; c++) {
                 v3 pos, col;
                 sample(c, pos, col);
@@ -775,12 +754,6 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
     const Px cur = load_px(s, rg, n_t, p_mat, p, origin);
     const uint32_t ps = pix_state(key, y * rg.W + x);
     const uint32_t slot0 = 2u * K;
-#if defined(ROMIS_ABL_SPATIAL_COPY)
-    if (ps != 0x9E3779B9u || cur.t != 1.0f) {
-        for (uint32_t j = 0; j < N; j++) { Sub in; sub_load(in, ia, ib, ridx(rg, j, p)); sub_store(in, oa, ob, odbg, ridx(rg, j, p), j * npx + p); }
-        return;
-    }
-#endif
     Combiner<NT> cmb;
     cmb.init(N);
     for (uint32_t n0 = 0; n0 < K; n0 += kBatch) {
@@ -791,11 +764,7 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
         for (uint32_t i = 0; i < kBatch; i++) {
             const uint32_t n = n0 + i;
             q[i] = (uint32_t)p;
-#if defined(ROMIS_ABL_SPATIAL_SELF)
-            if (n < K && draw(ps, 2u * n) == 0x12345u)
-#else
             if (n < K)
-#endif
                 q[i] = (uint32_t)neighbour_index(rg, x, y, uniform_offset(draw(ps, 2u * n), f.R),
                                        uniform_offset(draw(ps, 2u * n + 1u), f.R));
         }
@@ -816,12 +785,7 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
             float4 a[kBatch], b[kBatch];
 #pragma unroll
             for (uint32_t i = 0; i < kBatch; i++) {
-#if defined(ROMIS_ABL_SPATIAL_SAMELINE)
-                // ablation: the neighbour's reservoir read from the cache line its G-buffer record came from
-                if (ok[i]) { a[i] = n_t[gidx(rg, q[i])]; b[i] = make_float4(g[i].x, g[i].y, g[i].z, __uint_as_float(1u)); }
-#else
                 if (ok[i]) { a[i] = ia[gidx(rg, q[i])]; b[i] = ib[gidx(rg, q[i])]; }
-#endif
             }
             // consume in draw order with ONE inlined combine body: the batch is shifted down a register per
             // step (static indices only; a rolled loop over a[i] would spill the batch to memory)
@@ -917,6 +881,11 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
 #define ROMIS_SPATIAL_WPE 4
 #endif
 #define ROMIS_SPATIAL_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL_WPE)))
+// k_spatial1 fits 96 VGPRs (5 waves per SIMD) without spilling; the general kernels spill there
+#ifndef ROMIS_SPATIAL1_WPE
+#define ROMIS_SPATIAL1_WPE 5
+#endif
+#define ROMIS_SPATIAL1_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL1_WPE)))
 #define ROMIS_SPATIAL_KERNEL(NT, UB, NAME)                                                                             \
     extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,    \
@@ -1030,11 +999,7 @@ __device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& 
     // instead of 40 for the whole batch, which keeps the kernel at 91 VGPRs = 5 waves per SIMD)
     if (ok[0]) { na[0] = ld_at(ia, qo[0]); nb[0] = ld_at(ib, qo[0]); }
     // the pixel's own sample is consumed last; its target pdf does not depend on the stream
-#if defined(ROMIS_ABL_PDCUR)
-    const float pd_cur = ca.w;
-#else
     const float pd_cur = target_pdf(s, f, cur, xyz(ca), xyz(cb));
-#endif
     Comb1 cmb;
     cmb.pos = mk(0.0f, 0.0f, 0.0f); cmb.col = mk(0.0f, 0.0f, 0.0f);
     cmb.wsum = ROMIS_FLT_MIN; cmb.chosen = 0.0f; cmb.pd = 0.0f; cmb.macc = 0u; cmb.has_pd = false;
@@ -1077,7 +1042,7 @@ __device__ __forceinline__ void spatial1_body(const SceneDev& s, const Region& r
 }
 
 #define ROMIS_SPATIAL1_KERNEL(DBG, NAME)                                                                              \
-    extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f,      \
+    extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL1_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f,     \
                                                                             uint32_t key, float ox, float oy, float oz, \
                                                                             const float4* n_t, const float4* p_mat,     \
                                                                             const float4* ia, const float4* ib,         \

@@ -79,6 +79,19 @@ struct DevBuf {
 
 uint32_t f2u(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
 float u2f(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+// the exponent classes material_pow branches on (ROMIS_PWC_*): glibc's checkint(y) and zeroinfnan(y) cases
+uint32_t pw_class(float y) {
+    uint32_t iy; std::memcpy(&iy, &y, 4);
+    if (std::isnan(y)) return ROMIS_PWC_NAN;
+    if (y == 0.0f) return ROMIS_PWC_ZERO;
+    if (std::isinf(y)) return y > 0.0f ? ROMIS_PWC_PINF : ROMIS_PWC_NINF;
+    uint32_t c = y < 0.0f ? ROMIS_PWC_NEG : 0u;
+    const int e = (int)(iy >> 23 & 0xff);
+    if (e < 0x7f) return c;
+    if (e > 0x7f + 23) return c | ROMIS_PWC_INT;
+    if (iy & ((1u << (0x7f + 23 - e)) - 1)) return c;
+    return c | ((iy & (1u << (0x7f + 23 - e))) ? ROMIS_PWC_INT | ROMIS_PWC_ODD : ROMIS_PWC_INT);
+}
 
 struct Pending {
     int kernel;
@@ -642,19 +655,20 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
         float* o = &mats[12 * m];
         o[0] = mt.kd[0]; o[1] = mt.kd[1]; o[2] = mt.kd[2]; o[3] = mt.shininess;
         o[4] = mt.ks[0]; o[5] = mt.ks[1]; o[6] = mt.ks[2];
-        uint32_t mode = ROMIS_POW_GENERAL, n = 0;
+        uint32_t mode = ROMIS_POW_GLIBC;
         float thr = 0.0f;
-        const float y = mt.shininess;
+        const double y = (double)mt.shininess;
         if (mt.ks[0] == 0.0f && mt.ks[1] == 0.0f && mt.ks[2] == 0.0f) {
             mode = ROMIS_POW_SKIP;
-        } else if (y == std::trunc(y) && y >= 1.0f && y <= 1048576.0f) {
-            mode = ROMIS_POW_INT;
-            n = (uint32_t)y;
-            // |x| < thr  =>  |x|^n <= 2^-152, which the double powering rounds to a float +-0
-            thr = std::nextafter((float)std::exp2(-152.0 / (double)n), 0.0f);
+        } else if (std::isfinite(y) && y > 0.0) {
+            // |x| < thr  =>  y * log2|x| < -150 (1 + 2^-20): glibc's powf takes its underflow exit
+            // (ylogx <= -150, returns +-0, the sign for a negative base and an odd integer y); the margin
+            // dwarfs the 2^-32 relative error of its log2 and the rounding of y * log2|x|
+            thr = (float)std::exp2(-150.0 * (1.0 + 0x1p-20) / y);
+            if ((double)thr > std::exp2(-150.0 * (1.0 + 0x1p-20) / y)) thr = std::nextafter(thr, 0.0f);
         }
         o[7] = u2f(mode);
-        o[8] = thr; o[9] = u2f(n); o[10] = mt.transparency; o[11] = 0.0f;
+        o[8] = thr; o[9] = u2f(pw_class(mt.shininess)); o[10] = mt.transparency; o[11] = 0.0f;
     };
     for (uint32_t m = 0; m < num_meshes; m++) put_material(m, meshes[m].material);
     {

@@ -9,8 +9,16 @@
 
 // material pow modes (std::pow(cosTheta, shininess), shading.cpp:26)
 #define ROMIS_POW_SKIP 0u      // ks == 0: the specular term is +-0 whatever pow returns
-#define ROMIS_POW_INT 1u       // shininess is an integer in [1, 2^20]: binary powering in double
-#define ROMIS_POW_GENERAL 2u   // anything else: pm_powf_general
+#define ROMIS_POW_GLIBC 1u     // glibc's powf specialised to the material's exponent (kernels.hip material_pow)
+// exponent classes of ROMIS_POW_GLIBC (materials[3m + 2].y)
+#define ROMIS_PWC_ODD 1u       // glibc checkint(y) == 1: odd integer
+#define ROMIS_PWC_INT 2u       // checkint(y) != 0: integer
+#define ROMIS_PWC_NEG 4u       // y < 0
+#define ROMIS_PWC_ZERO 8u      // y == +-0
+#define ROMIS_PWC_NAN 16u      // y is NaN
+#define ROMIS_PWC_PINF 32u     // y == +inf
+#define ROMIS_PWC_NINF 64u     // y == -inf
+#define ROMIS_PWC_SPECIAL (ROMIS_PWC_ZERO | ROMIS_PWC_NAN | ROMIS_PWC_PINF | ROMIS_PWC_NINF)
 
 namespace romis {
 
@@ -33,7 +41,7 @@ struct SceneDev {
     const float4* tri_n2;
     uint32_t num_tris;
     // Materials: 3 float4 each: (kd.xyz, shininess), (ks.xyz, bits(pow mode)),
-    // (pow underflow threshold, bits(integer exponent), transparency, 0).  Last entry = miss material.
+    // (pow underflow threshold, bits(shininess class ROMIS_PWC_*), transparency, 0).  Last entry = miss material.
     const float4* materials;
     uint32_t num_materials;
     // Lights: 7 float4 each: (p0.xyz, bits(type)), (p1.xyz, 0), (p2.xyz, 0), c0, c1, c2, c3

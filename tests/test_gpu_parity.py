@@ -273,15 +273,25 @@ def test_final_shading_binned_rays(gpu, oracle, name):
 
 
 def test_device_math_matches_oracle(gpu, oracle):
+    """gl_powf / gl_expf on the GPU == the oracle's glibc restatement (== this image's libm, bit for bit:
+    tests/test_oracle_pinning.py) -- the scenes' exponents over 2^20 random bit patterns each, random exponents,
+    and the special cases."""
     rng = np.random.default_rng(3)
-    x = np.concatenate([rng.uniform(-1, 1, 4096), rng.uniform(0, 50, 4096), [0.0, -0.0, 1.0, -1.0, np.inf, -np.inf,
-                        np.nan, 1e-40, -3.0, 2.0]]).astype(np.float32)
-    y = np.concatenate([np.full(4096, 250.0), rng.uniform(-3, 3, 4096), [2.0, 3.0, np.nan, np.inf, -1.0, 3.0, 0.0,
-                        5.0, 0.5, -np.inf]]).astype(np.float32)
+    bits = lambda n: rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    n = 1 << 20
+    xs, ys = [], []
+    for e in (1.0, 4.0, 10.0, 250.0, 1 / 2.2, 1 / 2.4):
+        xs += [bits(n), rng.uniform(-1, 1, n // 4)]
+        ys += [np.full(n, e), np.full(n // 4, e)]
+    xs += [rng.uniform(0, 50, 4096), bits(n), [0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 1e-40, -3.0, 2.0]]
+    ys += [rng.uniform(-3, 3, 4096), bits(n), [2.0, 3.0, np.nan, np.inf, -1.0, 3.0, 0.0, 5.0, 0.5, -np.inf]]
+    x = np.concatenate([np.asarray(a, np.float32) for a in xs])
+    y = np.concatenate([np.asarray(a, np.float32) for a in ys])
     pw, ex = gpu.debug_math(x, y)
     lib = oracle.lib()
-    want_pw = np.array([lib.or_powf(float(a), float(b)) for a, b in zip(x, y)], np.float32)
-    want_ex = np.array([lib.or_expf(float(a)) for a in x], np.float32)
+    want_pw, want_ex = np.empty_like(x), np.empty_like(x)
+    lib.or_powf_n(x.ctypes.data, y.ctypes.data, want_pw.ctypes.data, x.size)
+    lib.or_expf_n(x.ctypes.data, want_ex.ctypes.data, x.size)
     assert_bits(pw, want_pw, "powf")
     assert_bits(ex, want_ex, "expf")
 

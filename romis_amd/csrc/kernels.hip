@@ -508,7 +508,7 @@ template <int NT>
 __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                           const float4* lights, const Bvh& bvh, float4 nt, float4 pm, uint32_t x,
                                           uint32_t y, size_t p, float4* __restrict__ ra, float4* __restrict__ rb,
-                                          float2* __restrict__ rdbg) {
+                                          float2* __restrict__ rdbg, float* __restrict__ rp) {
     const uint32_t L = s.num_lights;
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
@@ -562,10 +562,14 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 res_update<NT>(r, N, pos, col, weight(pd), rand01(draw(ps, 4u * c + 3u)), pd);
             }
             for (uint32_t j = 0; j < N; j++) {
+                // the held sample's target pdf: W's p-hat (light.cpp:90-93) and, N = 1, the pdf cache rp
+                const float pj = r[j].has_pd ? r[j].pd : target_pdf(s, f, px, r[j].pos, r[j].col);
                 if (f.initial_vis && !visible(bvh, px.P, r[j].pos)) r[j].W = 0.0f;
-                else r[j].W = contribution_weight(r[j].has_pd ? r[j].pd : target_pdf(s, f, px, r[j].pos, r[j].col), r[j].M,
-                                                  r[j].wsum);
+                else r[j].W = contribution_weight(pj, r[j].M, r[j].wsum);
+                if (NT == 1 && rp) rp[p] = pj;
             }
+        } else if (NT == 1 && rp) {
+            rp[p] = target_pdf(s, f, make_px(s, nt, pm, origin), r[0].pos, r[0].col);   // no lights: the initial sample
         }
         for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, ridx(rg, j, p), j * npx + p);
     }
@@ -578,7 +582,7 @@ template <int NT, bool LDS_LIGHTS>
 __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                          const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                          float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
-                                         WorkQueue wq) {
+                                         float* __restrict__ rp, WorkQueue wq) {
     const float4* lights = s.lights;
     if (LDS_LIGHTS) {
         for (uint32_t i = threadIdx.x; i < 7u * s.num_lights; i += blockDim.x) g_lds[i] = s.lights[i];
@@ -592,7 +596,7 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
         uint32_t x, y;
         size_t p;
         if (!work_pixel(rg, item, x, y, p)) continue;
-        ris_pixel<NT>(s, rg, f, key, origin, lights, bvh, n_t[gidx(rg, p)], p_mat[p], x, y, p, ra, rb, rdbg);
+        ris_pixel<NT>(s, rg, f, key, origin, lights, bvh, n_t[gidx(rg, p)], p_mat[p], x, y, p, ra, rb, rdbg, rp);
     }
 }
 
@@ -604,7 +608,8 @@ template <int NT, bool LDS_LIGHTS>
 __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region& rg, const CameraDev& cam,
                                                  const FeaturesDev& f, uint32_t key, float4* __restrict__ n_t,
                                                  float4* __restrict__ p_mat, float4* __restrict__ n_t2,
-                                                 float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg) {
+                                                 float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
+                                                 float* __restrict__ rp) {
     const uint32_t bvh_f4 = 2u * s.num_nodes + 3u * s.num_tris;
     const float4* lights = s.lights;
     if (LDS_LIGHTS) {
@@ -620,7 +625,7 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         if (!work_pixel(rg, item, x, y, p)) continue;
         float4 nt, pm;
         primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, nt, pm);
-        ris_pixel<NT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg);
+        ris_pixel<NT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp);
     }
 }
 
@@ -633,8 +638,8 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
 #define ROMIS_RIS_KERNEL(NT, LDS, NAME, ATTR)                                                                         \
     extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,   \
-                                                          float4* ra, float4* rb, float2* rdbg, WorkQueue wq) {         \
-        ris_body<NT, LDS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg, wq);                                 \
+                                                          float4* ra, float4* rb, float2* rdbg, float* rp, WorkQueue wq) { \
+        ris_body<NT, LDS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg, rp, wq);                             \
     }
 ROMIS_RIS_KERNEL(1, false, k_ris_n1, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL(2, false, k_ris_n2, )
@@ -646,8 +651,8 @@ ROMIS_RIS_KERNEL(0, true, k_ris_n0_lds, )
 #define ROMIS_PRIMARY_RIS_KERNEL(NT, LDS, NAME, ATTR)                                                                  \
     extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, CameraDev cam, FeaturesDev f,   \
                                                           uint32_t key, float4* n_t, float4* p_mat, float4* n_t2,      \
-                                                          float4* ra, float4* rb, float2* rdbg) {                      \
-        primary_ris_body<NT, LDS>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg);                                  \
+                                                          float4* ra, float4* rb, float2* rdbg, float* rp) {           \
+        primary_ris_body<NT, LDS>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp);                              \
     }
 ROMIS_PRIMARY_RIS_KERNEL(1, true, k_primary_ris_n1_lds, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(1, false, k_primary_ris_n1, ROMIS_RIS_ATTR)
@@ -673,17 +678,22 @@ struct Combiner {
     }
     // combine one input sub-reservoir (reservoir.cpp:47-54 / :75-82)
     __device__ __forceinline__ void consume(const SceneDev& s, const FeaturesDev& f, const Px& cur, const Sub& in, uint32_t ps, uint32_t slot0) {
-        float pd = target_pdf(s, f, cur, in.pos, in.col);
+        consume_pd(target_pdf(s, f, cur, in.pos, in.col), in, ps, slot0);
+    }
+    // the same with the input's target pdf at the combining pixel already known (the rp cache)
+    __device__ __forceinline__ void consume_pd(float pd, const Sub& in, uint32_t ps, uint32_t slot0) {
         float w = (pd * in.W) * (float)in.M;
         uint32_t k = res_update<NT>(out, n(), in.pos, in.col, w, rand01(draw(ps, slot0 + t)), pd);
         t++;
         macc_add<NT>(macc, k, in.M);
     }
-    __device__ __forceinline__ void finish_biased(const SceneDev& s, const FeaturesDev& f, const Px& cur) {
+    __device__ __forceinline__ void finish_biased(const SceneDev& s, const FeaturesDev& f, const Px& cur, float* pd_out = nullptr) {
         for (uint32_t j = 0; j < n(); j++) out[j].M = macc[j];
-        for (uint32_t j = 0; j < n(); j++)
-            out[j].W = contribution_weight(out[j].has_pd ? out[j].pd : target_pdf(s, f, cur, out[j].pos, out[j].col),
-                                           out[j].M, out[j].wsum);
+        for (uint32_t j = 0; j < n(); j++) {
+            const float pj = out[j].has_pd ? out[j].pd : target_pdf(s, f, cur, out[j].pos, out[j].col);
+            out[j].W = contribution_weight(pj, out[j].M, out[j].wsum);
+            if (pd_out) pd_out[j] = pj;
+        }
     }
 };
 
@@ -692,7 +702,8 @@ template <int NT>
 __device__ __forceinline__ void temporal_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
                                               v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                               const float4* ca, const float4* cb, const float4* __restrict__ pa,
-                                              const float4* __restrict__ pb, float4* oa, float4* ob, float2* odbg) {
+                                              const float4* __restrict__ pb, float4* oa, float4* ob, float2* odbg,
+                                              const float* rp_in, float* rp_out) {
     uint32_t x, y;
     size_t p;
     if (!region_pixel(rg, blockIdx.x * blockDim.x + threadIdx.x, x, y, p)) return;
@@ -715,18 +726,22 @@ __device__ __forceinline__ void temporal_body(const SceneDev& s, const Region& r
     const uint32_t ps = pix_state(key, y * rg.W + x);
     Combiner<NT> cmb;
     cmb.init(N);
-    for (uint32_t j = 0; j < N; j++) cmb.consume(s, f, px, cur[j], ps, 0u);
+    // N = 1 with the pdf cache: the current reservoir's target pdf here is the one its producer stored
+    if (NT == 1 && rp_in) cmb.consume_pd(rp_in[p], cur[0], ps, 0u);
+    else for (uint32_t j = 0; j < N; j++) cmb.consume(s, f, px, cur[j], ps, 0u);
     for (uint32_t j = 0; j < N; j++) cmb.consume(s, f, px, prev[j], ps, 0u);
-    cmb.finish_biased(s, f, px);
+    float pd_out[NT > 0 ? NT : 1];
+    cmb.finish_biased(s, f, px, NT == 1 ? pd_out : nullptr);
     for (uint32_t j = 0; j < N; j++) sub_store(cmb.out[j], oa, ob, odbg, ridx(rg, j, p), j * npx + p);
+    if (NT == 1 && rp_out) rp_out[p] = pd_out[0];
 }
 
 #define ROMIS_TEMPORAL_KERNEL(NT)                                                                                      \
     extern "C" __global__ __launch_bounds__(256) void k_temporal_n##NT(                                               \
         SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,          \
         const float4* p_mat, const float4* ca, const float4* cb, const float4* pa, const float4* pb, float4* oa,      \
-        float4* ob, float2* odbg) {                                                                                   \
-        temporal_body<NT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ca, cb, pa, pb, oa, ob, odbg);                   \
+        float4* ob, float2* odbg, const float* rp_in, float* rp_out) {                                                \
+        temporal_body<NT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ca, cb, pa, pb, oa, ob, odbg, rp_in, rp_out);    \
     }
 ROMIS_TEMPORAL_KERNEL(1)
 ROMIS_TEMPORAL_KERNEL(2)
@@ -950,6 +965,7 @@ __device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& 
                                                v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                                const float4* __restrict__ ia, const float4* __restrict__ ib,
                                                float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
+                                               const float* __restrict__ rp_in, float* __restrict__ rp_out,
                                                uint32_t x, uint32_t y) {
     const uint32_t K = f.K;   // <= kLeanK (host check)
     const int rx = (int)(x - rg.vx0), ry = (int)(y - rg.vy0);
@@ -977,6 +993,19 @@ __device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& 
     float4 na[kLeanK], nb[kLeanK];
     // pixel shading context (material + view vector) while the neighbour records are in flight
     const Px cur = make_px(s, cn, cpm, origin);
+    // A primary-ray miss (value-initialised HitInfo: material kd = ks = 0, normal 0, P not NaN): its zero normal
+    // rejects every neighbour (finite neighbour normals, s.normals_bounded: dot = +-0 < 0.906), and the target
+    // pdf of any finite-colour sample there is exactly 0, so the combine takes only the pixel's
+    // own reservoir with w = (0 * W) * M = +-0 (W finite): no sample is accepted, wSum stays FLT_MIN, M = M_own,
+    // W = 0.  The pass's result for such a lane is known without its target pdfs.
+    if (cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z) &&
+        __builtin_isfinite(ca.w) && __builtin_isfinite(cb.x + cb.y + cb.z)) {
+        st_at(oa, pofs, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+        st_at(ob, pofs, make_float4(0.0f, 0.0f, 0.0f, cb.w));
+        if (DBG) st_at(odbg, pofs >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
+        if (rp_out) st_at(rp_out, pofs >> 2, 0.0f);
+        return;
+    }
     // depth / normal heuristic (render_utils.cpp:114-118): one shared reciprocal of the pixel's depth
     const double rt = rcp_d(cur.t);
     const bool rt_ok = div_fast_ok(cur.t);
@@ -998,8 +1027,9 @@ __device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& 
     // accepted neighbours' reservoirs, one neighbour ahead of the consume sequence (two in flight: 16 VGPRs
     // instead of 40 for the whole batch, which keeps the kernel at 91 VGPRs = 5 waves per SIMD)
     if (ok[0]) { na[0] = ld_at(ia, qo[0]); nb[0] = ld_at(ib, qo[0]); }
-    // the pixel's own sample is consumed last; its target pdf does not depend on the stream
-    const float pd_cur = target_pdf(s, f, cur, xyz(ca), xyz(cb));
+    // the pixel's own sample is consumed last; its target pdf does not depend on the stream, and when the
+    // input's producer stored it (the pdf cache rp: same pixel, same G-buffer, same sample) it is read back
+    const float pd_cur = rp_in ? ld_at(rp_in, pofs >> 2) : target_pdf(s, f, cur, xyz(ca), xyz(cb));
     Comb1 cmb;
     cmb.pos = mk(0.0f, 0.0f, 0.0f); cmb.col = mk(0.0f, 0.0f, 0.0f);
     cmb.wsum = ROMIS_FLT_MIN; cmb.chosen = 0.0f; cmb.pd = 0.0f; cmb.macc = 0u; cmb.has_pd = false;
@@ -1014,40 +1044,224 @@ __device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& 
     }
     cmb.take(pd_cur, ca.w, __float_as_uint(cb.w), xyz(ca), xyz(cb));
     // finish_biased: M = routed sum, W from the held sample's target pdf (light.cpp:90-93 / reservoir.cpp:61-64)
+    // nothing accepted: the held sample is the initial (0, 0) one, whose shaded value is +-0 at any pixel with
+    // a non-NaN position (zero colour; NaN terms are zeroed; d >= 1e-5 or d = 1), so W = 0 (reservoir.cpp:62)
     float p = cmb.pd;
-    if (!cmb.has_pd) p = target_pdf(s, f, cur, cmb.pos, cmb.col);
+    if (!cmb.has_pd) p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, cmb.pos, cmb.col);
     const float W = contribution_weight(p, cmb.macc, cmb.wsum);
     st_at(oa, pofs, make_float4(cmb.pos.x, cmb.pos.y, cmb.pos.z, W));
     st_at(ob, pofs, make_float4(cmb.col.x, cmb.col.y, cmb.col.z, __uint_as_float(cmb.macc)));
     if (DBG) st_at(odbg, pofs >> 1, make_float2(cmb.wsum, cmb.chosen));
+    if (rp_out) st_at(rp_out, pofs >> 2, p);
+}
+
+// Tile of block b (XCD b % 8, block b runs on XCD b % 8): XCD x owns every 8th chunk of rg.xcd_rows tile
+// rows (chunks x, x + 8, x + 16, ...), walked row-major, so its L2 holds the chunk's G-buffer and reservoirs
+// while the gathers reach 10 px across tile borders; interleaving short chunks spreads cheap (background)
+// and expensive rows evenly over the XCDs -- contiguous bands left the background XCDs idle (1.28x the mean
+// work on the busiest XCD at C2, 1.02x with 2-row chunks).  rg.xcd_rows = 0: one contiguous band per XCD.
+__device__ __forceinline__ bool xcd_tile(const Region& rg, uint32_t T, uint32_t b, uint32_t& tile) {
+    const uint32_t x = b % 8u, j = b / 8u;
+    if (rg.xcd_rows == 0u) {
+        const uint32_t q = T / 8u, rem = T % 8u;
+        tile = x * q + min(x, rem) + j;
+        return j < q + (x < rem ? 1u : 0u);
+    }
+    const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
+    const uint32_t chunk = rg.xcd_rows * ntx;
+    const uint32_t i = j / chunk;
+    tile = ((x + 8u * i) * rg.xcd_rows) * ntx + (j - i * chunk);
+    return tile < T;
 }
 
 template <bool DBG>
 __device__ __forceinline__ void spatial1_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
                                               v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                               const float4* __restrict__ ia, const float4* __restrict__ ib,
-                                              float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg) {
-    // XCD-banded 32x8 tiles, waves of 8x8 pixels (rg.map2d = 2), as spatial_body
-    const uint32_t T = num_tiles(rg);
-    const uint32_t nb = gridDim.x, b = blockIdx.x, xcd = b % 8u;
-    const uint32_t xcd_blocks = nb / 8u + (xcd < nb % 8u ? 1u : 0u);
-    const uint32_t q = T / 8u, rem = T % 8u;
-    const uint32_t band0 = xcd * q + min(xcd, rem), band_len = q + (xcd < rem ? 1u : 0u);
-    for (uint32_t t = b / 8u; t < band_len; t += xcd_blocks) {
-        uint32_t x, y;
-        size_t p;
-        if (tile_pixel_of(rg, band0 + t, x, y, p))
-            spatial1_pixel<DBG>(s, rg, f, key, origin, n_t, p_mat, ia, ib, oa, ob, odbg, x, y);
-    }
+                                              float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
+                                              const float* __restrict__ rp_in, float* __restrict__ rp_out) {
+    // 32x8 tiles in the XCD order above, one per block; waves of 8x8 pixels (rg.map2d = 2)
+    uint32_t tile, x, y;
+    size_t p;
+    if (xcd_tile(rg, num_tiles(rg), blockIdx.x, tile) && tile_pixel_of(rg, tile, x, y, p))
+        spatial1_pixel<DBG>(s, rg, f, key, origin, n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out, x, y);
 }
+
+// ---------------------------------------------------------------------------------------------------------
+// k_spatial1_lds: the N = 1 biased pass with the tile's neighbourhood staged in LDS (north_star's screen-tile
+// staging).  The global-gather form is bound by its scattered accesses, not its arithmetic: every neighbour
+// costs three 16-byte gathers whose 64 lanes touch ~64 distinct cache lines each (a pass with the target pdfs
+// cut to a third took 92 of 99 us; removing the pixel's own pdf changed nothing).  Here a 256-thread block
+// owns a 32x8 tile and first copies the records of the tile grown by R -- (32 + 2R) x (8 + 2R) pixels of
+// n_t, res_a, res_b, 48 B each, 70 KB at R = 10 -- with row-coalesced loads into LDS; every neighbour read is
+// then an LDS read.  Two blocks fit a CU (2 waves per SIMD), so the kernel leans on instruction-level
+// parallelism instead of occupancy: the K neighbour target pdfs are independent of each other (only the
+// reservoir updates are ordered), so they are evaluated side by side before the ordered updates run.
+// Same arithmetic, RNG slots and update order as spatial1_pixel; R <= kLdsSpatialR (host check).
+constexpr uint32_t kLdsSpatialR = 10;
+constexpr uint32_t kApronMax = (kTileW + 2u * kLdsSpatialR) * (kTileH + 2u * kLdsSpatialR);   // 1456 px
+
+template <bool DBG, bool STAGE_NT>
+__device__ __forceinline__ void spatial1_lds_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
+                                                  v3 origin, const float4* __restrict__ n_t,
+                                                  const float4* __restrict__ p_mat, const float4* __restrict__ ia,
+                                                  const float4* __restrict__ ib, float4* __restrict__ oa,
+                                                  float4* __restrict__ ob, float2* __restrict__ odbg,
+                                                  const float* __restrict__ rp_in, float* __restrict__ rp_out) {
+    // STAGE_NT = false: only the reservoirs are staged (32 B per pixel, 3 blocks per CU); the neighbours'
+    // n_t records are gathered from global memory together with the staging loads (one round trip either way)
+    float4* const l_a = g_lds;
+    float4* const l_b = g_lds + kApronMax;
+    float4* const l_nt = g_lds + 2u * kApronMax;
+    uint32_t tile;
+    if (!xcd_tile(rg, num_tiles(rg), blockIdx.x, tile)) return;   // block-uniform
+    const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
+    const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTileH);
+    // neighbour clamp bounds (render_utils.cpp:109-110: the image; here also the stored view), global coords
+    const int xlo = max(0, (int)rg.vx0), xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1;
+    const int ylo = max(0, (int)rg.vy0), yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1;
+    const int R = (int)f.R;
+    // the staged rectangle: the tile grown by R, clipped to the clamp bounds (every neighbour lies inside)
+    const int ax0 = max(tx0 - R, xlo), ax1 = min(tx0 + (int)kTileW - 1 + R, xhi);
+    const int ay0 = max(ty0 - R, ylo), ay1 = min(ty0 + (int)kTileH - 1 + R, yhi);
+    const uint32_t AW = (uint32_t)(ax1 - ax0 + 1), n_apron = AW * (uint32_t)(ay1 - ay0 + 1);
+    // this lane's pixel: waves are 8x8 blocks of the tile (rg.map2d = 2)
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    const int x = tx0 + (int)(w * 8u + (l & 7u)), y = ty0 + (int)(l >> 3);
+    const bool live = x < (int)(rg.rx0 + rg.rw) && y < (int)(rg.ry0 + rg.rh);
+    const uint32_t pofs = ((uint32_t)(y - (int)rg.vy0) * rg.vw + (uint32_t)(x - (int)rg.vx0)) << 4;
+    // own records that are not staged, issued first
+    float4 cpm = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float pd_cached = 0.0f;
+    if (live) {
+        cpm = ld_at(p_mat, pofs);
+        if (rp_in) pd_cached = ld_at(rp_in, pofs >> 2);
+    }
+    // stage: at most ceil(1456 / 256) = 6 pixels per thread, all loads in flight before the LDS stores
+    {
+        constexpr uint32_t kPer = (kApronMax + 255u) / 256u;
+        const uint32_t magic = 0xFFFFFFFFu / AW + 1u;   // i / AW for i < 2^16 (checked below)
+        float4 va[kPer], vb[kPer], vn[kPer];
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++) {
+            const uint32_t i = threadIdx.x + 256u * k;
+            if (i < n_apron) {
+                uint32_t r = __umulhi(i, magic);
+                if (r * AW > i) r--;
+                const uint32_t c = i - r * AW;
+                const uint32_t g = (((uint32_t)(ay0 - (int)rg.vy0) + r) * rg.vw + (uint32_t)(ax0 - (int)rg.vx0) + c) << 4;
+                if (STAGE_NT) vn[k] = ld_at(n_t, g);
+                va[k] = ld_at(ia, g);
+                vb[k] = ld_at(ib, g);
+            }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++) {
+            const uint32_t i = threadIdx.x + 256u * k;
+            if (i < n_apron) {
+                if (STAGE_NT) l_nt[i] = vn[k];
+                l_a[i] = va[k];
+                l_b[i] = vb[k];
+            }
+        }
+    }
+    // neighbour draws while the staging loads are in flight
+    const uint32_t K = f.K;   // <= kLeanK (host check)
+    const uint32_t ps = pix_state(key, (uint32_t)y * rg.W + (uint32_t)x);
+    const uint32_t span = 2u * f.R + 1u;
+    uint32_t qi[kLeanK];
+    float4 gq[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        qi[n] = 0u;
+        if (n < K) {
+            const int nx = min(max(x - R + (int)__umulhi(draw(ps, 2u * n), span), xlo), xhi);
+            const int ny = min(max(y - R + (int)__umulhi(draw(ps, 2u * n + 1u), span), ylo), yhi);
+            qi[n] = (uint32_t)(ny - ay0) * AW + (uint32_t)(nx - ax0);
+            if (!STAGE_NT && live)
+                gq[n] = ld_at(n_t, ((uint32_t)(ny - (int)rg.vy0) * rg.vw + (uint32_t)(nx - (int)rg.vx0)) << 4);
+        }
+    }
+    float4 cn_g = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (!STAGE_NT && live) cn_g = ld_at(n_t, pofs);
+    __syncthreads();
+    if (!live) return;   // no barrier follows
+    const uint32_t ci = (uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0);
+    const float4 cn = STAGE_NT ? l_nt[ci] : cn_g, ca = l_a[ci], cb = l_b[ci];
+    const Px cur = make_px(s, cn, cpm, origin);
+    // primary-ray miss: the pass's result is known (spatial1_pixel)
+    if (cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z) &&
+        __builtin_isfinite(ca.w) && __builtin_isfinite(cb.x + cb.y + cb.z)) {
+        st_at(oa, pofs, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+        st_at(ob, pofs, make_float4(0.0f, 0.0f, 0.0f, cb.w));
+        if (DBG) st_at(odbg, pofs >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
+        if (rp_out) st_at(rp_out, pofs >> 2, 0.0f);
+        return;
+    }
+    // depth / normal heuristic (render_utils.cpp:114-118), one shared reciprocal of the pixel's depth
+    const double rt = rcp_d(cur.t);
+    const bool rt_ok = div_fast_ok(cur.t);
+    bool ok[kLeanK];
+    float4 na[kLeanK], nb[kLeanK];
+    float pd[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        ok[n] = false;
+        if (n < K) {
+            const float4 g = STAGE_NT ? l_nt[qi[n]] : gq[n];
+            na[n] = l_a[qi[n]];
+            nb[n] = l_b[qi[n]];
+            const float nd = vdot(xyz(g), cur.N);
+            float q = div_by_rcp_d(g.w, rt);
+            if (!rt_ok) q = g.w / cur.t;
+            ok[n] = !(nd < 0.90630778703f) && !(fabsf(1.0f - q) > 0.1f);
+        }
+    }
+    // the K target pdfs, independent of each other: evaluated side by side (rejected lanes' values unused)
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++)
+        if (n < K) pd[n] = target_pdf(s, f, cur, xyz(na[n]), xyz(nb[n]));
+    const float pd_cur = rp_in ? pd_cached : target_pdf(s, f, cur, xyz(ca), xyz(cb));
+    Comb1 cmb;
+    cmb.pos = mk(0.0f, 0.0f, 0.0f); cmb.col = mk(0.0f, 0.0f, 0.0f);
+    cmb.wsum = ROMIS_FLT_MIN; cmb.chosen = 0.0f; cmb.pd = 0.0f; cmb.macc = 0u; cmb.has_pd = false;
+    cmb.h = ps + 2u * K * 0x9E3779B9u;
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++)
+        if (n < K && ok[n]) cmb.take(pd[n], na[n].w, __float_as_uint(nb[n].w), xyz(na[n]), xyz(nb[n]));
+    cmb.take(pd_cur, ca.w, __float_as_uint(cb.w), xyz(ca), xyz(cb));
+    float p = cmb.pd;
+    if (!cmb.has_pd) p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, cmb.pos, cmb.col);
+    const float W = contribution_weight(p, cmb.macc, cmb.wsum);
+    st_at(oa, pofs, make_float4(cmb.pos.x, cmb.pos.y, cmb.pos.z, W));
+    st_at(ob, pofs, make_float4(cmb.col.x, cmb.col.y, cmb.col.z, __uint_as_float(cmb.macc)));
+    if (DBG) st_at(odbg, pofs >> 1, make_float2(cmb.wsum, cmb.chosen));
+    if (rp_out) st_at(rp_out, pofs >> 2, p);
+}
+
+#ifndef ROMIS_SPATIAL1_LDS_WPE
+#define ROMIS_SPATIAL1_LDS_WPE 2
+#endif
+#define ROMIS_SPATIAL1_LDS_KERNEL(DBG, STAGE_NT, WPE, NAME)                                                           \
+    extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void                        \
+    NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
+         const float4* p_mat, const float4* ia, const float4* ib, float4* oa, float4* ob, float2* odbg,               \
+         const float* rp_in, float* rp_out) {                                                                         \
+        spatial1_lds_body<DBG, STAGE_NT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out); \
+    }
+ROMIS_SPATIAL1_LDS_KERNEL(false, true, ROMIS_SPATIAL1_LDS_WPE, k_spatial1_lds)
+ROMIS_SPATIAL1_LDS_KERNEL(true, true, ROMIS_SPATIAL1_LDS_WPE, k_spatial1_lds_dbg)
+ROMIS_SPATIAL1_LDS_KERNEL(false, false, 3, k_spatial1_ldsr)
+ROMIS_SPATIAL1_LDS_KERNEL(true, false, 3, k_spatial1_ldsr_dbg)
 
 #define ROMIS_SPATIAL1_KERNEL(DBG, NAME)                                                                              \
     extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL1_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f,     \
                                                                             uint32_t key, float ox, float oy, float oz, \
                                                                             const float4* n_t, const float4* p_mat,     \
                                                                             const float4* ia, const float4* ib,         \
-                                                                            float4* oa, float4* ob, float2* odbg) {     \
-        spatial1_body<DBG>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg);                           \
+                                                                            float4* oa, float4* ob, float2* odbg,       \
+                                                                            const float* rp_in, float* rp_out) {        \
+        spatial1_body<DBG>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);           \
     }
 ROMIS_SPATIAL1_KERNEL(false, k_spatial1)
 ROMIS_SPATIAL1_KERNEL(true, k_spatial1_dbg)
@@ -1904,8 +2118,8 @@ hipError_t launch_primary(const SceneDev& s, const Region& rg0, const CameraDev&
 }
 
 hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
-                      const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, const Tuning& tu,
-                      QueueState& qs, hipStream_t stream) {
+                      const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, float* rp,
+                      const Tuning& tu, QueueState& qs, hipStream_t stream) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, 0);
     WorkQueue wq{nullptr, 0u};
@@ -1920,13 +2134,13 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f
     auto k = use_lds ? (f.N == 1 ? k_ris_n1_lds : (f.N == 2 ? k_ris_n2_lds : k_ris_n0_lds))
                      : (f.N == 1 ? k_ris_n1 : (f.N == 2 ? k_ris_n2 : k_ris_n0));
     ROMIS_LAUNCH(k, grid, dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ra,
-                       rb, rdbg, wq);
+                       rb, rdbg, f.N == 1 ? rp : nullptr, wq);
     return hipGetLastError();
 }
 
 hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const CameraDev& cam, const FeaturesDev& f, uint32_t key,
                               float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,
-                              const Tuning& tu, hipStream_t stream) {
+                              float* rp, const Tuning& tu, hipStream_t stream) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, tu.primary_2d);
     const size_t bvh = bvh_lds_bytes(s), lights = lights_lds_bytes(s);
@@ -1935,7 +2149,7 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
     auto k = use_lights ? (f.N == 1 ? k_primary_ris_n1_lds : (f.N == 2 ? k_primary_ris_n2_lds : k_primary_ris_n0_lds))
                         : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
     ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.ris_blocks), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
-                 cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg);
+                 cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr);
     return hipGetLastError();
 }
 
@@ -1944,19 +2158,21 @@ bool primary_ris_fits(const SceneDev& s) { return bvh_lds_bytes(s) <= kLdsBudget
 hipError_t launch_temporal(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
                            const float4* n_t, const float4* p_mat, const float4* ca, const float4* cb,
                            const float4* pa, const float4* pb, float4* oa, float4* ob, float2* odbg,
-                           const Tuning& tu, hipStream_t stream) {
+                           const float* rp_in, float* rp_out, const Tuning& tu, hipStream_t stream) {
     (void)tu;
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, 0);
     auto k = f.N == 1 ? k_temporal_n1 : (f.N == 2 ? k_temporal_n2 : k_temporal_n0);
     ROMIS_LAUNCH(k, dim3(items_of(rg)), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ca, cb,
-                       pa, pb, oa, ob, odbg);
+                       pa, pb, oa, ob, odbg, f.N == 1 ? rp_in : nullptr, f.N == 1 ? rp_out : nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
                           const float4* n_t, const float4* p_mat, const float4* ia, const float4* ib, float4* oa,
-                          float4* ob, float2* odbg, const Tuning& tu, hipStream_t stream) {
+                          float4* ob, float2* odbg, const float* rp_in, float* rp_out, bool* rp_written,
+                          const Tuning& tu, hipStream_t stream) {
+    if (rp_written) *rp_written = false;
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     Region rg = with_map(rg0, tu.spatial_xcd);   // XCD-banded order works on 2D tiles
     if (rg.map2d && tu.spatial_wave8) rg.map2d = 2u;
@@ -1964,8 +2180,33 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
     if (tu.spatial_blocks) grid = std::min(grid, std::max(8u, tu.spatial_blocks));
     if (tu.spatial_lean && !f.unbiased && f.N == 1 && f.K <= kLeanK && rg.ps == 1u && rg.map2d == 2u &&
         (size_t)rg.vw * rg.vh * 16u <= 0xFFFFFFFFull) {
-        ROMIS_LAUNCH(odbg ? k_spatial1_dbg : k_spatial1, dim3(grid), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1],
-                     o[2], n_t, p_mat, ia, ib, oa, ob, odbg);
+        // one block per tile, grid rounded to the XCD that owns the most tiles (xcd_tile)
+        const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
+        rg.xcd_rows = tu.spatial_xcd_rows;
+        if (rg.xcd_rows) {
+            const uint32_t chunks = (nty + rg.xcd_rows - 1) / rg.xcd_rows;
+            grid = 8u * ((chunks + 7u) / 8u) * rg.xcd_rows * ntx;
+        }
+        if (tu.spatial_lds == 2u && f.R <= kLdsSpatialR) {
+            ROMIS_LAUNCH(odbg ? k_spatial1_ldsr_dbg : k_spatial1_ldsr, dim3(grid), dim3(kBlock), 2u * kApronMax * 16u, stream,
+                         s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
+        } else if (tu.spatial_lds && f.R <= kLdsSpatialR) {
+            static bool attr_set = false;   // > 64 KB of dynamic LDS must be requested per kernel
+            if (!attr_set) {
+                for (const void* k : {(const void*)k_spatial1_lds, (const void*)k_spatial1_lds_dbg}) {
+                    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                             (int)(3u * kApronMax * 16u));
+                    if (e != hipSuccess) return e;
+                }
+                attr_set = true;
+            }
+            ROMIS_LAUNCH(odbg ? k_spatial1_lds_dbg : k_spatial1_lds, dim3(grid), dim3(kBlock), 3u * kApronMax * 16u, stream,
+                         s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
+        } else {
+            ROMIS_LAUNCH(odbg ? k_spatial1_dbg : k_spatial1, dim3(grid), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1],
+                         o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
+        }
+        if (rp_written) *rp_written = rp_out != nullptr;
         return hipGetLastError();
     }
     auto k = f.unbiased ? (f.N == 1 ? k_spatial_n1_unbiased : (f.N == 2 ? k_spatial_n2_unbiased : k_spatial_n0_unbiased))

@@ -5,24 +5,28 @@
 
 namespace romis {
 
+// The target-pdf cache (N = 1, SoA planes, nullable): rp[p] = the target pdf of pixel p's held sample at p.
+// RIS / temporal / k_spatial1 write it for their output; temporal and k_spatial1 read it for the input's own
+// sample instead of re-evaluating it (same pixel, same G-buffer, same sample: the same bits).
 // n_t2 (nullable): a second record buffer that also receives the G-buffer n_t (the ping-pong partner)
 hipError_t launch_primary(const SceneDev& s, const Region& rg, const CameraDev& cam, float4* n_t, float4* p_mat,
                           float4* n_t2, const Tuning& tu, hipStream_t stream);
 hipError_t launch_ris(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
-                      const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, const Tuning& tu,
-                      QueueState& qs, hipStream_t stream);
+                      const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, float* rp,
+                      const Tuning& tu, QueueState& qs, hipStream_t stream);
 // genPrimaryRayHits + genCanonicalSamples in one kernel over the same region (needs the BVH to fit in LDS)
 hipError_t launch_primary_ris(const SceneDev& s, const Region& rg, const CameraDev& cam, const FeaturesDev& f, uint32_t key,
                               float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,
-                              const Tuning& tu, hipStream_t stream);
+                              float* rp, const Tuning& tu, hipStream_t stream);
 bool primary_ris_fits(const SceneDev& s);
 hipError_t launch_temporal(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
                            const float4* n_t, const float4* p_mat, const float4* ca, const float4* cb,
                            const float4* pa, const float4* pb, float4* oa, float4* ob, float2* odbg,
-                           const Tuning& tu, hipStream_t stream);
+                           const float* rp_in, float* rp_out, const Tuning& tu, hipStream_t stream);
 hipError_t launch_spatial(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
                           const float4* n_t, const float4* p_mat, const float4* ia, const float4* ib, float4* oa,
-                          float4* ob, float2* odbg, const Tuning& tu, hipStream_t stream);
+                          float4* ob, float2* odbg, const float* rp_in, float* rp_out, bool* rp_written,
+                          const Tuning& tu, hipStream_t stream);
 hipError_t launch_final(const SceneDev& s, const Region& rg, const FeaturesDev& f, const float* origin,
                         const float4* n_t, const float4* p_mat, const float4* ra, const float4* rb, float* rgb,
                         const Tuning& tu, hipStream_t stream);

@@ -122,6 +122,7 @@ struct restir_ctx {
     uint32_t vw = 0, vh = 0, N = 0;
     DevBuf n_t, p_mat, ra[2], rb[2], dbg[2], rgb;   // stage API: SoA planes
     DevBuf rec[2];                                  // restir_render / halo frames: per-pixel records
+    DevBuf rp[2];                                   // their target-pdf cache planes (N = 1, planes layout)
     int cur = 0;
     uint32_t rgb_w = 0, rgb_h = 0;
 
@@ -145,6 +146,7 @@ struct restir_ctx {
         uint64_t send_bytes = 0, recv_bytes = 0;
         int cur = 0;
         bool fb_records = true;
+        bool rp_ok = false;   // the current grid's target-pdf cache is valid (restir_render's rp_ok)
     } halo;
     DevBuf halo_scratch;
 
@@ -521,6 +523,8 @@ struct FrameBufs {
     float4* ra(int i) const { return c->rec[i].as<float4>() + (records ? 1 : 0); }
     float4* rb(int i) const { return c->rec[i].as<float4>() + (records ? 2 : npx * N); }
     float4* nt2() const { return records ? c->rec[1].as<float4>() : nullptr; }
+    // the target-pdf cache planes (N = 1 planes layout only)
+    float* rp(int i) const { return (!records && N == 1) ? c->rp[i].as<float>() : nullptr; }
     const float4* pa(const restir_frame* f) const { return f->rec.as<float4>() + (records ? 1 : 0); }
     const float4* pb(const restir_frame* f) const { return f->rec.as<float4>() + (records ? 2 : npx * N); }
     Region region(Region r) const { return records ? with_records(r, N) : r; }
@@ -532,6 +536,8 @@ restir_status ensure_records(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N
     ST_TRY(c->p_mat.ensure(npx * 16));
     if (!fb.records) ST_TRY(c->n_t.ensure(npx * 16));
     for (int i = 0; i < 2; i++) ST_TRY(c->rec[i].ensure(npx * (fb.records ? 1u + 2u * N : 2u * N) * 16));
+    if (!fb.records && N == 1)
+        for (int i = 0; i < 2; i++) ST_TRY(c->rp[i].ensure(npx * 4));
     c->vw = vw; c->vh = vh; c->N = N;
     return RESTIR_OK;
 }
@@ -587,7 +593,7 @@ void restir_destroy(restir_ctx* c) {
         (void)hipStreamSynchronize(c->stream);
         for (DevBuf* b : {&c->nodes, &c->tri_v0, &c->tri_e1, &c->tri_e2, &c->tri_n0, &c->tri_n1, &c->tri_n2,
                           &c->materials, &c->lights, &c->n_t, &c->p_mat, &c->ra[0], &c->ra[1], &c->rb[0], &c->rb[1],
-                          &c->dbg[0], &c->dbg[1], &c->rgb, &c->queue_ctr, &c->halo_scratch, &c->rec[0], &c->rec[1]})
+                          &c->dbg[0], &c->dbg[1], &c->rgb, &c->queue_ctr, &c->halo_scratch, &c->rec[0], &c->rec[1], &c->rp[0], &c->rp[1]})
             b->release();
         for (Pending& p : c->pending) { (void)hipEventDestroy(p.start); (void)hipEventDestroy(p.stop); }
         for (hipEvent_t ev : c->free_events) (void)hipEventDestroy(ev);
@@ -745,6 +751,10 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
             }
         s.shade_finite = (finite && cmax * kmax <= 0x1p120) ? 1u : 0u;
     }
+    s.normals_bounded = 1u;
+    for (const std::vector<float>* nv : {&n0, &n1, &n2})
+        for (size_t i = 0; i < nv->size(); i++)
+            if ((i % 4) != 3 && !(std::fabs((*nv)[i]) <= 0x1p125f)) s.normals_bounded = 0u;
     c->has_scene = true;
     return RESTIR_OK;
 }
@@ -773,8 +783,8 @@ static restir_status render_mis(restir_ctx* c, const restir_camera* cam, const r
     HIP_TRY(hipMemsetAsync(c->mis_acc.p, 0, (size_t)c->mis_rows * W * H * 4, c->stream));
     for (uint32_t it = 0; it < features->max_iterations_mis; it++) {
         TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, it), camd.origin, nt, pm,
-                                          c->ra[0].as<float4>(), c->rb[0].as<float4>(), c->dbg[0].as<float2>(), c->tuning,
-                                          c->queue, c->stream));
+                                          c->ra[0].as<float4>(), c->rb[0].as<float4>(), c->dbg[0].as<float2>(), nullptr,
+                                          c->tuning, c->queue, c->stream));
         TIMED(c, RESTIR_K_MIS, launch_mis_accumulate(s, W, H, f, camd.origin, nt, pm, c->mis_nbr.as<uint32_t>(),
                                                      c->ra[0].as<float4>(), c->rb[0].as<float4>(), c->dbg[0].as<float2>(), it,
                                                      c->mis_acc.as<float>(), c->mis_smp.as<float>(), c->mis_smp_samples,
@@ -864,24 +874,26 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     const uint32_t ris_key = restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, 0);
     if (c->tuning.fuse_primary_ris && primary_ris_fits(s)) {   // same region: one kernel (kernels.hip k_primary_ris)
         TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),
-                                                          fb.rb(cur), nullptr, c->tuning, c->stream));
+                                                          fb.rb(cur), nullptr, fb.rp(cur), c->tuning, c->stream));
     } else {
         TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, fb.nt(0), pm, fb.nt2(), c->tuning, c->stream));
         TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, ris_key, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), nullptr,
-                                          c->tuning, c->queue, c->stream));
+                                          fb.rp(cur), c->tuning, c->queue, c->stream));
     }
     if (temporal) {
         TIMED(c, RESTIR_K_TEMPORAL,
               launch_temporal(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0), camd.origin, fb.nt(cur), pm,
-                              fb.ra(cur), fb.rb(cur), fb.pa(prev), fb.pb(prev), fb.ra(cur), fb.rb(cur), nullptr, c->tuning,
-                              c->stream));
+                              fb.ra(cur), fb.rb(cur), fb.pa(prev), fb.pb(prev), fb.ra(cur), fb.rb(cur), nullptr,
+                              fb.rp(cur), fb.rp(cur), c->tuning, c->stream));
     }
+    bool rp_ok = fb.rp(cur) != nullptr;   // the current grid's target-pdf cache holds its samples' pdfs
     for (uint32_t pass = 0; pass < passes; pass++) {
         const Region pr = grow_rect(owned, (passes - 1u - pass) * f.R);
         const int nxt = cur ^ 1;
         TIMED(c, RESTIR_K_SPATIAL,
               launch_spatial(s, pr, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_SPATIAL, pass), camd.origin, fb.nt(cur), pm,
-                             fb.ra(cur), fb.rb(cur), fb.ra(nxt), fb.rb(nxt), nullptr, c->tuning, c->stream));
+                             fb.ra(cur), fb.rb(cur), fb.ra(nxt), fb.rb(nxt), nullptr, rp_ok ? fb.rp(cur) : nullptr,
+                             fb.rp(nxt), &rp_ok, c->tuning, c->stream));
         cur = nxt;
     }
     TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), c->rgb.as<float>(),
@@ -1041,7 +1053,7 @@ restir_status restir_stage_ris(restir_ctx* c, const restir_camera* cam, const re
     const int cur = c->cur;
     TIMED(c, RESTIR_K_RIS, launch_ris(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                                       c->ra[cur].as<float4>(), c->rb[cur].as<float4>(),
-                                      debug ? c->dbg[cur].as<float2>() : nullptr, c->tuning, c->queue, c->stream));
+                                      debug ? c->dbg[cur].as<float2>() : nullptr, nullptr, c->tuning, c->queue, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
@@ -1058,7 +1070,7 @@ restir_status restir_stage_temporal(restir_ctx* c, const restir_camera* cam, con
           launch_temporal(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                           c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->ra[prv].as<float4>(), c->rb[prv].as<float4>(),
                           c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), debug ? c->dbg[cur].as<float2>() : nullptr,
-                          c->tuning, c->stream));
+                          nullptr, nullptr, c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
@@ -1074,7 +1086,7 @@ restir_status restir_stage_spatial(restir_ctx* c, const restir_camera* cam, cons
     TIMED(c, RESTIR_K_SPATIAL,
           launch_spatial(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                          c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->ra[nxt].as<float4>(), c->rb[nxt].as<float4>(),
-                         debug ? c->dbg[nxt].as<float2>() : nullptr, c->tuning, c->stream));
+                         debug ? c->dbg[nxt].as<float2>() : nullptr, nullptr, nullptr, nullptr, c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->cur = nxt;   // the pass output becomes "current" (RES_*), its input "prev" (PREV_*)
     return RESTIR_OK;
@@ -1273,12 +1285,13 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
     // reservoirs only on the owned rectangle
     TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, h.view, h.camd, fb.nt(0), pm, fb.nt2(), c->tuning, c->stream));
     TIMED(c, RESTIR_K_RIS, launch_ris(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_RIS, 0), h.camd.origin,
-                                      fb.nt(0), pm, fb.ra(0), fb.rb(0), nullptr, c->tuning, c->queue, c->stream));
+                                      fb.nt(0), pm, fb.ra(0), fb.rb(0), nullptr, fb.rp(0), c->tuning, c->queue, c->stream));
     if (temporal)
         TIMED(c, RESTIR_K_TEMPORAL,
               launch_temporal(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_TEMPORAL, 0), h.camd.origin, fb.nt(0),
-                              pm, fb.ra(0), fb.rb(0), fb.pa(prev), fb.pb(prev), fb.ra(0), fb.rb(0), nullptr, c->tuning,
-                              c->stream));
+                              pm, fb.ra(0), fb.rb(0), fb.pa(prev), fb.pb(prev), fb.ra(0), fb.rb(0), nullptr, fb.rp(0),
+                              fb.rp(0), c->tuning, c->stream));
+    h.rp_ok = fb.rp(0) != nullptr;
     h.active = true;
     if (send_bytes) *send_bytes = h.send_bytes;
     if (recv_bytes) *recv_bytes = h.recv_bytes;
@@ -1333,7 +1346,7 @@ restir_status restir_halo_spatial(restir_ctx* c) {
     TIMED(c, RESTIR_K_SPATIAL,
           launch_spatial(c->sdev, h.owned, h.f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_SPATIAL, h.pass), h.camd.origin,
                          fb.nt(h.cur), c->p_mat.as<float4>(), fb.ra(h.cur), fb.rb(h.cur), fb.ra(nxt), fb.rb(nxt), nullptr,
-                         c->tuning, c->stream));
+                         h.rp_ok ? fb.rp(h.cur) : nullptr, fb.rp(nxt), &h.rp_ok, c->tuning, c->stream));
     h.cur = nxt;
     h.pass++;
     return RESTIR_OK;
@@ -1401,6 +1414,8 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "ris.lds")) t.ris_lds = v;
     else if (!std::strcmp(key, "spatial.xcd")) t.spatial_xcd = v;
     else if (!std::strcmp(key, "spatial.blocks")) t.spatial_blocks = v;
+    else if (!std::strcmp(key, "spatial.xcd_rows")) t.spatial_xcd_rows = v;
+    else if (!std::strcmp(key, "spatial.lds")) t.spatial_lds = v;
     else if (!std::strcmp(key, "spatial.wave8")) t.spatial_wave8 = v;
     else if (!std::strcmp(key, "spatial.lean")) t.spatial_lean = v;
     else if (!std::strcmp(key, "fuse.primary_ris")) t.fuse_primary_ris = v;

@@ -51,6 +51,8 @@ struct SceneDev {
     float light_scale;         // L when 1/L is a power of two (then p / (1/L) == p * L exactly), else 0
     uint32_t lights_finite;    // every light coordinate / colour is finite
     uint32_t shade_finite;     // every light colour x material kd / ks product is finite (shade()'s NaN tests)
+    uint32_t normals_bounded;  // every vertex normal component finite with |n| <= 2^125: interpolated normals are
+                               // finite, so a miss pixel's zero normal rejects every neighbour (dot = +-0)
 };
 
 // Image region bookkeeping: global image W x H (y = 0 bottom), storage view (the computed region, row-major)
@@ -64,6 +66,7 @@ struct Region {
     // lives at index j * js + p * ps.  SoA planes: ps = 1, js = view pixels.  Per-pixel records
     // [n_t, a_0, b_0, a_1, b_1, ...] (restir_render): ps = 1 + 2N, js = 2, with res_a = rec + 1, res_b = rec + 2.
     uint32_t ps, js;
+    uint32_t xcd_rows;   // k_spatial1's XCD tile order (xcd_tile); 0 elsewhere
 };
 
 // Launch-shape knobs (restir_set_tuning); they never change results, only speed.
@@ -75,6 +78,9 @@ struct Tuning {
     uint32_t ris_lds = 1;          // stage the light table in LDS when it fits
     uint32_t ris_queue = 0;        // persistent blocks (this many) pulling tiles from a WorkQueue; 0 = off
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
+    uint32_t spatial_lds = 0;      // k_spatial1: stage the tile's neighbourhood in LDS (R <= 10): 1 n_t + reservoirs,
+                                   // 2 reservoirs only; both measured slower than the gathers
+    uint32_t spatial_xcd_rows = 4; // k_spatial1: XCD x takes every 8th chunk of this many tile rows (0: one band)
     uint32_t spatial_blocks = 0;
     uint32_t spatial_wave8 = 1;
     uint32_t fuse_primary_ris = 1; // restir_render: k_primary_ris instead of k_primary + k_ris when the BVH fits LDS

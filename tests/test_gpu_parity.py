@@ -197,29 +197,44 @@ def test_temporal_bit_exact(gpu, oracle, N, clamp):
     assert_bits(gpu.download(_abi.BUF_RES_DBG), od, "wSum/chosen")
 
 
+# spatial kernels of an N = 1 biased pass: k_spatial1 (gathers; XCD order in 4-row chunks or one band),
+# k_spatial1_lds (n_t + reservoirs staged in LDS), k_spatial1_ldsr (reservoirs staged), the general kernel
+SPATIAL_VARIANTS = {"gather": {"spatial.lean": 1, "spatial.lds": 0},
+                    "gather_band": {"spatial.lean": 1, "spatial.lds": 0, "spatial.xcd_rows": 0},
+                    "lds": {"spatial.lean": 1, "spatial.lds": 1},
+                    "ldsr": {"spatial.lean": 1, "spatial.lds": 2},
+                    "general": {"spatial.lean": 0}}
+SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 0, "spatial.xcd_rows": 4}
+
+
 @pytest.mark.parametrize("name", ["nightclub_128pt", "cornell_parallelogram"])
 @pytest.mark.parametrize("N", [1, 2, 3])
 @pytest.mark.parametrize("mode", ["biased", "unbiased", "unbiased_vis"])
-@pytest.mark.parametrize("lean", [1, 0])
+@pytest.mark.parametrize("lean", list(SPATIAL_VARIANTS))
 def test_spatial_pass_bit_exact(gpu, oracle, name, N, mode, lean):
-    if lean == 0 and (N != 1 or mode != "biased"):
-        pytest.skip("spatial.lean only selects the kernel of N = 1 biased passes")
-    gpu.set_tuning("spatial.lean", lean)   # 1: k_spatial1 (default), 0: the general spatial kernel
-    _, osc, cam = setup(gpu, oracle, name, N)
-    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
-    f = _abi.default_features(num_samples_in_reservoir=N, unbiased_combination=int(mode != "biased"),
-                              spatial_reuse_visibility_check=int(mode == "unbiased_vis"))
-    a, b, _ = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
-    for which, arr in [(_abi.BUF_GBUF_N_T, n_t), (_abi.BUF_GBUF_P_MAT, p_mat), (_abi.BUF_RES_A, a), (_abi.BUF_RES_B, b)]:
-        gpu.upload(which, arr)
-    for p in range(2):
-        kp = key(_abi.RESTIR_STAGE_SPATIAL, p)
-        gpu.stage_spatial(cam, f, kp)
-        a, b, d = oracle.spatial_pass(osc, f, kp, origin(oracle, cam), W, H, n_t, p_mat, (a, b))
-        assert_bits(gpu.download(_abi.BUF_RES_A), a, f"pass {p} res_a")
-        assert_bits(gpu.download(_abi.BUF_RES_B), b, f"pass {p} res_b")
-        assert_bits(gpu.download(_abi.BUF_RES_DBG), d, f"pass {p} wSum/chosen")
-    gpu.set_tuning("spatial.lean", 1)
+    if lean != "gather" and (N != 1 or mode != "biased"):
+        pytest.skip("the kernel variants differ only for N = 1 biased passes")
+    for k, v in SPATIAL_VARIANTS[lean].items():
+        gpu.set_tuning(k, v)
+    try:
+        _, osc, cam = setup(gpu, oracle, name, N)
+        n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+        f = _abi.default_features(num_samples_in_reservoir=N, unbiased_combination=int(mode != "biased"),
+                                  spatial_reuse_visibility_check=int(mode == "unbiased_vis"))
+        a, b, _ = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
+        for which, arr in [(_abi.BUF_GBUF_N_T, n_t), (_abi.BUF_GBUF_P_MAT, p_mat), (_abi.BUF_RES_A, a),
+                           (_abi.BUF_RES_B, b)]:
+            gpu.upload(which, arr)
+        for p in range(2):
+            kp = key(_abi.RESTIR_STAGE_SPATIAL, p)
+            gpu.stage_spatial(cam, f, kp)
+            a, b, d = oracle.spatial_pass(osc, f, kp, origin(oracle, cam), W, H, n_t, p_mat, (a, b))
+            assert_bits(gpu.download(_abi.BUF_RES_A), a, f"pass {p} res_a")
+            assert_bits(gpu.download(_abi.BUF_RES_B), b, f"pass {p} res_b")
+            assert_bits(gpu.download(_abi.BUF_RES_DBG), d, f"pass {p} wSum/chosen")
+    finally:
+        for k, v in SPATIAL_DEFAULTS.items():
+            gpu.set_tuning(k, v)
 
 
 @pytest.mark.parametrize("k,r", [(0, 10), (10, 30), (5, 1)])

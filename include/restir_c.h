@@ -232,7 +232,19 @@ restir_status restir_render(restir_ctx* ctx, const restir_camera* cam, const res
                             const restir_frame* prev, restir_frame** out_next, float* out_rgb);
 
 restir_status restir_frame_retain(restir_frame* frame);
+/* Drops a reference.  The last one hands the grid's device records back to the producing context for re-use,
+ * ordered on the GPU after every kernel that wrote or read them (no host or device-wide synchronisation). */
 void          restir_frame_release(restir_frame* frame);
+
+/* The grid a frame holds -- renderReSTIR's returned ReservoirGrid (render.h:25-28, render.cpp:61) -- over the
+ * frame's computed view (vw x vh pixels at (vx0, vy0) of the W x H image; the whole image for untiled frames).
+ * restir_frame_info: any pointer may be NULL.  restir_frame_download copies, per sub-reservoir j and view pixel
+ * p (index j * vw * vh + p, rows y = 0 bottom): outputSamples[j].position -> pos[3 i], .color -> color[3 i],
+ * .W -> w[i], sampleNums[j] -> m[i]; any output may be NULL, each holds vw * vh * N entries (x3 for pos /
+ * color).  Waits for the frame's producer, then copies synchronously. */
+restir_status restir_frame_info(const restir_frame* frame, uint32_t* width, uint32_t* height, uint32_t* vx0,
+                                uint32_t* vy0, uint32_t* vw, uint32_t* vh, uint32_t* n);
+restir_status restir_frame_download(const restir_frame* frame, float* pos, float* color, float* w, uint32_t* m);
 restir_status restir_synchronize(restir_ctx* ctx);
 
 /* Last rendered image (owned pixels), host float RGB, row 0 = top. */

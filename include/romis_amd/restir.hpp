@@ -12,9 +12,12 @@
 // The Scene / EmbreeInterface pair becomes Renderer::setScene (uploads materials, lights and the BVH once).
 #pragma once
 
+#include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../restir_c.h"
@@ -33,6 +36,44 @@ inline void check(restir_status s, const char* what) {
 struct Features : restir_features {
     Features() { restir_features_default(this); }
 };
+
+// The reference's own struct Features (src/utils/common.h:89-136) -> Features, field by field by the reference's
+// member names (any type with those members works, so the reference's header is not needed here).  The enums
+// keep their values: RayTraceMode {ReSTIR, RMIS, ROMIS} (common.h:25-29) = restir_mode,
+// NeighbourSelectionStrategy (common.h:36-41) = restir_neighbour_strategy, MISWeightRMIS (common.h:31-34) =
+// restir_mis_weight.  Fields off the path (enableRecursive, enableHardShadow, maxReflectionRecursion, ...) are
+// not read by renderReSTIR / renderRMIS / renderROMIS and have no counterpart.
+template <class RefFeatures>
+Features fromReferenceFeatures(const RefFeatures& rf) {
+    Features f;
+    f.ray_trace_mode = static_cast<uint32_t>(rf.rayTraceMode);
+    f.initial_light_samples = rf.initialLightSamples;
+    f.num_samples_in_reservoir = rf.numSamplesInReservoir;
+    f.num_neighbours_to_sample = rf.numNeighboursToSample;
+    f.spatial_resample_radius = rf.spatialResampleRadius;
+    f.spatial_resampling_passes = rf.spatialResamplingPasses;
+    f.temporal_clamp_m = rf.temporalClampM;
+    f.initial_samples_visibility_check = rf.initialSamplesVisibilityCheck ? 1 : 0;
+    f.unbiased_combination = rf.unbiasedCombination ? 1 : 0;
+    f.spatial_reuse = rf.spatialReuse ? 1 : 0;
+    f.spatial_reuse_visibility_check = rf.spatialReuseVisibilityCheck ? 1 : 0;
+    f.temporal_reuse = rf.temporalReuse ? 1 : 0;
+    f.enable_shading = rf.enableShading ? 1 : 0;
+    f.enable_texture_mapping = rf.enableTextureMapping ? 1 : 0;
+    f.enable_tone_mapping = rf.enableToneMapping ? 1 : 0;
+    f.gamma = rf.gamma;
+    f.exposure = rf.exposure;
+    f.neighbour_same_geometry = rf.neighbourSameGeometry ? 1 : 0;
+    f.use_progressive_romis = rf.useProgressiveROMIS ? 1 : 0;
+    f.save_alphas_visualisation = rf.saveAlphasVisualisation ? 1 : 0;
+    f.neighbour_max_depth_difference_fraction = rf.neighbourMaxDepthDifferenceFraction;
+    f.neighbour_max_normal_angle_difference_radians = rf.neighbourMaxNormalAngleDifferenceRadians;
+    f.max_iterations_mis = rf.maxIterationsMIS;
+    f.neighbour_selection_strategy = static_cast<uint32_t>(rf.neighbourSelectionStrategy);
+    f.mis_weight_rmis = static_cast<uint32_t>(rf.misWeightRMIS);
+    f.progressive_update_mod = rf.progressiveUpdateMod;
+    return f;
+}
 
 // Trackball state after Trackball(window, glm::radians(fov), dist) + setCamera(lookAt, glm::radians(rot), dist)
 struct Camera : restir_camera {
@@ -69,6 +110,13 @@ struct Screen {
     float* pixel(int x, int yFromTop) { return &rgb[(size_t(yFromTop) * width + x) * 3]; }
 };
 
+// One sub-reservoir's state as reservoir.h:18-32 keeps it: outputSamples[j] = {position, color, W},
+// sampleNums[j] = M.
+struct ReservoirSample {
+    float position[3], color[3], W;
+    uint32_t M;
+};
+
 // Device-resident ReservoirGrid (reservoir.h:75).
 class ReservoirGrid {
 public:
@@ -77,6 +125,25 @@ public:
     ReservoirGrid(const ReservoirGrid&) = delete;
     ReservoirGrid& operator=(const ReservoirGrid&) = delete;
     restir_frame* handle() const { return frame_; }
+    // host copy, [N][vh][vw] (rows y = 0 bottom): the per-pixel state renderReSTIR returns (render.cpp:61)
+    std::vector<ReservoirSample> download(uint32_t* n = nullptr, uint32_t* vw = nullptr, uint32_t* vh = nullptr) const {
+        uint32_t N = 0, w = 0, h = 0;
+        check(restir_frame_info(frame_, nullptr, nullptr, nullptr, nullptr, &w, &h, &N), "restir_frame_info");
+        const size_t cnt = size_t(N) * w * h;
+        std::vector<float> pos(3 * cnt), col(3 * cnt), W(cnt);
+        std::vector<uint32_t> M(cnt);
+        check(restir_frame_download(frame_, pos.data(), col.data(), W.data(), M.data()), "restir_frame_download");
+        std::vector<ReservoirSample> out(cnt);
+        for (size_t i = 0; i < cnt; i++) {
+            for (int a = 0; a < 3; a++) { out[i].position[a] = pos[3 * i + a]; out[i].color[a] = col[3 * i + a]; }
+            out[i].W = W[i];
+            out[i].M = M[i];
+        }
+        if (n) *n = N;
+        if (vw) *vw = w;
+        if (vh) *vh = h;
+        return out;
+    }
 
 private:
     restir_frame* frame_;
@@ -111,6 +178,37 @@ private:
     restir_ctx* ctx_ = nullptr;
 };
 
+// Contexts for callers that render concurrently: the reference's CLI renders one std::thread per camera through
+// renderRayTraced with a shared Scene and EmbreeInterface (main.cpp:213-230).  Each calling thread gets its own
+// Renderer -- its own HIP stream, buffers and scene upload -- created on first use, so the threads never
+// serialise on one context's mutex, and each camera keeps its own previous-frame grid (the caller's
+// std::shared_ptr<ReservoirGrid>, as in the reference).  Thread-safe.
+class RendererPool {
+public:
+    RendererPool(int device, Scene scene, uint32_t seed = RESTIR_DEFAULT_SEED)
+        : device_(device), scene_(std::move(scene)), seed_(seed) {}
+    RendererPool(const RendererPool&) = delete;
+    RendererPool& operator=(const RendererPool&) = delete;
+    // this thread's renderer (frame index 0 at creation, advancing by one per render)
+    Renderer& local() {
+        std::lock_guard<std::mutex> lk(mu_);
+        std::unique_ptr<Renderer>& r = per_thread_[std::this_thread::get_id()];
+        if (!r) {
+            r = std::make_unique<Renderer>(device_);
+            r->setScene(scene_);
+            r->setSeed(seed_, 0);
+        }
+        return *r;
+    }
+
+private:
+    int device_;
+    Scene scene_;
+    uint32_t seed_;
+    std::mutex mu_;
+    std::map<std::thread::id, std::unique_ptr<Renderer>> per_thread_;
+};
+
 // renderReSTIR (render.cpp:28-62): primary hits, initial RIS, [temporal if prev], [spatial x passes], final
 // shading + tone mapping into `screen`; returns the frame's final grid for the next frame's temporal reuse.
 inline std::shared_ptr<ReservoirGrid> renderReSTIR(Renderer& r, const std::shared_ptr<ReservoirGrid>& prev,
@@ -140,6 +238,11 @@ inline std::shared_ptr<ReservoirGrid> renderRayTraced(Renderer& r, const std::sh
         case RESTIR_MODE_ROMIS: renderMIS(r, camera, screen, features); return nullptr;
         default: throw RestirError("Unsupported ray-tracing render mode requested from entry point");
     }
+}
+// ... from any thread: the calling thread's context of the pool
+inline std::shared_ptr<ReservoirGrid> renderRayTraced(RendererPool& pool, const std::shared_ptr<ReservoirGrid>& prev,
+                                                      const Camera& camera, Screen& screen, const Features& features) {
+    return renderRayTraced(pool.local(), prev, camera, screen, features);
 }
 
 }  // namespace romis

@@ -132,6 +132,9 @@ SIGNATURES = {
                                 C.POINTER(Tile), _P, C.POINTER(_P), C.POINTER(C.c_float)]),
     "restir_frame_retain": (C.c_int, [_P]),
     "restir_frame_release": (None, [_P]),
+    "restir_frame_info": (C.c_int, [_P] + [C.POINTER(C.c_uint32)] * 7),
+    "restir_frame_download": (C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                        C.POINTER(C.c_uint32)]),
     "restir_synchronize": (C.c_int, [_P]),
     "restir_download_rgb": (C.c_int, [_P, C.POINTER(C.c_float), C.c_size_t]),
     "restir_stage_configure": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32]),

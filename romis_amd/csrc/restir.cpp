@@ -14,7 +14,9 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <vector>
 #include <string>
 #include <vector>
 
@@ -100,13 +102,95 @@ struct Pending {
 
 }  // namespace
 
+// Record buffers that temporal frames hand back (restir_frame_release): each comes with the events of the work
+// that last touched it (the producing frame's kernels, every render that read it as a predecessor), so a context
+// re-uses it by making its stream wait on those events -- no hipMalloc / hipFree / device-wide sync per frame.
+struct FramePool {
+    struct Entry {
+        DevBuf buf;
+        std::vector<hipEvent_t> busy;
+    };
+    std::mutex mu;
+    std::vector<Entry> free;
+    bool closed = false;   // the owning context is gone: returned buffers are freed
+    int device = 0;
+    static void drain(Entry& e) {
+        for (hipEvent_t ev : e.busy) { (void)hipEventSynchronize(ev); (void)hipEventDestroy(ev); }
+        e.busy.clear();
+        e.buf.release();
+    }
+    // a buffer of at least `bytes` whose past users `stream` now waits for; false: none pooled
+    bool take(size_t bytes, hipStream_t stream, DevBuf& out) {
+        std::lock_guard<std::mutex> lk(mu);
+        for (size_t i = 0; i < free.size(); i++) {
+            if (free[i].buf.bytes < bytes) continue;
+            for (hipEvent_t ev : free[i].busy) {
+                (void)hipStreamWaitEvent(stream, ev, 0);
+                (void)hipEventDestroy(ev);   // released when the recorded work completes
+            }
+            out = free[i].buf;
+            free.erase(free.begin() + (long)i);
+            return true;
+        }
+        return false;
+    }
+    void give(DevBuf buf, std::vector<hipEvent_t> busy) {
+        Entry e{buf, std::move(busy)};
+        std::lock_guard<std::mutex> lk(mu);
+        if (closed || free.size() >= 4) { drain(e); return; }
+        free.push_back(std::move(e));
+    }
+    void close() {
+        std::lock_guard<std::mutex> lk(mu);
+        closed = true;
+        for (Entry& e : free) drain(e);
+        free.clear();
+    }
+};
+
 struct restir_frame {
     std::atomic<int> refs{1};
     int device = 0;
     DevBuf rec;   // the frame's reservoirs over its view: per-pixel records [n_t, a_0, b_0, ...] or [a planes | b planes]
     bool records = true;
     uint32_t W = 0, H = 0, vx0 = 0, vy0 = 0, vw = 0, vh = 0, N = 0;
+    std::shared_ptr<FramePool> pool;   // where rec goes back on release (the producing context's)
+    std::mutex mu;
+    hipEvent_t ready = nullptr;        // recorded on the producer's stream after its last kernel touching rec
+    std::vector<hipEvent_t> reads;     // recorded after each render that read this frame as its predecessor
 };
+
+namespace {
+hipEvent_t record_event(hipStream_t s) {
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (hipEventRecord(ev, s) != hipSuccess) { (void)hipEventDestroy(ev); return nullptr; }
+    return ev;
+}
+// a frame's records leave the producing context: remember where they go back to and when they are written
+restir_frame* make_frame(const std::shared_ptr<FramePool>& pool, int device, hipStream_t s) {
+    restir_frame* fr = new restir_frame();
+    fr->device = device;
+    fr->pool = pool;
+    fr->ready = record_event(s);
+    return fr;
+}
+// the consumer of a predecessor frame: its stream waits for the producer's kernels (another context / stream)
+restir_status use_prev(const restir_frame* prev, int device, hipStream_t s) {
+    if (prev->device != device)
+        return fail(RESTIR_ERR_INVALID, "temporal predecessor lives on device %d, this context on %d", prev->device, device);
+    if (prev->ready) HIP_TRY(hipStreamWaitEvent(s, prev->ready, 0));
+    return RESTIR_OK;
+}
+// ... and records that it read it, so the records are not recycled under the read
+void used_prev(const restir_frame* prev, hipStream_t s) {
+    restir_frame* fr = const_cast<restir_frame*>(prev);
+    hipEvent_t ev = record_event(s);
+    if (!ev) { (void)hipStreamSynchronize(s); return; }
+    std::lock_guard<std::mutex> lk(fr->mu);
+    fr->reads.push_back(ev);
+}
+}  // namespace
 
 struct restir_ctx {
     int device = 0;
@@ -122,6 +206,7 @@ struct restir_ctx {
     uint32_t vw = 0, vh = 0, N = 0;
     DevBuf n_t, p_mat, ra[2], rb[2], dbg[2], rgb;   // stage API: SoA planes
     DevBuf rec[2];                                  // restir_render / halo frames: per-pixel records
+    std::shared_ptr<FramePool> pool = std::make_shared<FramePool>();
     DevBuf rp[2];                                   // their target-pdf cache planes (N = 1, planes layout)
     int cur = 0;
     uint32_t rgb_w = 0, rgb_h = 0;
@@ -535,7 +620,12 @@ restir_status ensure_records(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N
     fb = FrameBufs{c, c->tuning.records != 0, npx, N};
     ST_TRY(c->p_mat.ensure(npx * 16));
     if (!fb.records) ST_TRY(c->n_t.ensure(npx * 16));
-    for (int i = 0; i < 2; i++) ST_TRY(c->rec[i].ensure(npx * (fb.records ? 1u + 2u * N : 2u * N) * 16));
+    const size_t rec_bytes = npx * (fb.records ? 1u + 2u * N : 2u * N) * 16;
+    for (int i = 0; i < 2; i++) {
+        // a buffer handed to a frame comes back through the pool (stream-ordered against its past users)
+        if (!c->rec[i].p && c->pool->take(rec_bytes, c->stream, c->rec[i])) continue;
+        ST_TRY(c->rec[i].ensure(rec_bytes));
+    }
     if (!fb.records && N == 1)
         for (int i = 0; i < 2; i++) ST_TRY(c->rp[i].ensure(npx * 4));
     c->vw = vw; c->vh = vh; c->N = N;
@@ -597,6 +687,7 @@ void restir_destroy(restir_ctx* c) {
             b->release();
         for (Pending& p : c->pending) { (void)hipEventDestroy(p.start); (void)hipEventDestroy(p.stop); }
         for (hipEvent_t ev : c->free_events) (void)hipEventDestroy(ev);
+        c->pool->close();   // frames still alive free their records themselves on release
         (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -854,12 +945,14 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
         if (has_ghost && passes > 0)
             return fail(RESTIR_ERR_UNSUPPORTED, "temporal reuse on a ghost-zoned tile needs the predecessor's ghost zone: "
                                                 "render such tiles with the halo-exchange stages (restir_halo_begin)");
+        if (prev->records != (c->tuning.records != 0))
+            return fail(RESTIR_ERR_INVALID, "temporal predecessor grid was rendered with the other buffer layout");
+        ST_TRY(use_prev(prev, c->device, c->stream));
     }
 
     FrameBufs fb;
     ST_TRY(ensure_records(c, t.gwidth, t.gheight, N, fb));
-    if (temporal && prev->records != fb.records)
-        return fail(RESTIR_ERR_INVALID, "temporal predecessor grid was rendered with the other buffer layout");
+    c->stage_ok = false;   // ensure_records re-sized the shared view state: the stage API must be reconfigured
     ST_TRY(c->rgb.ensure((size_t)t.width * t.height * 12));
     c->rgb_w = t.width; c->rgb_h = t.height;
 
@@ -885,6 +978,7 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
               launch_temporal(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0), camd.origin, fb.nt(cur), pm,
                               fb.ra(cur), fb.rb(cur), fb.pa(prev), fb.pb(prev), fb.ra(cur), fb.rb(cur), nullptr,
                               fb.rp(cur), fb.rp(cur), c->tuning, c->stream));
+        used_prev(prev, c->stream);
     }
     bool rp_ok = fb.rp(cur) != nullptr;   // the current grid's target-pdf cache holds its samples' pdfs
     for (uint32_t pass = 0; pass < passes; pass++) {
@@ -901,8 +995,7 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     c->cur = cur;
 
     if (out_next) {
-        restir_frame* fr = new restir_frame();
-        fr->device = c->device;
+        restir_frame* fr = make_frame(c->pool, c->device, c->stream);   // after the final kernel, the records' last reader
         fr->W = width; fr->H = height; fr->vx0 = t.gx0; fr->vy0 = t.gy0; fr->vw = t.gwidth; fr->vh = t.gheight; fr->N = N;
         // hand the final grid's records to the frame (no copy); the context re-allocates lazily
         std::swap(fr->rec, c->rec[cur]);
@@ -925,11 +1018,55 @@ restir_status restir_frame_retain(restir_frame* fr) {
 void restir_frame_release(restir_frame* fr) {
     if (!fr) return;
     if (fr->refs.fetch_sub(1) == 1) {
+        // stream-ordered: the records go back to the producing context's pool with the events of the work that
+        // touched them (the next user waits on those on its own stream); no device-wide synchronisation
         (void)hipSetDevice(fr->device);
-        (void)hipDeviceSynchronize();
-        fr->rec.release();
+        std::vector<hipEvent_t> busy = std::move(fr->reads);
+        if (fr->ready) busy.push_back(fr->ready);
+        if (fr->pool) {
+            fr->pool->give(fr->rec, std::move(busy));
+        } else {
+            FramePool::Entry e{fr->rec, std::move(busy)};
+            FramePool::drain(e);
+        }
+        fr->rec = DevBuf{};
         delete fr;
     }
+}
+
+restir_status restir_frame_info(const restir_frame* fr, uint32_t* width, uint32_t* height, uint32_t* vx0, uint32_t* vy0,
+                                uint32_t* vw, uint32_t* vh, uint32_t* n) {
+    if (!fr) return fail(RESTIR_ERR_INVALID, "frame is NULL");
+    if (width) *width = fr->W;
+    if (height) *height = fr->H;
+    if (vx0) *vx0 = fr->vx0;
+    if (vy0) *vy0 = fr->vy0;
+    if (vw) *vw = fr->vw;
+    if (vh) *vh = fr->vh;
+    if (n) *n = fr->N;
+    return RESTIR_OK;
+}
+
+restir_status restir_frame_download(const restir_frame* fr, float* pos, float* color, float* w, uint32_t* m) {
+    if (!fr) return fail(RESTIR_ERR_INVALID, "frame is NULL");
+    HIP_TRY(hipSetDevice(fr->device));
+    if (fr->ready) HIP_TRY(hipEventSynchronize(fr->ready));
+    const size_t npx = (size_t)fr->vw * fr->vh, N = fr->N;
+    // the records as stored: per pixel [n_t, a_0, b_0, a_1, b_1, ...] or planes [a_0 .. a_N-1 | b_0 .. b_N-1]
+    const size_t f4 = fr->records ? npx * (1 + 2 * N) : npx * 2 * N;
+    std::vector<float> host(4 * f4);
+    HIP_TRY(hipMemcpy(host.data(), fr->rec.p, host.size() * 4, hipMemcpyDeviceToHost));
+    for (size_t j = 0; j < N; j++)
+        for (size_t p = 0; p < npx; p++) {
+            const float* a = fr->records ? &host[4 * (p * (1 + 2 * N) + 1 + 2 * j)] : &host[4 * (j * npx + p)];
+            const float* b = fr->records ? &host[4 * (p * (1 + 2 * N) + 2 + 2 * j)] : &host[4 * ((N + j) * npx + p)];
+            const size_t i = j * npx + p;
+            if (pos) { pos[3 * i] = a[0]; pos[3 * i + 1] = a[1]; pos[3 * i + 2] = a[2]; }
+            if (w) w[i] = a[3];
+            if (color) { color[3 * i] = b[0]; color[3 * i + 1] = b[1]; color[3 * i + 2] = b[2]; }
+            if (m) std::memcpy(&m[i], &b[3], 4);
+        }
+    return RESTIR_OK;
 }
 
 restir_status restir_synchronize(restir_ctx* c) {
@@ -1252,21 +1389,32 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
     const uint32_t passes = features->spatial_reuse ? features->spatial_resampling_passes : 0u;
     restir_tile t{};
     ST_TRY(restir_tile_plan(width, height, tiles_x, tiles_y, rank, passes ? f.R : 0u, &t));
+    // plan into locals, validate everything, then commit to c->halo (a failure leaves no half-updated plan)
     restir_halo_segment sg[RESTIR_MAX_HALO_SEGS], rg_[RESTIR_MAX_HALO_SEGS];
-    uint32_t n = RESTIR_MAX_HALO_SEGS;
-    ST_TRY(restir_halo_plan(width, height, tiles_x, tiles_y, rank, f.R, f.N, sg, rg_, &n));
-    auto& h = c->halo;
-    ST_TRY(to_segs(sg, n, h.send, h.send_bytes));
-    ST_TRY(to_segs(rg_, n, h.recv, h.recv_bytes));
-    if (!passes) { h.send.n = h.recv.n = 0; h.send.px0[0] = h.recv.px0[0] = 0; h.send_bytes = h.recv_bytes = 0; }
+    uint32_t n = 0;
+    HaloSegs send{}, recv{};
+    uint64_t send_b = 0, recv_b = 0;
+    if (passes) {   // no spatial pass, no exchange: skip the plan (and its segment cap)
+        n = RESTIR_MAX_HALO_SEGS;
+        ST_TRY(restir_halo_plan(width, height, tiles_x, tiles_y, rank, f.R, f.N, sg, rg_, &n));
+        ST_TRY(to_segs(sg, n, send, send_b));
+        ST_TRY(to_segs(rg_, n, recv, recv_b));
+    }
     const bool temporal = features->temporal_reuse && prev != nullptr;
-    if (temporal && (prev->N != f.N || prev->vw != t.gwidth || prev->vh != t.gheight || prev->vx0 != t.gx0 ||
-                     prev->vy0 != t.gy0 || prev->W != width || prev->H != height))
-        return fail(RESTIR_ERR_INVALID, "temporal predecessor grid does not match this tile's view / N");
+    if (temporal) {
+        if (prev->N != f.N || prev->vw != t.gwidth || prev->vh != t.gheight || prev->vx0 != t.gx0 ||
+            prev->vy0 != t.gy0 || prev->W != width || prev->H != height)
+            return fail(RESTIR_ERR_INVALID, "temporal predecessor grid does not match this tile's view / N");
+        if (prev->records != (c->tuning.records != 0))
+            return fail(RESTIR_ERR_INVALID, "temporal predecessor grid was rendered with the other buffer layout");
+        ST_TRY(use_prev(prev, c->device, c->stream));
+    }
+    auto& h = c->halo;
+    h.active = false;
     FrameBufs fb;
     ST_TRY(ensure_records(c, t.gwidth, t.gheight, f.N, fb));
-    if (temporal && prev->records != fb.records)
-        return fail(RESTIR_ERR_INVALID, "temporal predecessor grid was rendered with the other buffer layout");
+    c->stage_ok = false;
+    h.send = send; h.recv = recv; h.send_bytes = send_b; h.recv_bytes = recv_b;
     ST_TRY(c->rgb.ensure((size_t)t.width * t.height * 12));
     c->rgb_w = t.width; c->rgb_h = t.height;
     h.W = width; h.H = height;
@@ -1291,6 +1439,7 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
               launch_temporal(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_TEMPORAL, 0), h.camd.origin, fb.nt(0),
                               pm, fb.ra(0), fb.rb(0), fb.pa(prev), fb.pb(prev), fb.ra(0), fb.rb(0), nullptr, fb.rp(0),
                               fb.rp(0), c->tuning, c->stream));
+    if (temporal) used_prev(prev, c->stream);
     h.rp_ok = fb.rp(0) != nullptr;
     h.active = true;
     if (send_bytes) *send_bytes = h.send_bytes;
@@ -1366,8 +1515,7 @@ restir_status restir_halo_end(restir_ctx* c, restir_frame** out_next, float* out
     c->cur = h.cur;
     h.active = false;
     if (out_next) {
-        restir_frame* fr = new restir_frame();
-        fr->device = c->device;
+        restir_frame* fr = make_frame(c->pool, c->device, c->stream);
         fr->W = h.W; fr->H = h.H; fr->vx0 = h.view.vx0; fr->vy0 = h.view.vy0; fr->vw = h.view.vw; fr->vh = h.view.vh;
         fr->N = h.f.N;
         std::swap(fr->rec, c->rec[h.cur]);

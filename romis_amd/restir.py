@@ -29,6 +29,26 @@ class ReservoirGrid:
             self._lib.restir_frame_release(self.handle)
             self.handle = None
 
+    def info(self) -> dict:
+        """(W, H) of the image and the (vx0, vy0, vw, vh) view the grid covers, N sub-reservoirs per pixel."""
+        v = [C.c_uint32() for _ in range(7)]
+        check(self._lib, self._lib.restir_frame_info(self.handle, *[C.byref(x) for x in v]), "restir_frame_info")
+        return dict(zip(("W", "H", "vx0", "vy0", "vw", "vh", "N"), (x.value for x in v)))
+
+    def download(self):
+        """The grid's (pos [N][vh][vw][3], color [N][vh][vw][3], W [N][vh][vw], M [N][vh][vw] uint32), rows y = 0
+        bottom -- the per-pixel Reservoir state renderReSTIR returns (render.cpp:61)."""
+        i = self.info()
+        n = i["N"] * i["vh"] * i["vw"]
+        pos, col = np.zeros((n, 3), np.float32), np.zeros((n, 3), np.float32)
+        w, m = np.zeros(n, np.float32), np.zeros(n, np.uint32)
+        FP, UP = C.POINTER(C.c_float), C.POINTER(C.c_uint32)
+        check(self._lib, self._lib.restir_frame_download(self.handle, pos.ctypes.data_as(FP), col.ctypes.data_as(FP),
+                                                         w.ctypes.data_as(FP), m.ctypes.data_as(UP)),
+              "restir_frame_download")
+        shp = (i["N"], i["vh"], i["vw"])
+        return pos.reshape(shp + (3,)), col.reshape(shp + (3,)), w.reshape(shp), m.reshape(shp)
+
 
 class Renderer:
     def __init__(self, device: int = 0):

@@ -9,58 +9,15 @@
 // scene.bin (little endian): u32 num_meshes; per mesh: u32 V, u32 T, f32[3V] positions, f32[3V] normals,
 // u32[3T] triangles, f32[8] material (kd3 ks3 shininess transparency); u32 num_lights, restir_light[L];
 // f32[9] camera (fovy aspect lookAt3 distance rotation3).
-#include <romis_amd/restir.hpp>
+#include "scene_io.h"
 
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
 #include <vector>
-
-template <class T>
-static void rd(FILE* f, T* p, size_t n) {
-    if (n && std::fread(p, sizeof(T), n, f) != n) { std::fprintf(stderr, "short read\n"); std::exit(2); }
-}
 
 int main(int argc, char** argv) {
     if (argc < 9) { std::fprintf(stderr, "usage: %s scene.bin out.rgb W H frames N passes temporal\n", argv[0]); return 2; }
     const int W = std::atoi(argv[3]), H = std::atoi(argv[4]), frames = std::atoi(argv[5]);
-    FILE* f = std::fopen(argv[1], "rb");
-    if (!f) { std::perror("scene"); return 2; }
-    romis::Scene scene;
-    uint32_t nm = 0;
-    rd(f, &nm, 1);
-    scene.meshes.resize(nm);
-    for (auto& m : scene.meshes) {
-        uint32_t V = 0, T = 0;
-        rd(f, &V, 1);
-        rd(f, &T, 1);
-        m.positions.resize(3 * size_t(V));
-        m.normals.resize(3 * size_t(V));
-        m.triangles.resize(3 * size_t(T));
-        rd(f, m.positions.data(), m.positions.size());
-        rd(f, m.normals.data(), m.normals.size());
-        rd(f, m.triangles.data(), m.triangles.size());
-        float mat[8];
-        rd(f, mat, 8);
-        std::memcpy(m.material.kd, mat, 12);
-        std::memcpy(m.material.ks, mat + 3, 12);
-        m.material.shininess = mat[6];
-        m.material.transparency = mat[7];
-    }
-    uint32_t nl = 0;
-    rd(f, &nl, 1);
-    scene.lights.resize(nl);
-    rd(f, scene.lights.data(), nl);
-    float cam[9];
-    rd(f, cam, 9);
-    std::fclose(f);
-
     romis::Camera camera;
-    camera.fovy = cam[0];
-    camera.aspect = cam[1];
-    std::memcpy(camera.look_at, cam + 2, 12);
-    camera.distance = cam[5];
-    std::memcpy(camera.rotation, cam + 6, 12);
+    romis::Scene scene = read_scene(argv[1], &camera);
 
     romis::Features features;
     features.num_samples_in_reservoir = uint32_t(std::atoi(argv[6]));

@@ -311,6 +311,20 @@ def test_device_math_matches_oracle(gpu, oracle):
     assert_bits(ex, want_ex, "expf")
 
 
+def assert_grid(grid, res, what):
+    """The device grid renderReSTIR returns (restir_frame_download) == the oracle's reservoirs: selected light
+    sample (position, colour), W and M of every sub-reservoir of every pixel, bit for bit."""
+    a, b = res
+    pos, col, w, m = grid.download()
+    N, vh, vw = w.shape
+    a = a.reshape(N, vh, vw, 4)
+    b = b.reshape(N, vh, vw, 4)
+    assert_bits(pos, np.ascontiguousarray(a[..., :3]), f"{what} grid position")
+    assert_bits(w, np.ascontiguousarray(a[..., 3]), f"{what} grid W")
+    assert_bits(col, np.ascontiguousarray(b[..., :3]), f"{what} grid colour")
+    assert np.array_equal(m, np.ascontiguousarray(b[..., 3]).view(np.uint32)), f"{what} grid M"
+
+
 # --------------------------------------------------------------------------------------------------------
 # whole frames through restir_render (renderReSTIR)
 # the BASELINE.json configs at parity-test size: C1 (RIS only), C2, the 512-parallelogram nightclub, C4 (1024
@@ -328,9 +342,10 @@ def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased, M, 
                               spatial_reuse_visibility_check=vis)
     gpu.set_seed(SEED, 0)
     rgb, grid = gpu.render_restir(None, cam, W, H, f)
-    want, _, _ = oracle.render_frame(osc, cam, f, W, H, SEED, 0)
+    want, res, _ = oracle.render_frame(osc, cam, f, W, H, SEED, 0)
     np.testing.assert_allclose(rgb, want, rtol=1e-5, atol=1e-7)
     assert_bits(rgb, want, "rgb")
+    assert_grid(grid, res, name)
 
 
 @pytest.mark.parametrize("w,h,N,passes,M", [(1, 1, 1, 2, 32), (37, 23, 2, 2, 32), (33, 9, 1, 1, 1), (40, 24, 32, 1, 8),
@@ -351,6 +366,7 @@ def test_odd_sizes_and_extremes_match_oracle(gpu, oracle, w, h, N, passes, M):
         rgb, grid = gpu.render_restir(prev_gpu, cam, w, h, f)
         want, res, _ = oracle.render_frame(osc, cam, f, w, h, SEED, frame, prev=prev_or)
         assert_bits(rgb, want, f"{w}x{h} N={N} frame {frame}")
+        assert_grid(grid, res, f"{w}x{h} N={N} frame {frame}")
         prev_gpu, prev_or = grid, res
 
 
@@ -378,6 +394,7 @@ def _temporal_sequence(gpu, oracle):
         rgb, grid = gpu.render_restir(prev_gpu, cam, W, H, f)
         want, res, _ = oracle.render_frame(osc, cam, f, W, H, SEED, frame, prev=prev_or)
         assert_bits(rgb, want, f"frame {frame} rgb")
+        assert_grid(grid, res, f"frame {frame}")
         prev_gpu, prev_or = grid, res
 
 
@@ -491,3 +508,49 @@ def test_errors_are_reported(gpu):
         gpu.render_restir(None, cam, W, H, _abi.default_features(ray_trace_mode=7))
     with pytest.raises(RestirError, match="INVALID"):
         gpu.render_restir(None, cam, W, H, _abi.default_features(num_samples_in_reservoir=0))
+
+
+def test_render_invalidates_stage_state(gpu, oracle):
+    """A frame render re-sizes the context's shared view state: the stage API reports RESTIR_ERR_STATE until
+    restir_stage_configure runs again, instead of copying with the frame's sizes (advisor finding)."""
+    from romis_amd._abi import RestirError
+    name = "nightclub_128pt"
+    _, osc, cam = setup(gpu, oracle, name, 1)
+    gpu.stage_configure(W, H, 1)
+    big = scene.camera_for(name, 2 * W, 2 * H)
+    gpu.render_restir(None, big, 2 * W, 2 * H, _abi.default_features(num_samples_in_reservoir=1, temporal_reuse=0))
+    with pytest.raises(RestirError, match="STATE"):
+        gpu.download(_abi.BUF_RES_A)
+
+
+def test_temporal_frames_recycle_records(gpu, oracle):
+    """Released temporal frames hand their records back to the context (stream-ordered): a long sequence whose
+    predecessors are dropped as it goes stays bit-exact, and a predecessor read by a second context (its own
+    stream) is waited for, not raced."""
+    from romis_amd import restir
+    name = "nightclub_128pt"
+    s = get_scene(name)
+    gpu.set_scene(s)
+    osc = oracle.OracleScene(s)
+    cam = scene.camera_for(name, W, H)
+    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=1, temporal_reuse=1)
+    gpu.set_seed(SEED, 0)
+    other = restir.Renderer(0)
+    try:
+        other.set_scene(s)
+        prev_gpu, prev_or = None, None
+        for frame in range(6):
+            rgb, grid = gpu.render_restir(prev_gpu, cam, W, H, f, want_rgb=frame % 2 == 1)
+            _, res, _ = oracle.render_frame(osc, cam, f, W, H, SEED, frame, prev=prev_or)
+            if frame % 2 == 1:
+                assert_grid(grid, res, f"frame {frame}")
+            # the second context renders its frame `frame + 1` from this grid before the first context's
+            # stream has necessarily finished writing it
+            other.set_seed(SEED, frame + 1)
+            rgb2, grid2 = other.render_restir(grid, cam, W, H, f)
+            want2, res2, _ = oracle.render_frame(osc, cam, f, W, H, SEED, frame + 1, prev=res)
+            assert_bits(rgb2, want2, f"second context frame {frame + 1}")
+            del grid2
+            prev_gpu, prev_or = grid, res   # the previous predecessor is released here
+    finally:
+        other.close()

@@ -46,7 +46,8 @@
 extern "C" {
 #endif
 
-#define RESTIR_ABI_VERSION 2   /* 2: restir_features gained the R-MIS / R-OMIS fields */
+#define RESTIR_ABI_VERSION 3   /* 2: restir_features gained the R-MIS / R-OMIS fields;
+                                  3: textures (restir_texture, restir_material.kd_texture, restir_mesh.texcoords) */
 
 #define RESTIR_STAGE_RIS      1u
 #define RESTIR_STAGE_TEMPORAL 2u
@@ -89,12 +90,21 @@ typedef struct restir_light {
     float c3[3];   /*                                    | Parallelogram.color3 */
 } restir_light;
 
-/* Material (framework/include/framework/mesh.h:22-34); kdTexture is not carried. */
+/* Image (framework/include/framework/image.h): width x height texels, row-major [y][x] with y = 0 the image
+ * file's first row (Image::pixels order), each texel the stb RGB bytes / 255.0f (image.cpp:22-31). */
+typedef struct restir_texture {
+    uint32_t     width, height;
+    const float* rgb;              /* [height][width][3] */
+} restir_texture;
+
+/* Material (framework/include/framework/mesh.h:22-34).  kd_texture = Material::kdTexture: 0 = none, else
+ * 1 + an index into restir_set_scene_textured's textures (several materials may share one Image). */
 typedef struct restir_material {
-    float kd[3];
-    float ks[3];
-    float shininess;
-    float transparency;
+    float    kd[3];
+    float    ks[3];
+    float    shininess;
+    float    transparency;
+    uint32_t kd_texture;
 } restir_material;
 
 /* Mesh (mesh.h:36-43): one material per mesh, like loadMesh's per-material sub-meshes. */
@@ -105,6 +115,7 @@ typedef struct restir_mesh {
     const uint32_t* triangles;     /* [num_triangles][3] vertex indices */
     uint32_t        num_triangles;
     restir_material material;
+    const float*    texcoords;     /* [num_vertices][2] Vertex::texCoord; NULL = (0, 0) (loadMesh's default) */
 } restir_mesh;
 
 /* Trackball state (framework/include/framework/trackball.h:13-66) as set by Trackball(window, fovy, dist)
@@ -139,7 +150,7 @@ typedef struct restir_features {
     uint8_t  spatial_reuse_visibility_check;
     uint8_t  temporal_reuse;
     uint8_t  enable_shading;
-    uint8_t  enable_texture_mapping;         /* accepted; textures are not carried (no effect) */
+    uint8_t  enable_texture_mapping;         /* diffuseAlbedo's switch (utils.cpp:33-37) */
     uint8_t  enable_tone_mapping;
     float    gamma;
     float    exposure;
@@ -214,6 +225,14 @@ restir_status restir_set_seed(restir_ctx* ctx, uint32_t seed, uint32_t frame_ind
  * EmbreeInterface(scene), embree_interface.cpp:14-51). */
 restir_status restir_set_scene(restir_ctx* ctx, const restir_mesh* meshes, uint32_t num_meshes,
                                const restir_light* lights, uint32_t num_lights);
+/* The same with the Images textured materials point at (diffuseAlbedo's kdTexture, utils.cpp:33-37): with
+ * features->enable_texture_mapping (the Features default, common.h:95) a textured material's diffuse colour
+ * is acquireTexel(kdTexture, the hit's interpolated texCoord) (texture.cpp:4-9, embree_interface.cpp:80-81).
+ * Texture coordinates outside [0, 1] read out of bounds in the reference (its float -> size_t conversion);
+ * here they clamp to the edge texel. */
+restir_status restir_set_scene_textured(restir_ctx* ctx, const restir_mesh* meshes, uint32_t num_meshes,
+                                        const restir_light* lights, uint32_t num_lights,
+                                        const restir_texture* textures, uint32_t num_textures);
 
 /* renderRayTraced (render.cpp:268-290) by features->ray_trace_mode:
  * RMIS / ROMIS -- renderRMIS / renderROMIS (render.cpp:64-265): primary hits -> neighbour selection grid ->
@@ -255,7 +274,8 @@ restir_status restir_download_rgb(restir_ctx* ctx, float* out_rgb, size_t count)
  * (row-major, y = 0 bottom), and for reservoirs [N][pixels]:
  *   gbuf_n_t   : float4 (N.xyz, t)         gbuf_p_mat : float4 (P.xyz, bits(material index))
  *   res_a      : float4 (light pos.xyz, W) res_b      : float4 (light colour.xyz, bits(M))
- *   res_dbg    : float2 (wSum, chosenSampleWeight)                                                   */
+ *   res_dbg    : float2 (wSum, chosenSampleWeight)
+ *   gbuf_uv    : float2 (the hit's interpolated texCoord; written and read only for scenes with textures) */
 typedef enum restir_buffer {
     RESTIR_BUF_GBUF_N_T   = 0,   /* read by the spatial heuristic for every neighbour: keep it compact */
     RESTIR_BUF_GBUF_P_MAT = 1,
@@ -274,7 +294,8 @@ typedef enum restir_buffer {
      *             i in row T*T + c*T + i), progressive alphas (3*T rows after b, same order), progressive colour
      *             (3 rows) */
     RESTIR_BUF_MIS_NBR    = 9,
-    RESTIR_BUF_MIS_ACC    = 10
+    RESTIR_BUF_MIS_ACC    = 10,
+    RESTIR_BUF_GBUF_UV    = 11
 } restir_buffer;
 #define RESTIR_ROMIS_MAX_TECHNIQUES 8u   /* k + 1 distributions per pixel (the technique matrix lives in registers) */
 

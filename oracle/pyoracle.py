@@ -41,6 +41,11 @@ def lib() -> C.CDLL:
         sig = {
             "or_scene_create": (P, [C.POINTER(_abi.Mesh), u32, C.POINTER(_abi.Light), u32]),
             "or_scene_destroy": (None, [P]),
+            "or_scene_create_textured": (P, [C.POINTER(_abi.Mesh), u32, C.POINTER(_abi.Light), u32,
+                                             C.POINTER(_abi.Texture), u32]),
+            "or_scene_bind_uv": (None, [P, FP]),
+            "or_acquire_texel": (None, [P, u32, FP, FP]),
+            "or_primary_uv": (None, [P, C.POINTER(_abi.CameraFrame), u32, u32, Rect, Rect, FP, FP, FP]),
             "or_scene_num_triangles": (u32, [P]),
             "or_scene_miss_material": (u32, [P]),
             "or_rng_key": (u32, [u32, u32, u32, u32]),
@@ -91,10 +96,18 @@ def fp(a: np.ndarray | None):
 class OracleScene:
     def __init__(self, scene):
         meshes, nm, lights, nl, keep = scene.to_abi()
-        self._keep = (meshes, lights, keep)
-        self.handle = lib().or_scene_create(meshes, nm, lights, nl)
+        texs, ntex, tkeep = scene.textures_abi()
+        self._keep = (meshes, lights, keep, texs, tkeep)
+        self.handle = lib().or_scene_create_textured(meshes, nm, lights, nl, texs, ntex)
         self.num_lights = nl
+        self.num_textures = ntex
         self.miss_material = lib().or_scene_miss_material(self.handle)
+        self.uv = None   # the bound G-buffer texCoord plane (textured scenes; set by gbuffer / bind_uv)
+
+    def bind_uv(self, uv: np.ndarray | None) -> None:
+        """The texCoord plane ([pixels][2], like n_t / p_mat) the following stage calls read."""
+        self.uv = None if uv is None else np.ascontiguousarray(uv, np.float32)
+        lib().or_scene_bind_uv(self.handle, fp(self.uv))
 
     def __del__(self):
         if getattr(self, "handle", None):
@@ -113,12 +126,24 @@ def full_rect(W, H) -> Rect:
 
 
 def gbuffer(osc: OracleScene, cam: _abi.Camera, W: int, H: int, view: Rect | None = None):
+    """(n_t, p_mat) of genPrimaryRayHits; for textured scenes the texCoord plane is bound to `osc` (osc.uv) for
+    the stage calls that follow."""
     view = view or full_rect(W, H)
     n = view.w * view.h
     n_t = np.zeros((n, 4), np.float32)
     p_mat = np.zeros((n, 4), np.float32)
-    lib().or_primary(osc.handle, C.byref(camera_frame(cam)), W, H, view, view, fp(n_t), fp(p_mat))
+    uv = np.zeros((n, 2), np.float32) if osc.num_textures else None
+    lib().or_primary_uv(osc.handle, C.byref(camera_frame(cam)), W, H, view, view, fp(n_t), fp(p_mat), fp(uv))
+    if osc.num_textures:
+        osc.bind_uv(uv)
     return n_t, p_mat
+
+
+def acquire_texel(osc: OracleScene, texture: int, tc) -> np.ndarray:
+    out = np.zeros(3, np.float32)
+    t = np.ascontiguousarray(tc, np.float32)
+    lib().or_acquire_texel(osc.handle, texture, fp(t), fp(out))
+    return out
 
 
 def empty_reservoirs(N: int, npx: int):

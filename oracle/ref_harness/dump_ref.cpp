@@ -6,17 +6,25 @@
 //              incl. tinyobj triangulation and centerAndScaleToUnitMesh :150-175) + light lists
 //              (regularLightGrid scene.cpp:5-28, constructNightClubLights :30-66)
 //   tonemap  : exposureToneMapping (src/post_processing/tone_mapping.cpp:8-11)
+//   textures : the Image a textured material carries (framework/src/image.cpp:13-34: stb RGB bytes / 255.0f),
+//              as its bytes (the harness checks every texel is exactly byte / 255.0f), and acquireTexel
+//              (src/scene/texture.cpp:4-9) on deterministic and edge texture coordinates
 //   glm      : the vendored glm 0.9.9.9 primitives the hot path uses (normalize, dot, length, distance, cross,
 //              mix, quat(euler) * v) on deterministic inputs, so the C restatement's operation order is pinned.
 //
 // Floats are written as their IEEE-754 bit patterns (uint32) so the fixtures are bit-exact.
 #include <scene/scene.h>
+#include <scene/texture.h>
 #include <post_processing/tone_mapping.h>
+#include <framework/image.h>
 
 #include <glm/glm.hpp>
 #include <glm/gtc/quaternion.hpp>
 
+#include <cmath>
 #include <cstdint>
+#include <cstdlib>
+#include <vector>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -42,8 +50,24 @@ static void dumpScene(FILE* o, SceneType type, const char* name, const std::file
         if (m) std::fprintf(o, ",");
         std::fprintf(o, "{\"kd\":"); pv3(o, mesh.material.kd);
         std::fprintf(o, ",\"ks\":"); pv3(o, mesh.material.ks);
-        std::fprintf(o, ",\"shininess\":%u,\"transparency\":%u,\"textured\":%d,\"vertices\":[",
+        std::fprintf(o, ",\"shininess\":%u,\"transparency\":%u,\"textured\":%d,",
                      fb(mesh.material.shininess), fb(mesh.material.transparency), mesh.material.kdTexture ? 1 : 0);
+        if (mesh.material.kdTexture) {
+            const Image& img = *mesh.material.kdTexture;
+            std::fprintf(o, "\"texture\":{\"width\":%d,\"height\":%d,\"rgb_u8\":\"", img.width, img.height);
+            for (const glm::vec3& px : img.pixels)
+                for (int c = 0; c < 3; c++) {
+                    const float v = px[c];
+                    const int b = (int)(v * 255.0f + 0.5f);
+                    if (b < 0 || b > 255 || fb((float)b / 255.0f) != fb(v)) {
+                        std::fprintf(stderr, "texel %a is not a byte / 255.0f\n", (double)v);
+                        std::exit(1);
+                    }
+                    std::fprintf(o, "%02x", b);
+                }
+            std::fprintf(o, "\"},");
+        }
+        std::fprintf(o, "\"vertices\":[");
         for (size_t v = 0; v < mesh.vertices.size(); v++) {
             if (v) std::fprintf(o, ",");
             std::fprintf(o, "[");
@@ -91,6 +115,7 @@ int main(int argc, char** argv) {
     std::fprintf(o, "{\"scenes\":{");
     dumpScene(o, SceneType::SingleTriangle, "SingleTriangle", dataDir);               std::fprintf(o, ",");
     dumpScene(o, SceneType::Cube, "Cube", dataDir);                                   std::fprintf(o, ",");
+    dumpScene(o, SceneType::CubeTextured, "CubeTextured", dataDir);                   std::fprintf(o, ",");
     dumpScene(o, SceneType::CornellBox, "CornellBox", dataDir);                       std::fprintf(o, ",");
     dumpScene(o, SceneType::CornellBoxParallelogramLight, "CornellBoxParallelogramLight", dataDir); std::fprintf(o, ",");
     dumpScene(o, SceneType::CornellNightClub, "CornellNightClub", dataDir);           std::fprintf(o, ",");
@@ -109,6 +134,30 @@ int main(int argc, char** argv) {
             if (i) std::fprintf(o, ",");
             std::fprintf(o, "["); pv3(o, grid[i].v0); std::fprintf(o, ","); pv3(o, grid[i].edge01);
             std::fprintf(o, ","); pv3(o, grid[i].edge02); std::fprintf(o, "]");
+        }
+        std::fprintf(o, "]},");
+    }
+
+    // acquireTexel on the CubeTextured texture: random coordinates in [0, 1], the edges, the texture's vertex
+    // coordinates and coordinates just below the texel boundaries (the float -> size_t truncation).
+    {
+        Scene cube = loadScenePrebuilt(SceneType::CubeTextured, dataDir);
+        const Image& img = *cube.meshes.at(0).material.kdTexture;
+        Features f{};
+        std::vector<glm::vec2> tc;
+        for (int i = 0; i < 512; i++) tc.push_back(glm::vec2(frand(0.0f, 1.0f), frand(0.0f, 1.0f)));
+        for (float a : {0.0f, 1.0f, 0.5f, 0.125f, 0.375f, 0.625f, 0.875f, 0.99999994f, 1e-7f})
+            for (float b : {0.0f, 1.0f, 0.25f, 0.75f, 0.99999994f}) tc.push_back(glm::vec2(a, b));
+        for (int k = 1; k < 127; k += 7) {
+            const float edge = (float)k / (float)(img.width - 1);
+            tc.push_back(glm::vec2(edge, edge));
+            tc.push_back(glm::vec2(std::nextafter(edge, 0.0f), std::nextafter(edge, 1.0f)));
+        }
+        std::fprintf(o, "\"texel\":{\"scene\":\"CubeTextured\",\"cases\":[");
+        for (size_t i = 0; i < tc.size(); i++) {
+            const glm::vec3 t = acquireTexel(img, tc[i], f);
+            if (i) std::fprintf(o, ",");
+            std::fprintf(o, "["); pv2(o, tc[i]); std::fprintf(o, ","); pv3(o, t); std::fprintf(o, "]");
         }
         std::fprintf(o, "]},");
     }

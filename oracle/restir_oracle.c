@@ -93,11 +93,29 @@ struct or_scene {
     uint32_t num_materials;   /* including the miss material at the end */
     restir_light* lights;
     uint32_t num_lights;
+    /* textures (Material::kdTexture images) and per-triangle texture coordinates t0, t1, t2 ([T][2] each) */
+    uint32_t num_textures;
+    uint32_t* tex_w; uint32_t* tex_h;
+    float** tex_rgb;
+    float* tc0; float* tc1; float* tc2;
+    /* the G-buffer's texCoord plane of the following stage calls (or_scene_bind_uv), indexed like n_t / p_mat */
+    const float* uv;
 };
 
-or_scene* or_scene_create(const restir_mesh* meshes, uint32_t num_meshes, const restir_light* lights,
-                          uint32_t num_lights) {
+or_scene* or_scene_create_textured(const restir_mesh* meshes, uint32_t num_meshes, const restir_light* lights,
+                                   uint32_t num_lights, const restir_texture* textures, uint32_t num_textures) {
     or_scene* s = (or_scene*)calloc(1, sizeof(or_scene));
+    s->num_textures = num_textures;
+    s->tex_w = (uint32_t*)calloc(num_textures ? num_textures : 1, 4);
+    s->tex_h = (uint32_t*)calloc(num_textures ? num_textures : 1, 4);
+    s->tex_rgb = (float**)calloc(num_textures ? num_textures : 1, sizeof(float*));
+    for (uint32_t i = 0; i < num_textures; i++) {
+        const size_t n = (size_t)textures[i].width * textures[i].height * 3;
+        s->tex_w[i] = textures[i].width;
+        s->tex_h[i] = textures[i].height;
+        s->tex_rgb[i] = (float*)malloc((n ? n : 1) * 4);
+        if (n) memcpy(s->tex_rgb[i], textures[i].rgb, n * 4);
+    }
     uint32_t T = 0;
     for (uint32_t m = 0; m < num_meshes; m++) T += meshes[m].num_triangles;
     s->num_tris = T;
@@ -105,6 +123,8 @@ or_scene* or_scene_create(const restir_mesh* meshes, uint32_t num_meshes, const 
     s->v0 = (float*)malloc(n3 * 4); s->e1 = (float*)malloc(n3 * 4); s->e2 = (float*)malloc(n3 * 4);
     s->n0 = (float*)malloc(n3 * 4); s->n1 = (float*)malloc(n3 * 4); s->n2 = (float*)malloc(n3 * 4);
     s->mat = (uint32_t*)malloc((T ? T : 1) * 4);
+    size_t n2 = (size_t)(T ? T : 1) * 2;
+    s->tc0 = (float*)calloc(n2, 4); s->tc1 = (float*)calloc(n2, 4); s->tc2 = (float*)calloc(n2, 4);
     s->num_materials = num_meshes + 1;
     s->materials = (restir_material*)calloc(s->num_materials, sizeof(restir_material));
     uint32_t t = 0;
@@ -121,6 +141,12 @@ or_scene* or_scene_create(const restir_mesh* meshes, uint32_t num_meshes, const 
             st3(&s->n0[3 * t], ld3(&mesh->normals[3 * tri[0]]));
             st3(&s->n1[3 * t], ld3(&mesh->normals[3 * tri[1]]));
             st3(&s->n2[3 * t], ld3(&mesh->normals[3 * tri[2]]));
+            if (mesh->texcoords)
+                for (int k = 0; k < 2; k++) {
+                    s->tc0[2 * t + k] = mesh->texcoords[2 * tri[0] + k];
+                    s->tc1[2 * t + k] = mesh->texcoords[2 * tri[1] + k];
+                    s->tc2[2 * t + k] = mesh->texcoords[2 * tri[2] + k];
+                }
             s->mat[t] = m;
         }
     }
@@ -136,8 +162,17 @@ or_scene* or_scene_create(const restir_mesh* meshes, uint32_t num_meshes, const 
     return s;
 }
 
+or_scene* or_scene_create(const restir_mesh* meshes, uint32_t num_meshes, const restir_light* lights,
+                          uint32_t num_lights) {
+    return or_scene_create_textured(meshes, num_meshes, lights, num_lights, NULL, 0);
+}
+
+void or_scene_bind_uv(or_scene* s, const float* uv) { s->uv = uv; }
+
 void or_scene_destroy(or_scene* s) {
     if (!s) return;
+    for (uint32_t i = 0; i < s->num_textures; i++) free(s->tex_rgb[i]);
+    free(s->tex_w); free(s->tex_h); free(s->tex_rgb); free(s->tc0); free(s->tc1); free(s->tc2);
     free(s->v0); free(s->e1); free(s->e2); free(s->n0); free(s->n1); free(s->n2); free(s->mat);
     free(s->materials); free(s->lights); free(s);
 }
@@ -224,8 +259,8 @@ static v3 camera_dir(const restir_camera_frame* cam, uint32_t x, uint32_t y, uin
 
 /* genPrimaryRayHits (render_utils.cpp:13-34) with closestHit's attribute interpolation
  * (embree_interface.cpp:64-90; rtcInterpolate0 restated as (1-u-v) a0 + u a1 + v a2, UNPINNED). */
-void or_primary(const or_scene* s, const restir_camera_frame* cam, uint32_t W, uint32_t H, or_rect view,
-                or_rect rect, float* n_t, float* p_mat) {
+void or_primary_uv(const or_scene* s, const restir_camera_frame* cam, uint32_t W, uint32_t H, or_rect view,
+                   or_rect rect, float* n_t, float* p_mat, float* uv) {
     v3 o = ld3(cam->origin);
 #pragma omp parallel for schedule(guided)
     for (int yy = 0; yy < (int)rect.h; yy++) {
@@ -236,11 +271,16 @@ void or_primary(const or_scene* s, const restir_camera_frame* cam, uint32_t W, u
             float t = FLT_MAX, u = 0.0f, v = 0.0f;
             uint32_t tri = 0;
             v3 n = mk(0.0f, 0.0f, 0.0f);
+            float tc[2] = {0.0f, 0.0f};   /* a miss keeps the value-initialised HitInfo::texCoord */
             uint32_t m = s->num_materials - 1;
             if (closest_hit(s, o, d, &t, &u, &v, &tri)) {
                 float w0 = (1.0f - u) - v;
                 n = vadd(vadd(vscale(ld3(&s->n0[3 * tri]), w0), vscale(ld3(&s->n1[3 * tri]), u)),
                          vscale(ld3(&s->n2[3 * tri]), v));
+                /* texCoord: rtcInterpolate0 of vertex attribute slot 1 (embree_interface.cpp:80-81), the same
+                 * (1-u-v) t0 + u t1 + v t2 form as the normal */
+                for (int k = 0; k < 2; k++)
+                    tc[k] = (s->tc0[2 * tri + k] * w0 + s->tc1[2 * tri + k] * u) + s->tc2[2 * tri + k] * v;
                 m = s->mat[tri];
             } else {
                 t = FLT_MAX;
@@ -248,8 +288,33 @@ void or_primary(const or_scene* s, const restir_camera_frame* cam, uint32_t W, u
             v3 P = vadd(o, vscale(d, t));   /* ray.origin + (ray.t * ray.direction) */
             n_t[4 * p + 0] = n.x; n_t[4 * p + 1] = n.y; n_t[4 * p + 2] = n.z; n_t[4 * p + 3] = t;
             p_mat[4 * p + 0] = P.x; p_mat[4 * p + 1] = P.y; p_mat[4 * p + 2] = P.z; p_mat[4 * p + 3] = u2f(m);
+            if (uv) { uv[2 * p] = tc[0]; uv[2 * p + 1] = tc[1]; }
         }
     }
+}
+
+void or_primary(const or_scene* s, const restir_camera_frame* cam, uint32_t W, uint32_t H, or_rect view,
+                or_rect rect, float* n_t, float* p_mat) {
+    or_primary_uv(s, cam, W, H, view, rect, n_t, p_mat, NULL);
+}
+
+/* acquireTexel (texture.cpp:4-9): size_t discreteX = texCoord.x * (width - 1) -- the float product truncated
+ * toward zero -- and memoryLoc = discreteY * width + discreteX into the row-major pixels.  Products outside
+ * [0, width - 1] read out of bounds in the reference (UB); they clamp to the edge texel here. */
+static inline uint32_t texel_index(float c, uint32_t n) {
+    float v = c * (float)((int)n - 1);
+    if (!(v >= 0.0f)) return 0u;
+    if (v >= (float)(n - 1)) return n - 1;
+    return (uint32_t)v;
+}
+static const float* acquire_texel(const or_scene* s, uint32_t tex, const float* tc) {
+    uint32_t w = s->tex_w[tex], h = s->tex_h[tex];
+    size_t loc = (size_t)texel_index(tc[1], h) * w + texel_index(tc[0], w);
+    return &s->tex_rgb[tex][3 * loc];
+}
+void or_acquire_texel(const or_scene* s, uint32_t tex, const float tc[2], float out[3]) {
+    const float* t = acquire_texel(s, tex, tc);
+    out[0] = t[0]; out[1] = t[1]; out[2] = t[2];
 }
 
 /* ------------------------------------------------------------------------------------------------------ */
@@ -258,6 +323,7 @@ typedef struct {
     v3 P, N, V;      /* V = normalize(o - P) is light-independent (hoisted; same bits) */
     const restir_material* mat;
     float t;
+    const float* texel;   /* acquireTexel at the hit's texCoord when the material has a kdTexture, else NULL */
 } or_px;
 
 static inline or_px load_px(const or_scene* s, const float* n_t, const float* p_mat, size_t p, v3 origin) {
@@ -269,13 +335,17 @@ static inline or_px load_px(const or_scene* s, const float* n_t, const float* p_
     if (m >= s->num_materials) m = s->num_materials - 1;
     r.mat = &s->materials[m];
     r.V = vnormalize(vsub(origin, r.P));
+    r.texel = NULL;
+    if (s->uv && r.mat->kd_texture && r.mat->kd_texture <= s->num_textures)
+        r.texel = acquire_texel(s, r.mat->kd_texture - 1u, &s->uv[2 * p]);
     return r;
 }
 
-/* computeShading (shading.cpp:7-34); diffuseAlbedo = kd (utils.cpp:33-37, no textures carried). */
+/* computeShading (shading.cpp:7-34); diffuseAlbedo (utils.cpp:33-37): the texel when texture mapping is on
+ * and the material has a kdTexture, else kd.  With shading off the reference returns material.kd itself. */
 static v3 shade(const restir_features* f, const or_px* px, v3 lpos, v3 lcol) {
-    v3 kd = ld3(px->mat->kd);
-    if (!f->enable_shading) return kd;
+    if (!f->enable_shading) return ld3(px->mat->kd);
+    v3 kd = (f->enable_texture_mapping && px->texel) ? ld3(px->texel) : ld3(px->mat->kd);
     v3 L = vnormalize(vsub(lpos, px->P));
     float dotNL = vdot(px->N, L);
     if (dotNL < 0.0f) return mk(0.0f, 0.0f, 0.0f);
@@ -618,7 +688,11 @@ int or_render_frame(const or_scene* s, const restir_camera* cam, const restir_fe
     const size_t n4 = (size_t)view.w * view.h * N * 4;
     restir_camera_frame cf;
     or_camera_derive(cam, &cf);
-    or_primary(s, &cf, W, H, view, view, n_t, p_mat);
+    /* textured scenes: the G-buffer's texCoord plane, bound for every stage of the frame */
+    float* uv = s->num_textures ? (float*)calloc((size_t)view.w * view.h * 2, 4) : NULL;
+    const float* bound = s->uv;
+    or_primary_uv(s, &cf, W, H, view, view, n_t, p_mat, uv);
+    if (uv) ((or_scene*)s)->uv = uv;
     or_ris(s, f, or_rng_key(seed, frame, RESTIR_STAGE_RIS, 0), cf.origin, W, H, view, view, n_t, p_mat,
            out_a, out_b, NULL);
     float* ta = (float*)malloc(n4 * 4);
@@ -649,6 +723,8 @@ int or_render_frame(const or_scene* s, const restir_camera* cam, const restir_fe
     free(ta);
     free(tb);
     or_final(s, f, cf.origin, W, H, view, rect, n_t, p_mat, out_a, out_b, rgb);
+    ((or_scene*)s)->uv = bound;
+    free(uv);
     return rc;
 }
 
@@ -1144,7 +1220,10 @@ int or_render_mis(const or_scene* s, const restir_camera* cam, const restir_feat
     float* n_t = (float*)malloc(npx * 16);
     float* p_mat = (float*)malloc(npx * 16);
     or_rect view = {0, 0, W, H};
-    or_primary(s, &cf, W, H, view, view, n_t, p_mat);
+    float* uv = s->num_textures ? (float*)calloc(npx * 2, 4) : NULL;
+    const float* bound = s->uv;
+    or_primary_uv(s, &cf, W, H, view, view, n_t, p_mat, uv);
+    if (uv) ((or_scene*)s)->uv = uv;
     const uint32_t cap = or_mis_capacity(f, W, H);
     uint32_t* nbr = (uint32_t*)calloc((size_t)(1u + cap) * npx, 4);
     or_neighbours(s, f, or_rng_key(seed, frame, RESTIR_STAGE_NEIGHBOURS, 0), or_rng_key(seed, frame, RESTIR_STAGE_NEIGHBOURS, 1),
@@ -1163,6 +1242,8 @@ int or_render_mis(const or_scene* s, const restir_camera* cam, const restir_feat
             or_rmis_accumulate(s, f, cf.origin, W, H, n_t, p_mat, nbr, a, b, acc);
     }
     or_mis_finish(f, W, H, acc, rgb);
+    ((or_scene*)s)->uv = bound;
+    free(uv);
     free(n_t); free(p_mat); free(nbr); free(acc); free(a); free(b); free(d);
     return rc;
 }

@@ -35,6 +35,11 @@ typedef struct or_rect { uint32_t x0, y0, w, h; } or_rect;
 
 or_scene* or_scene_create(const restir_mesh* meshes, uint32_t num_meshes, const restir_light* lights,
                           uint32_t num_lights);
+or_scene* or_scene_create_textured(const restir_mesh* meshes, uint32_t num_meshes, const restir_light* lights,
+                                   uint32_t num_lights, const restir_texture* textures, uint32_t num_textures);
+/* the G-buffer texCoord plane ([pixels][2], indexed like n_t / p_mat) the following stage calls read; NULL = none */
+void      or_scene_bind_uv(or_scene* s, const float* uv);
+void      or_acquire_texel(const or_scene* s, uint32_t texture, const float tc[2], float out[3]);
 void      or_scene_destroy(or_scene* s);
 uint32_t  or_scene_num_triangles(const or_scene* s);
 uint32_t  or_scene_miss_material(const or_scene* s);
@@ -58,6 +63,8 @@ float or_target_pdf(const or_scene* s, const restir_features* f, const float ori
  * planes are [N][view pixels]; each pass writes only the pixels of `rect` (a sub-rectangle of view). */
 void or_primary(const or_scene* s, const restir_camera_frame* cam, uint32_t W, uint32_t H, or_rect view,
                 or_rect rect, float* n_t, float* p_mat);
+void or_primary_uv(const or_scene* s, const restir_camera_frame* cam, uint32_t W, uint32_t H, or_rect view,
+                   or_rect rect, float* n_t, float* p_mat, float* uv);
 void or_ris(const or_scene* s, const restir_features* f, uint32_t key, const float origin[3], uint32_t W,
             uint32_t H, or_rect view, or_rect rect, const float* n_t, const float* p_mat, float* res_a,
             float* res_b, float* res_dbg);

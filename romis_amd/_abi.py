@@ -27,6 +27,7 @@ NEIGHBOURS_RANDOM, NEIGHBOURS_SIMILAR, NEIGHBOURS_DISSIMILAR, NEIGHBOURS_EQUAL_S
 BUF_GBUF_N_T, BUF_GBUF_P_MAT, BUF_RES_A, BUF_RES_B, BUF_RES_DBG = 0, 1, 2, 3, 4
 BUF_PREV_A, BUF_PREV_B, BUF_PREV_DBG, BUF_RGB = 5, 6, 7, 8
 BUF_MIS_NBR, BUF_MIS_ACC = 9, 10
+BUF_GBUF_UV = 11
 
 K_PRIMARY, K_RIS, K_TEMPORAL, K_SPATIAL, K_FINAL, K_PRIMARY_RIS, K_MIS, K_COUNT = 0, 1, 2, 3, 4, 5, 6, 7
 KERNEL_NAMES = ["primary", "ris", "temporal", "spatial", "final", "primary_ris", "mis"]
@@ -42,13 +43,18 @@ class Light(C.Structure):
 
 
 class Material(C.Structure):
-    _fields_ = [("kd", F3), ("ks", F3), ("shininess", C.c_float), ("transparency", C.c_float)]
+    _fields_ = [("kd", F3), ("ks", F3), ("shininess", C.c_float), ("transparency", C.c_float),
+                ("kd_texture", C.c_uint32)]
 
 
 class Mesh(C.Structure):
     _fields_ = [("positions", C.POINTER(C.c_float)), ("normals", C.POINTER(C.c_float)),
                 ("num_vertices", C.c_uint32), ("triangles", C.POINTER(C.c_uint32)),
-                ("num_triangles", C.c_uint32), ("material", Material)]
+                ("num_triangles", C.c_uint32), ("material", Material), ("texcoords", C.POINTER(C.c_float))]
+
+
+class Texture(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("rgb", C.POINTER(C.c_float))]
 
 
 class Camera(C.Structure):
@@ -90,7 +96,8 @@ class Tile(C.Structure):
 
 
 assert C.sizeof(Light) == 88
-assert C.sizeof(Material) == 32
+assert C.sizeof(Material) == 36
+assert C.sizeof(Mesh) == 80 and C.sizeof(Texture) == 16
 assert C.sizeof(Features) == 72
 
 
@@ -128,6 +135,8 @@ SIGNATURES = {
     "restir_destroy": (None, [_P]),
     "restir_set_seed": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
     "restir_set_scene": (C.c_int, [_P, C.POINTER(Mesh), C.c_uint32, C.POINTER(Light), C.c_uint32]),
+    "restir_set_scene_textured": (C.c_int, [_P, C.POINTER(Mesh), C.c_uint32, C.POINTER(Light), C.c_uint32,
+                                            C.POINTER(Texture), C.c_uint32]),
     "restir_render": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Features), C.c_uint32, C.c_uint32,
                                 C.POINTER(Tile), _P, C.POINTER(_P), C.POINTER(C.c_float)]),
     "restir_frame_retain": (C.c_int, [_P]),

@@ -169,12 +169,33 @@ struct Px {
     v3 P, N, V;
     float t;
     uint32_t mat;
-    float4 kd_sh;   // kd.xyz, shininess
+    float4 kd_sh;   // diffuseAlbedo.xyz (kd, or the kdTexture texel -- apply_albedo), shininess
     float4 ks_pm;   // ks.xyz, bits(pow mode)
-    float4 pw;      // (underflow threshold, bits(integer exponent), transparency, 0)
+    float4 pw;      // (pow underflow threshold, bits(shininess class), transparency, bits(kd_texture))
 };
 
-__device__ __forceinline__ Px make_px(const SceneDev& s, float4 a, float4 b, v3 origin) {
+// acquireTexel's index (texture.cpp:5-6): the float product texCoord * (size - 1) truncated toward zero;
+// products outside [0, size - 1] (an out-of-bounds read in the reference) clamp to the edge texel
+__device__ __forceinline__ uint32_t texel_index(float c, uint32_t n) {
+    const float v = c * (float)((int)n - 1);
+    if (!(v >= 0.0f)) return 0u;
+    if (v >= (float)(n - 1u)) return n - 1u;
+    return (uint32_t)v;
+}
+
+// diffuseAlbedo (utils.cpp:33-37): with texture mapping on and a kdTexture on the material, the texel at the
+// hit's texCoord (the G-buffer plane s.gbuf_uv, view pixel p) replaces kd as the diffuse colour
+__device__ __forceinline__ void apply_albedo(const SceneDev& s, Px& r, size_t p) {
+    const uint32_t tex = __float_as_uint(r.pw.w);
+    if (s.tex_on && tex) {
+        const float2 tc = s.gbuf_uv[p];
+        const uint4 dim = s.tex_dims[tex - 1u];   // width, height, first texel
+        const float4 t = s.tex_texels[dim.z + texel_index(tc.y, dim.y) * dim.x + texel_index(tc.x, dim.x)];
+        r.kd_sh.x = t.x; r.kd_sh.y = t.y; r.kd_sh.z = t.z;
+    }
+}
+
+__device__ __forceinline__ Px make_px(const SceneDev& s, float4 a, float4 b, v3 origin, size_t p) {
     Px r;
     r.N = xyz(a); r.t = a.w;
     r.P = xyz(b);
@@ -185,6 +206,7 @@ __device__ __forceinline__ Px make_px(const SceneDev& s, float4 a, float4 b, v3 
     r.ks_pm = s.materials[3 * m + 1];
     r.pw = s.materials[3 * m + 2];
     r.V = vnormalize(vsub(origin, r.P));
+    apply_albedo(s, r, p);
     return r;
 }
 
@@ -193,7 +215,7 @@ __device__ __forceinline__ size_t ridx(const Region& rg, uint32_t j, size_t p) {
 
 __device__ __forceinline__ Px load_px(const SceneDev& s, const Region& rg, const float4* __restrict__ n_t,
                                       const float4* __restrict__ p_mat, size_t p, v3 origin) {
-    return make_px(s, n_t[gidx(rg, p)], p_mat[p], origin);
+    return make_px(s, n_t[gidx(rg, p)], p_mat[p], origin, p);
 }
 
 // std::pow(cosTheta, shininess) (shading.cpp:26) = glibc's powf (device_math.h gl_powf), specialised per
@@ -241,8 +263,8 @@ __device__ __forceinline__ float material_pow(const GlTabs& tb, float x, const P
 // computeShading (shading.cpp:7-34), general form: every IEEE special case, any material
 __device__ __forceinline__ v3 shade_ref(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,
                                         const GlTabs& tb = gl_global_tabs()) {
+    if (!f.shading) return xyz(s.materials[3 * px.mat]);   // material.kd, not the albedo (shading.cpp:8)
     v3 kd = xyz(px.kd_sh);
-    if (!f.shading) return kd;
     float d;   // glm::distance(hitPos, lightPos) == |lightPos - hitPos|, the length normalize() takes
     v3 L = vnormalize_len(vsub(lpos, px.P), d);
     float dotNL = vdot(px.N, L);
@@ -458,15 +480,22 @@ __device__ __forceinline__ void primary_pixel(const SceneDev& s, const Region& r
         float t, u = 0.0f, v = 0.0f;
         uint32_t tri;
         v3 n = mk(0.0f, 0.0f, 0.0f);
+        float2 tc = make_float2(0.0f, 0.0f);   // a miss keeps the value-initialised HitInfo::texCoord
         uint32_t m = s.num_materials - 1;
         if (closest(bvh, o, d, t, u, v, tri)) {
             float w0 = (1.0f - u) - v;
             float4 a = s.tri_n0[tri], b = s.tri_n1[tri], c = s.tri_n2[tri];
             n = vadd(vadd(vscale(xyz(a), w0), vscale(xyz(b), u)), vscale(xyz(c), v));
             m = __float_as_uint(a.w);
+            if (s.gbuf_uv) {   // texCoord: rtcInterpolate0 of attribute slot 1 (embree_interface.cpp:80-81)
+                const float4 t01 = s.tri_uv[2 * tri], t2 = s.tri_uv[2 * tri + 1];
+                tc.x = (t01.x * w0 + t01.z * u) + t2.x * v;
+                tc.y = (t01.y * w0 + t01.w * u) + t2.y * v;
+            }
         } else {
             t = ROMIS_FLT_MAX;
         }
+        if (s.gbuf_uv) s.gbuf_uv[p] = tc;
         v3 P = vadd(o, vscale(d, t));
         const float4 nt = make_float4(n.x, n.y, n.z, t);
         n_t[gidx(rg, p)] = nt;
@@ -517,7 +546,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
         Sub r[NT > 0 ? NT : RESTIR_MAX_N_DEV];
         for (uint32_t j = 0; j < N; j++) sub_init(r[j]);
         if (L != 0) {
-            Px px = make_px(s, nt, pm, origin);
+            Px px = make_px(s, nt, pm, origin, p);
             const uint32_t ps = pix_state(key, y * rg.W + x);
             for (uint32_t j = 0; j < N; j++) r[j].M = 0u;
             // A primary-ray miss carries the value-initialised HitInfo (kd = ks = 0, N = 0): its target pdf is
@@ -569,7 +598,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 if (NT == 1 && rp) rp[p] = pj;
             }
         } else if (NT == 1 && rp) {
-            rp[p] = target_pdf(s, f, make_px(s, nt, pm, origin), r[0].pos, r[0].col);   // no lights: the initial sample
+            rp[p] = target_pdf(s, f, make_px(s, nt, pm, origin, p), r[0].pos, r[0].col);   // no lights: the initial sample
         }
         for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, ridx(rg, j, p), j * npx + p);
     }
@@ -992,7 +1021,7 @@ __device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& 
     }
     float4 na[kLeanK], nb[kLeanK];
     // pixel shading context (material + view vector) while the neighbour records are in flight
-    const Px cur = make_px(s, cn, cpm, origin);
+    const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
     // A primary-ray miss (value-initialised HitInfo: material kd = ks = 0, normal 0, P not NaN): its zero normal
     // rejects every neighbour (finite neighbour normals, s.normals_bounded: dot = +-0 < 0.906), and the target
     // pdf of any finite-colour sample there is exactly 0, so the combine takes only the pixel's
@@ -1188,7 +1217,7 @@ __device__ __forceinline__ void spatial1_lds_body(const SceneDev& s, const Regio
     if (!live) return;   // no barrier follows
     const uint32_t ci = (uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0);
     const float4 cn = STAGE_NT ? l_nt[ci] : cn_g, ca = l_a[ci], cb = l_b[ci];
-    const Px cur = make_px(s, cn, cpm, origin);
+    const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
     // primary-ray miss: the pass's result is known (spatial1_pixel)
     if (cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z) &&
         __builtin_isfinite(ca.w) && __builtin_isfinite(cb.x + cb.y + cb.z)) {
@@ -1636,7 +1665,7 @@ __device__ __forceinline__ void rmis_body(const SceneDev& s, uint32_t W, uint32_
     if (p >= W * H) return;
     const size_t npx = (size_t)W * H;
     const uint32_t N = f.N;
-    const Px cur = make_px(s, n_t[p], p_mat[p], origin);
+    const Px cur = make_px(s, n_t[p], p_mat[p], origin, p);
     const uint32_t c = nbr[p];
     v3 fc = mk(0.0f, 0.0f, 0.0f);
     for (uint32_t i = 0; i < c; i++) {
@@ -1652,7 +1681,7 @@ __device__ __forceinline__ void rmis_body(const SceneDev& s, uint32_t W, uint32_
                 float denominator = ROMIS_FLT_MIN;
                 for (uint32_t i2 = 0; i2 < c; i2++) {
                     const uint32_t q2 = nbr[(size_t)(1u + i2) * npx + p];
-                    denominator += target_pdf(s, f, make_px(s, n_t[q2], p_mat[q2], origin), pos, col);
+                    denominator += target_pdf(s, f, make_px(s, n_t[q2], p_mat[q2], origin, q2), pos, col);
                 }
                 misWeight = numerator / denominator;
             }
@@ -1870,10 +1899,10 @@ __device__ __forceinline__ void romis_samples_body(const SceneDev& s, uint32_t W
             const uint32_t qq = nbr[(size_t)(1 + d) * npx + p];
             const float4 db = rb[(size_t)si * npx + qq];
             const float2 dd = rdbg[(size_t)si * npx + qq];
-            out[(size_t)d * npx] = aucw_reciprocal(s, f, make_px(s, n_t[qq], p_mat[qq], origin),
+            out[(size_t)d * npx] = aucw_reciprocal(s, f, make_px(s, n_t[qq], p_mat[qq], origin, qq),
                                                    (float)__float_as_uint(db.w), dd.x, dd.y, pos, col);
         }
-        const Px cur = make_px(s, n_t[p], p_mat[p], origin);
+        const Px cur = make_px(s, n_t[p], p_mat[p], origin, p);
         const v3 sc = visible(bvh, cur.P, pos) ? shade(s, f, cur, pos, col) : mk(0.0f, 0.0f, 0.0f);
         out[(size_t)T * npx] = sc.x;
         out[(size_t)(T + 1) * npx] = sc.y;

@@ -198,13 +198,14 @@ struct restir_ctx {
     std::mutex mu;
 
     // scene
-    DevBuf nodes, tri_v0, tri_e1, tri_e2, tri_n0, tri_n1, tri_n2, materials, lights;
+    DevBuf nodes, tri_v0, tri_e1, tri_e2, tri_n0, tri_n1, tri_n2, materials, lights, tex_texels, tex_dims, tri_uv;
     SceneDev sdev{};
     bool has_scene = false;
 
     // work buffers for one view
     uint32_t vw = 0, vh = 0, N = 0;
     DevBuf n_t, p_mat, ra[2], rb[2], dbg[2], rgb;   // stage API: SoA planes
+    DevBuf uv;                                      // the G-buffer texCoord plane (textured scenes)
     DevBuf rec[2];                                  // restir_render / halo frames: per-pixel records
     std::shared_ptr<FramePool> pool = std::make_shared<FramePool>();
     DevBuf rp[2];                                   // their target-pdf cache planes (N = 1, planes layout)
@@ -443,6 +444,7 @@ FeaturesDev to_dev(const restir_features* f) {
     d.spatial_vis = f->spatial_reuse_visibility_check;
     d.shading = f->enable_shading;
     d.tone_map = f->enable_tone_mapping;
+    d.texture = f->enable_texture_mapping;
     d.gamma = f->gamma;
     d.exposure = f->exposure;
     d.mode = f->ray_trace_mode;
@@ -456,6 +458,14 @@ FeaturesDev to_dev(const restir_features* f) {
     d.iterations = f->max_iterations_mis;
     return d;
 }
+
+}  // namespace
+
+// The scene as one launch over a view of npx pixels sees it: the G-buffer texCoord plane (allocated for textured
+// scenes; k_primary writes it, every target pdf reads it) and whether diffuseAlbedo reads the textures.
+static restir_status scene_for(restir_ctx* c, const FeaturesDev& f, size_t npx, SceneDev& out);
+
+namespace {
 
 // neighbourhood capacity of generateResampleIndicesGrid's output (neighbour_selection.cpp:45-105): k + 1, or the
 // whole window for the strategies whose size arithmetic can take every member of a class
@@ -646,6 +656,16 @@ Region grow_rect(const Region& base, uint32_t g) {
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------------------
+static restir_status scene_for(restir_ctx* c, const FeaturesDev& f, size_t npx, SceneDev& out) {
+    out = c->sdev;
+    if (c->sdev.num_textures) {
+        ST_TRY(c->uv.ensure(std::max<size_t>(npx, 1) * 8));
+        out.gbuf_uv = c->uv.as<float2>();
+        out.tex_on = f.texture ? 1u : 0u;
+    }
+    return RESTIR_OK;
+}
+
 extern "C" {
 
 restir_status restir_create(int device, restir_ctx** out) {
@@ -682,7 +702,7 @@ void restir_destroy(restir_ctx* c) {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
         for (DevBuf* b : {&c->nodes, &c->tri_v0, &c->tri_e1, &c->tri_e2, &c->tri_n0, &c->tri_n1, &c->tri_n2,
-                          &c->materials, &c->lights, &c->n_t, &c->p_mat, &c->ra[0], &c->ra[1], &c->rb[0], &c->rb[1],
+                          &c->materials, &c->lights, &c->tex_texels, &c->tex_dims, &c->tri_uv, &c->uv, &c->n_t, &c->p_mat, &c->ra[0], &c->ra[1], &c->rb[0], &c->rb[1],
                           &c->dbg[0], &c->dbg[1], &c->rgb, &c->queue_ctr, &c->halo_scratch, &c->rec[0], &c->rec[1], &c->rp[0], &c->rp[1]})
             b->release();
         for (Pending& p : c->pending) { (void)hipEventDestroy(p.start); (void)hipEventDestroy(p.stop); }
@@ -703,15 +723,30 @@ restir_status restir_set_seed(restir_ctx* c, uint32_t seed, uint32_t frame_index
 
 restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_t num_meshes, const restir_light* lights,
                                uint32_t num_lights) {
+    return restir_set_scene_textured(c, meshes, num_meshes, lights, num_lights, nullptr, 0);
+}
+
+restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes, uint32_t num_meshes,
+                                        const restir_light* lights, uint32_t num_lights, const restir_texture* textures,
+                                        uint32_t num_textures) {
     if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
     if (num_meshes && !meshes) return fail(RESTIR_ERR_INVALID, "meshes is NULL");
     if (num_lights && !lights) return fail(RESTIR_ERR_INVALID, "lights is NULL");
+    if (num_textures && !textures) return fail(RESTIR_ERR_INVALID, "textures is NULL");
+    for (uint32_t i = 0; i < num_textures; i++)
+        if (!textures[i].width || !textures[i].height || !textures[i].rgb)
+            return fail(RESTIR_ERR_INVALID, "texture %u: empty image", i);
+    for (uint32_t m = 0; m < num_meshes; m++)
+        if (meshes[m].material.kd_texture > num_textures)
+            return fail(RESTIR_ERR_INVALID, "mesh %u: kd_texture %u of %u textures", m, meshes[m].material.kd_texture,
+                        num_textures);
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
 
     // flatten triangles (mesh order = original index order, like the oracle)
     std::vector<BvhTriangle> tris;
     std::vector<float> n0, n1, n2;   // float4 records
+    std::vector<float> tuv;          // 2 float4 per triangle: (t0.xy, t1.xy), (t2.xy, 0, 0)
     for (uint32_t m = 0; m < num_meshes; m++) {
         const restir_mesh& mesh = meshes[m];
         if (mesh.num_triangles && (!mesh.positions || !mesh.normals || !mesh.triangles))
@@ -730,6 +765,12 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
                 dst.insert(dst.end(), &mesh.normals[3 * t[k]], &mesh.normals[3 * t[k]] + 3);
                 dst.push_back(k == 0 ? u2f(m) : 0.0f);
             }
+            for (int k = 0; k < 3; k++) {
+                tuv.push_back(mesh.texcoords ? mesh.texcoords[2 * t[k]] : 0.0f);
+                tuv.push_back(mesh.texcoords ? mesh.texcoords[2 * t[k] + 1] : 0.0f);
+            }
+            tuv.push_back(0.0f);
+            tuv.push_back(0.0f);
         }
     }
     if (tris.size() >= (1u << 24)) return fail(RESTIR_ERR_INVALID, "too many triangles (%zu)", tris.size());
@@ -765,7 +806,7 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
             if ((double)thr > std::exp2(-150.0 * (1.0 + 0x1p-20) / y)) thr = std::nextafter(thr, 0.0f);
         }
         o[7] = u2f(mode);
-        o[8] = thr; o[9] = u2f(pw_class(mt.shininess)); o[10] = mt.transparency; o[11] = 0.0f;
+        o[8] = thr; o[9] = u2f(pw_class(mt.shininess)); o[10] = mt.transparency; o[11] = u2f(mt.kd_texture);
     };
     for (uint32_t m = 0; m < num_meshes; m++) put_material(m, meshes[m].material);
     {
@@ -800,6 +841,31 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
     ST_TRY(c->tri_n2.upload(n2.data(), n2.size() * 4, c->stream));
     ST_TRY(c->materials.upload(mats.data(), mats.size() * 4, c->stream));
     ST_TRY(c->lights.upload(lt.data(), lt.size() * 4, c->stream));
+    // textures: texels as float4, images back to back; (width, height, first texel, 0) per image
+    std::vector<float> texels;
+    std::vector<uint32_t> dims;
+    double tmax = 0.0;
+    bool tfinite = true;
+    for (uint32_t i = 0; i < num_textures; i++) {
+        const restir_texture& tx = textures[i];
+        dims.insert(dims.end(), {tx.width, tx.height, (uint32_t)(texels.size() / 4), 0u});
+        for (size_t k = 0; k < (size_t)tx.width * tx.height; k++) {
+            for (int a = 0; a < 3; a++) {
+                const float v = tx.rgb[3 * k + a];
+                texels.push_back(v);
+                tfinite = tfinite && std::isfinite(v);
+                tmax = std::max(tmax, (double)std::fabs(v));
+            }
+            texels.push_back(0.0f);
+        }
+    }
+    if (texels.size() / 4 >= 0xFFFFFFFFull) return fail(RESTIR_ERR_INVALID, "textures too large");
+    if (texels.empty()) texels.assign(4, 0.0f);
+    if (dims.empty()) dims.assign(4, 0u);
+    if (tuv.empty()) tuv.assign(8, 0.0f);
+    ST_TRY(c->tex_texels.upload(texels.data(), texels.size() * 4, c->stream));
+    ST_TRY(c->tex_dims.upload(dims.data(), dims.size() * 4, c->stream));
+    ST_TRY(c->tri_uv.upload(tuv.data(), tuv.size() * 4, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));   // host vectors go out of scope
 
     SceneDev& s = c->sdev;
@@ -814,6 +880,12 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
     s.num_tris = (uint32_t)T;
     s.materials = c->materials.as<float4>();
     s.num_materials = num_meshes + 1;
+    s.tex_texels = c->tex_texels.as<float4>();
+    s.tex_dims = c->tex_dims.as<uint4>();
+    s.tri_uv = c->tri_uv.as<float4>();
+    s.num_textures = num_textures;
+    s.gbuf_uv = nullptr;   // per launch (scene_for)
+    s.tex_on = 0u;
     s.lights = c->lights.as<float4>();
     s.num_lights = num_lights;
     s.light_types = types;
@@ -840,6 +912,8 @@ restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_
                 finite = finite && std::isfinite(v);
                 kmax = std::max(kmax, (double)std::fabs(v));
             }
+        finite = finite && tfinite;   // texels are diffuse colours too
+        kmax = std::max(kmax, tmax);
         s.shade_finite = (finite && cmax * kmax <= 0x1p120) ? 1u : 0u;
     }
     s.normals_bounded = 1u;
@@ -864,7 +938,8 @@ static restir_status render_mis(restir_ctx* c, const restir_camera* cam, const r
     const CameraDev camd = camera_dev(cam);
     const Region view = make_region(W, H, 0, 0, W, H, 0, 0, W, H);
     const uint32_t frame = c->frame_index++;
-    const SceneDev& s = c->sdev;
+    SceneDev s;
+    ST_TRY(scene_for(c, f, (size_t)W * H, s));
     float4* nt = c->n_t.as<float4>();
     float4* pm = c->p_mat.as<float4>();
     TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, nt, pm, nullptr, c->tuning, c->stream));
@@ -960,7 +1035,8 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     const Region view = fb.region(make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.gx0, t.gy0, t.gwidth, t.gheight));
     const Region owned = fb.region(make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.x0, t.y0, t.width, t.height));
     const uint32_t frame = c->frame_index++;
-    const SceneDev& s = c->sdev;
+    SceneDev s;
+    ST_TRY(scene_for(c, f, (size_t)t.gwidth * t.gheight, s));
     float4* pm = c->p_mat.as<float4>();
     int cur = 0;
 
@@ -1117,6 +1193,10 @@ static restir_status stage_buffer(restir_ctx* c, restir_buffer which, DevBuf** o
         case RESTIR_BUF_PREV_B: *out = &c->rb[prv]; *bytes = npx * c->N * 16; break;
         case RESTIR_BUF_PREV_DBG: *out = &c->dbg[prv]; *bytes = npx * c->N * 8; break;
         case RESTIR_BUF_RGB: *out = &c->rgb; *bytes = (size_t)c->rgb_w * c->rgb_h * 12; break;
+        case RESTIR_BUF_GBUF_UV:
+            if (!c->sdev.num_textures) return fail(RESTIR_ERR_INVALID, "gbuf_uv: the scene has no textures");
+            ST_TRY(c->uv.ensure(npx * 8));
+            *out = &c->uv; *bytes = npx * 8; break;
         case RESTIR_BUF_MIS_NBR:
             if (!c->mis_cap) return fail(RESTIR_ERR_STATE, "MIS buffers: call restir_stage_mis_capacity first");
             *out = &c->mis_nbr; *bytes = (size_t)(1u + c->mis_cap) * npx * 4; break;
@@ -1167,7 +1247,11 @@ restir_status restir_stage_primary(restir_ctx* c, const restir_camera* cam) {
     if (!cam) return fail(RESTIR_ERR_INVALID, "camera is NULL");
     STAGE_PRELUDE();
     const CameraDev camd = camera_dev(cam);
-    TIMED(c, RESTIR_K_PRIMARY, launch_primary(c->sdev, c->stage_rg, camd, c->n_t.as<float4>(), c->p_mat.as<float4>(), nullptr,
+    FeaturesDev d{};
+    d.texture = 1u;
+    SceneDev sd;
+    ST_TRY(scene_for(c, d, (size_t)c->vw * c->vh, sd));
+    TIMED(c, RESTIR_K_PRIMARY, launch_primary(sd, c->stage_rg, camd, c->n_t.as<float4>(), c->p_mat.as<float4>(), nullptr,
                                               c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
@@ -1186,9 +1270,11 @@ restir_status restir_stage_ris(restir_ctx* c, const restir_camera* cam, const re
     STAGE_PRELUDE();
     FeaturesDev d;
     ST_TRY(stage_features(c, f, d));
+    SceneDev sd;
+    ST_TRY(scene_for(c, d, (size_t)c->vw * c->vh, sd));
     const CameraDev camd = camera_dev(cam);
     const int cur = c->cur;
-    TIMED(c, RESTIR_K_RIS, launch_ris(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
+    TIMED(c, RESTIR_K_RIS, launch_ris(sd, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                                       c->ra[cur].as<float4>(), c->rb[cur].as<float4>(),
                                       debug ? c->dbg[cur].as<float2>() : nullptr, nullptr, c->tuning, c->queue, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1201,10 +1287,12 @@ restir_status restir_stage_temporal(restir_ctx* c, const restir_camera* cam, con
     STAGE_PRELUDE();
     FeaturesDev d;
     ST_TRY(stage_features(c, f, d));
+    SceneDev sd;
+    ST_TRY(scene_for(c, d, (size_t)c->vw * c->vh, sd));
     const CameraDev camd = camera_dev(cam);
     const int cur = c->cur, prv = cur ^ 1;
     TIMED(c, RESTIR_K_TEMPORAL,
-          launch_temporal(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
+          launch_temporal(sd, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                           c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->ra[prv].as<float4>(), c->rb[prv].as<float4>(),
                           c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), debug ? c->dbg[cur].as<float2>() : nullptr,
                           nullptr, nullptr, c->tuning, c->stream));
@@ -1218,10 +1306,12 @@ restir_status restir_stage_spatial(restir_ctx* c, const restir_camera* cam, cons
     STAGE_PRELUDE();
     FeaturesDev d;
     ST_TRY(stage_features(c, f, d));
+    SceneDev sd;
+    ST_TRY(scene_for(c, d, (size_t)c->vw * c->vh, sd));
     const CameraDev camd = camera_dev(cam);
     const int cur = c->cur, nxt = cur ^ 1;
     TIMED(c, RESTIR_K_SPATIAL,
-          launch_spatial(c->sdev, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
+          launch_spatial(sd, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                          c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->ra[nxt].as<float4>(), c->rb[nxt].as<float4>(),
                          debug ? c->dbg[nxt].as<float2>() : nullptr, nullptr, nullptr, nullptr, c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1234,9 +1324,11 @@ restir_status restir_stage_final(restir_ctx* c, const restir_camera* cam, const 
     STAGE_PRELUDE();
     FeaturesDev d;
     ST_TRY(stage_features(c, f, d));
+    SceneDev sd;
+    ST_TRY(scene_for(c, d, (size_t)c->vw * c->vh, sd));
     const CameraDev camd = camera_dev(cam);
     const int cur = c->cur;
-    TIMED(c, RESTIR_K_FINAL, launch_final(c->sdev, c->stage_rg, d, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
+    TIMED(c, RESTIR_K_FINAL, launch_final(sd, c->stage_rg, d, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                                           c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->rgb.as<float>(), c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
@@ -1247,6 +1339,8 @@ restir_status restir_stage_mis_capacity(restir_ctx* c, const restir_features* f,
     STAGE_PRELUDE();
     FeaturesDev d;
     ST_TRY(stage_features(c, f, d));
+    SceneDev sd;
+    ST_TRY(scene_for(c, d, (size_t)c->vw * c->vh, sd));
     ST_TRY(ensure_mis(c, f, c->vw, c->vh));
     *out_cap = c->mis_cap;
     return RESTIR_OK;
@@ -1256,8 +1350,10 @@ restir_status restir_stage_neighbours(restir_ctx* c, const restir_features* f, u
     STAGE_PRELUDE();
     FeaturesDev d;
     ST_TRY(stage_features(c, f, d));
+    SceneDev sd;
+    ST_TRY(scene_for(c, d, (size_t)c->vw * c->vh, sd));
     ST_TRY(ensure_mis(c, f, c->vw, c->vh));
-    TIMED(c, RESTIR_K_MIS, launch_mis_neighbours(c->sdev, c->vw, c->vh, d, key_similar, key_dissimilar, c->n_t.as<float4>(),
+    TIMED(c, RESTIR_K_MIS, launch_mis_neighbours(sd, c->vw, c->vh, d, key_similar, key_dissimilar, c->n_t.as<float4>(),
                                                  c->p_mat.as<float4>(), c->mis_nbr.as<uint32_t>(), c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
@@ -1268,12 +1364,14 @@ restir_status restir_stage_mis_accumulate(restir_ctx* c, const restir_camera* ca
     STAGE_PRELUDE();
     FeaturesDev d;
     ST_TRY(stage_features(c, f, d));
+    SceneDev sd;
+    ST_TRY(scene_for(c, d, (size_t)c->vw * c->vh, sd));
     ST_TRY(check_romis_window(f, c->vw, c->vh));
     ST_TRY(ensure_mis(c, f, c->vw, c->vh));
     const CameraDev camd = camera_dev(cam);
     const int cur = c->cur;
     if (iteration == 0) HIP_TRY(hipMemsetAsync(c->mis_acc.p, 0, (size_t)c->mis_rows * c->vw * c->vh * 4, c->stream));
-    TIMED(c, RESTIR_K_MIS, launch_mis_accumulate(c->sdev, c->vw, c->vh, d, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
+    TIMED(c, RESTIR_K_MIS, launch_mis_accumulate(sd, c->vw, c->vh, d, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                                                  c->mis_nbr.as<uint32_t>(), c->ra[cur].as<float4>(), c->rb[cur].as<float4>(),
                                                  c->dbg[cur].as<float2>(), iteration, c->mis_acc.as<float>(),
                                                  c->mis_smp.as<float>(), c->mis_smp_samples, c->tuning, c->stream));
@@ -1285,6 +1383,8 @@ restir_status restir_stage_mis_finish(restir_ctx* c, const restir_features* f) {
     STAGE_PRELUDE();
     FeaturesDev d;
     ST_TRY(stage_features(c, f, d));
+    SceneDev sd;
+    ST_TRY(scene_for(c, d, (size_t)c->vw * c->vh, sd));
     if (!c->mis_cap) return fail(RESTIR_ERR_STATE, "MIS buffers: run restir_stage_mis_accumulate first");
     TIMED(c, RESTIR_K_MIS, launch_mis_finish(c->vw, c->vh, d, c->mis_acc.as<float>(), c->rgb.as<float>(), c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1427,7 +1527,8 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
     h.pass = 0;
     h.passes = passes;
     h.cur = 0;
-    const SceneDev& s = c->sdev;
+    SceneDev s;
+    ST_TRY(scene_for(c, f, (size_t)t.gwidth * t.gheight, s));
     float4* pm = c->p_mat.as<float4>();
     // G-buffer on the whole view (the spatial passes read the neighbours' depth / normal / position),
     // reservoirs only on the owned rectangle
@@ -1492,8 +1593,10 @@ restir_status restir_halo_spatial(restir_ctx* c) {
     HIP_TRY(hipSetDevice(c->device));
     const int nxt = h.cur ^ 1;
     const FrameBufs fb{c, h.fb_records, (size_t)h.view.vw * h.view.vh, h.f.N};
+    SceneDev sd;
+    ST_TRY(scene_for(c, h.f, (size_t)h.view.vw * h.view.vh, sd));
     TIMED(c, RESTIR_K_SPATIAL,
-          launch_spatial(c->sdev, h.owned, h.f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_SPATIAL, h.pass), h.camd.origin,
+          launch_spatial(sd, h.owned, h.f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_SPATIAL, h.pass), h.camd.origin,
                          fb.nt(h.cur), c->p_mat.as<float4>(), fb.ra(h.cur), fb.rb(h.cur), fb.ra(nxt), fb.rb(nxt), nullptr,
                          h.rp_ok ? fb.rp(h.cur) : nullptr, fb.rp(nxt), &h.rp_ok, c->tuning, c->stream));
     h.cur = nxt;
@@ -1510,7 +1613,9 @@ restir_status restir_halo_end(restir_ctx* c, restir_frame** out_next, float* out
         return fail(RESTIR_ERR_STATE, "restir_halo_end after %u of %u spatial passes", h.pass, h.passes);
     HIP_TRY(hipSetDevice(c->device));
     const FrameBufs fb{c, h.fb_records, (size_t)h.view.vw * h.view.vh, h.f.N};
-    TIMED(c, RESTIR_K_FINAL, launch_final(c->sdev, h.owned, h.f, h.camd.origin, fb.nt(h.cur), c->p_mat.as<float4>(),
+    SceneDev sd;
+    ST_TRY(scene_for(c, h.f, (size_t)h.view.vw * h.view.vh, sd));
+    TIMED(c, RESTIR_K_FINAL, launch_final(sd, h.owned, h.f, h.camd.origin, fb.nt(h.cur), c->p_mat.as<float4>(),
                                           fb.ra(h.cur), fb.rb(h.cur), c->rgb.as<float>(), c->tuning, c->stream));
     c->cur = h.cur;
     h.active = false;

@@ -53,6 +53,18 @@ struct SceneDev {
     uint32_t shade_finite;     // every light colour x material kd / ks product is finite (shade()'s NaN tests)
     uint32_t normals_bounded;  // every vertex normal component finite with |n| <= 2^125: interpolated normals are
                                // finite, so a miss pixel's zero normal rejects every neighbour (dot = +-0)
+    // Textures (Material::kdTexture): texels as float4 (rgb, 0), all images back to back; tex_dims[i] =
+    // (width, height, first texel, 0); per-triangle texture coordinates by original index, 2 float4 each:
+    // (t0.xy, t1.xy), (t2.xy, 0, 0).  materials[3m + 2].w = bits(kd_texture), 0 = none.
+    const float4* tex_texels;
+    const uint4* tex_dims;
+    const float4* tri_uv;
+    uint32_t num_textures;
+    // per launch (set by the host for the view being rendered): the G-buffer texCoord plane (nullptr for scenes
+    // without textures; k_primary writes it, everything else reads it) and whether diffuseAlbedo reads
+    // textures (Features::enableTextureMapping and num_textures > 0)
+    float2* gbuf_uv;
+    uint32_t tex_on;
 };
 
 // Image region bookkeeping: global image W x H (y = 0 bottom), storage view (the computed region, row-major)
@@ -129,6 +141,7 @@ struct FeaturesDev {
     uint32_t clamp_m;
     uint32_t initial_vis, unbiased, spatial_vis, shading, tone_map;
     float gamma, exposure;
+    uint32_t texture;         // enableTextureMapping
     // R-MIS / R-OMIS and the neighbour-selection heuristic (common.h:110-121)
     uint32_t mode;            // restir_mode
     uint32_t strategy;        // restir_neighbour_strategy

@@ -69,9 +69,12 @@ class Renderer:
 
     # ---- scene / seed -------------------------------------------------------------------------------
     def set_scene(self, scene) -> None:
+        """EmbreeInterface(scene): meshes, lights and the Images of textured materials (restir_set_scene_textured)."""
         meshes, nm, lights, nl, keep = scene.to_abi()
-        check(self.lib, self.lib.restir_set_scene(self.ctx, meshes, nm, lights, nl), "restir_set_scene")
-        self._scene_keep = (meshes, lights, keep)
+        texs, ntex, tkeep = scene.textures_abi()
+        check(self.lib, self.lib.restir_set_scene_textured(self.ctx, meshes, nm, lights, nl, texs, ntex),
+              "restir_set_scene_textured")
+        self._scene_keep = (meshes, lights, keep, texs, tkeep)
 
     def set_seed(self, seed: int = _abi.RESTIR_DEFAULT_SEED, frame: int = 0) -> None:
         check(self.lib, self.lib.restir_set_seed(self.ctx, seed, frame), "restir_set_seed")
@@ -166,7 +169,7 @@ class Renderer:
             _abi.BUF_GBUF_N_T: (npx, 4), _abi.BUF_GBUF_P_MAT: (npx, 4),
             _abi.BUF_RES_A: (n, npx, 4), _abi.BUF_RES_B: (n, npx, 4), _abi.BUF_RES_DBG: (n, npx, 2),
             _abi.BUF_PREV_A: (n, npx, 4), _abi.BUF_PREV_B: (n, npx, 4), _abi.BUF_PREV_DBG: (n, npx, 2),
-            _abi.BUF_RGB: (h, w, 3),
+            _abi.BUF_RGB: (h, w, 3), _abi.BUF_GBUF_UV: (npx, 2),
         }[which]
 
     def upload(self, which: int, arr: np.ndarray) -> None:

@@ -31,6 +31,14 @@ class MeshData:
     shininess: np.float32
     transparency: np.float32
     name: str = ""
+    texcoords: np.ndarray | None = None   # [V, 2] float32 Vertex::texCoord (None: loadMesh's (0, 0))
+    texture: object = None                # Texture (Material::kdTexture) or None
+
+
+@dataclass
+class Texture:
+    """Image (framework/include/framework/image.h): rgb [height][width][3] float32, row 0 = the file's first row."""
+    rgb: np.ndarray
 
 
 @dataclass
@@ -43,9 +51,18 @@ class Scene:
     def num_triangles(self) -> int:
         return int(sum(len(m.triangles) for m in self.meshes))
 
+    def textures(self) -> list:
+        """The distinct Images the meshes' materials point at (restir_material.kd_texture = 1 + index)."""
+        out = []
+        for m in self.meshes:
+            if m.texture is not None and not any(t is m.texture for t in out):
+                out.append(m.texture)
+        return out
+
     def to_abi(self):
         """(Mesh array, Light array, keepalive) for restir_set_scene / or_scene_create."""
         keep = []
+        texs = self.textures()
         meshes = (_abi.Mesh * max(1, len(self.meshes)))()
         for i, m in enumerate(self.meshes):
             pos = np.ascontiguousarray(m.positions, dtype=f32)
@@ -61,10 +78,28 @@ class Scene:
             meshes[i].material.ks[:] = [float(x) for x in m.ks]
             meshes[i].material.shininess = float(m.shininess)
             meshes[i].material.transparency = float(m.transparency)
+            meshes[i].material.kd_texture = 0 if m.texture is None else 1 + next(
+                k for k, t in enumerate(texs) if t is m.texture)
+            if m.texcoords is not None:
+                tc = np.ascontiguousarray(m.texcoords, dtype=f32)
+                keep.append(tc)
+                meshes[i].texcoords = tc.ctypes.data_as(C.POINTER(C.c_float))
         lights = (_abi.Light * max(1, len(self.lights)))()
         for i, l in enumerate(self.lights):
             lights[i] = l
         return meshes, len(self.meshes), lights, len(self.lights), keep
+
+    def textures_abi(self):
+        """(Texture array, count, keepalive) for restir_set_scene_textured / or_scene_create_textured."""
+        texs = self.textures()
+        arr = (_abi.Texture * max(1, len(texs)))()
+        keep = []
+        for i, t in enumerate(texs):
+            rgb = np.ascontiguousarray(t.rgb, dtype=f32)
+            keep.append(rgb)
+            arr[i].width, arr[i].height = rgb.shape[1], rgb.shape[0]
+            arr[i].rgb = rgb.ctypes.data_as(C.POINTER(C.c_float))
+        return arr, len(texs), keep
 
 
 def _bits(a) -> np.ndarray:
@@ -105,8 +140,15 @@ def load_prebuilt(name: str) -> Scene:
         pos = _bits([v[0] for v in m["vertices"]]).reshape(-1, 3)
         nrm = _bits([v[1] for v in m["vertices"]]).reshape(-1, 3)
         tri = np.asarray(m["triangles"], dtype=np.uint32).reshape(-1, 3)
+        tc = _bits([v[2] for v in m["vertices"]]).reshape(-1, 2)
+        tex = None
+        if "texture" in m:   # Image: stb RGB bytes / 255.0f (image.cpp:22-31), bytes from the reference's load
+            t = m["texture"]
+            b = np.frombuffer(bytes.fromhex(t["rgb_u8"]), dtype=np.uint8).astype(f32)
+            tex = Texture((b / f32(255.0)).astype(f32).reshape(t["height"], t["width"], 3))
         meshes.append(MeshData(pos, nrm, tri, _bits(m["kd"]), _bits(m["ks"]), _bits([m["shininess"]])[0],
-                               _bits([m["transparency"]])[0], name=f"{name}:{i}"))
+                               _bits([m["transparency"]])[0], name=f"{name}:{i}",
+                               texcoords=tc if np.any(tc) or tex is not None else None, texture=tex))
     lights = [light_from_record(r) for r in d["lights"]]
     return Scene(meshes, lights, name)
 

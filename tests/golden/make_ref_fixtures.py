@@ -1,10 +1,10 @@
 """Regenerate the fixtures that pin the oracle's inputs against the reference's OWN code.
 
 Builds oracle/_ref/dump_ref (oracle/Makefile `ref`: the reference's scene.cpp, mesh.cpp, image.cpp,
-tiny_obj_loader.cc and tone_mapping.cpp compiled unmodified from /root/reference, linked with
+tiny_obj_loader.cc, texture.cpp and tone_mapping.cpp compiled unmodified from /root/reference, linked with
 oracle/ref_harness/dump_ref.cpp), runs it on /root/reference/data and splits its output into
   romis_amd/scenes/prebuilt_scenes.json  -- loadScenePrebuilt() results (scene assets the product loads)
-  tests/golden/ref_fixtures.json         -- regularLightGrid, exposureToneMapping and glm primitive vectors
+  tests/golden/ref_fixtures.json         -- regularLightGrid, exposureToneMapping, acquireTexel and glm primitive vectors
 Floats are stored as IEEE-754 bit patterns.  Run in the build container only (needs /root/reference).
 """
 import json
@@ -30,7 +30,7 @@ def main() -> int:
         json.dump(scenes, fh, separators=(",", ":"))
     fx = {"source": "oracle/_ref/dump_ref (reference scene.cpp / tone_mapping.cpp / vendored glm 0.9.9.9)",
           "float_encoding": "ieee754-bits",
-          "light_grid": d["light_grid"], "tonemap": d["tonemap"], "glm": d["glm"]}
+          "light_grid": d["light_grid"], "tonemap": d["tonemap"], "glm": d["glm"], "texel": d["texel"]}
     with open(os.path.join(ROOT, "tests", "golden", "ref_fixtures.json"), "w") as fh:
         json.dump(fx, fh, separators=(",", ":"))
     return 0

@@ -29,7 +29,7 @@ _scenes = {}
 
 def get_scene(name):
     if name not in _scenes:
-        _scenes[name] = scene.bench_scene(name) if name != "Cube" else scene.load_prebuilt("Cube")
+        _scenes[name] = scene.bench_scene(name) if name not in ("Cube", "CubeTextured") else scene.load_prebuilt(name)
     return _scenes[name]
 
 
@@ -554,3 +554,72 @@ def test_temporal_frames_recycle_records(gpu, oracle):
             prev_gpu, prev_or = grid, res   # the previous predecessor is released here
     finally:
         other.close()
+
+
+
+# --------------------------------------------------------------------------------------------------------
+# textures: diffuseAlbedo = acquireTexel(kdTexture, texCoord) on CubeTextured (scene.cpp:91-95)
+TEX = "CubeTextured"
+
+
+def test_textured_gbuffer_bit_exact(gpu, oracle):
+    """genPrimaryRayHits on a textured scene also interpolates the hit's texCoord (embree_interface.cpp:80-81)."""
+    _, osc, cam = setup(gpu, oracle, TEX, 1)
+    gpu.stage_primary(cam)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    assert_bits(gpu.download(_abi.BUF_GBUF_N_T), n_t, "n_t")
+    assert_bits(gpu.download(_abi.BUF_GBUF_P_MAT), p_mat, "p_mat")
+    assert_bits(gpu.download(_abi.BUF_GBUF_UV), osc.uv, "texCoord")
+    hit = n_t[:, 3] < 1e30
+    assert hit.mean() > 0.05 and len(np.unique(osc.uv[hit], axis=0)) > 100
+
+
+@pytest.mark.parametrize("texture", [1, 0])
+@pytest.mark.parametrize("N", [1, 2])
+def test_textured_stages_bit_exact(gpu, oracle, texture, N):
+    """RIS, a spatial pass and final shading on CubeTextured with texture mapping on (texel albedo) and off
+    (kd), each stage on the oracle's inputs."""
+    _, osc, cam = setup(gpu, oracle, TEX, N)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    for which, arr in [(_abi.BUF_GBUF_N_T, n_t), (_abi.BUF_GBUF_P_MAT, p_mat), (_abi.BUF_GBUF_UV, osc.uv)]:
+        gpu.upload(which, arr)
+    f = _abi.default_features(num_samples_in_reservoir=N, enable_texture_mapping=texture)
+    gpu.stage_ris(cam, f, key(_abi.RESTIR_STAGE_RIS))
+    a, b, d = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
+    assert_bits(gpu.download(_abi.BUF_RES_A), a, "ris res_a")
+    assert_bits(gpu.download(_abi.BUF_RES_B), b, "ris res_b")
+    assert_bits(gpu.download(_abi.BUF_RES_DBG), d, "ris wSum/chosen")
+    kp = key(_abi.RESTIR_STAGE_SPATIAL, 0)
+    gpu.stage_spatial(cam, f, kp)
+    a, b, d = oracle.spatial_pass(osc, f, kp, origin(oracle, cam), W, H, n_t, p_mat, (a, b))
+    assert_bits(gpu.download(_abi.BUF_RES_A), a, "spatial res_a")
+    assert_bits(gpu.download(_abi.BUF_RES_B), b, "spatial res_b")
+    gpu.stage_final(cam, f)
+    want = oracle.final(osc, f, origin(oracle, cam), W, H, n_t, p_mat, (a, b))
+    assert_bits(gpu.download(_abi.BUF_RGB), want, "rgb")
+
+
+@pytest.mark.parametrize("texture", [1, 0])
+def test_textured_frames_match_oracle(gpu, oracle, texture):
+    """Whole CubeTextured frames (2 temporal frames, 2 spatial passes): images and returned grids bit-exact; the
+    texture visibly changes the image."""
+    s = get_scene(TEX)
+    gpu.set_scene(s)
+    osc = oracle.OracleScene(s)
+    cam = scene.camera_for(TEX, W, H)
+    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=2, temporal_reuse=1,
+                              enable_texture_mapping=texture)
+    gpu.set_seed(SEED, 0)
+    prev_gpu, prev_or = None, None
+    first = None
+    for frame in range(2):
+        rgb, grid = gpu.render_restir(prev_gpu, cam, W, H, f)
+        want, res, _ = oracle.render_frame(osc, cam, f, W, H, SEED, frame, prev=prev_or)
+        assert_bits(rgb, want, f"frame {frame} rgb")
+        assert_grid(grid, res, f"frame {frame}")
+        prev_gpu, prev_or = grid, res
+        first = want if first is None else first
+    f0 = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=2, temporal_reuse=1,
+                               enable_texture_mapping=1 - texture)
+    other, _, _ = oracle.render_frame(osc, cam, f0, W, H, SEED, 0, prev=None)
+    assert not np.array_equal(other, first)

@@ -176,3 +176,26 @@ def test_rng_golden_values(oracle):
         want = json.load(fh)
     assert key == want["key"]
     assert got == want["draws"]
+
+
+def test_cube_textured_scene_carries_its_image():
+    """loadScenePrebuilt(CubeTextured) (scene.cpp:91-95): one mesh with map_Kd default.png -- a 128 x 128 Image
+    whose texels are the stb bytes / 255.0f (the harness checked every texel against the reference's pixels)
+    -- and per-vertex texture coordinates from the OBJ's vt records."""
+    s = scene.load_prebuilt("CubeTextured")
+    assert len(s.meshes) == 1 and len(s.lights) == 1
+    m = s.meshes[0]
+    assert m.texture is not None and m.texture.rgb.shape == (128, 128, 3)
+    assert m.texcoords is not None and m.texcoords.shape == (len(m.positions), 2)
+    assert 0.0 <= m.texcoords.min() and m.texcoords.max() <= 1.0
+    assert len(np.unique(m.texture.rgb.reshape(-1, 3), axis=0)) >= 2
+
+
+def test_acquire_texel_matches_reference_build(oracle, fx):
+    """acquireTexel (texture.cpp:4-9), compiled unmodified into oracle/_ref: the oracle's restatement returns
+    the reference's texel bit for bit on random, edge and texel-boundary coordinates."""
+    s = scene.load_prebuilt(fx["texel"]["scene"])
+    osc = oracle.OracleScene(s)
+    for tc_bits, want_bits in fx["texel"]["cases"]:
+        got = oracle.acquire_texel(osc, 0, f32(tc_bits))
+        assert got.view(np.uint32).tolist() == want_bits, f32(tc_bits)

@@ -30,6 +30,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md "Chip-level parameters")
+FP32_VECTOR_PEAK_TFS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md "Matrix cores", F32 row)
+RIS_FLOP_PER_CANDIDATE = 160
 TILE_W, TILE_H = 1920, 1080
 
 
@@ -146,17 +148,35 @@ def cpu_baseline(sc, cam_fn, features, rows, W, H):
     def band(n):   # owned rows [y0, y0+n) plus the ghost rows the spatial passes read
         return pyoracle.Rect(0, y0 - g, W, n + 2 * g), pyoracle.Rect(0, y0, W, n)
 
-    v, rc = band(2)
-    pyoracle.render_frame(osc, cam, features, W, H, view=v, rect=rc, threads=threads)   # warm
-    v, rc = band(rows)
-    t0 = time.perf_counter()
-    pyoracle.render_frame(osc, cam, features, W, H, view=v, rect=rc, threads=threads)
-    dt = time.perf_counter() - t0
+    def timed(reference_rng, n):
+        pyoracle.set_rng_mode(reference_rng)
+        try:
+            v, rc = band(2)
+            pyoracle.render_frame(osc, cam, features, W, H, view=v, rect=rc, threads=threads)   # warm
+            v, rc = band(n)
+            t0 = time.perf_counter()
+            pyoracle.render_frame(osc, cam, features, W, H, view=v, rect=rc, threads=threads)
+            return time.perf_counter() - t0
+        finally:
+            pyoracle.set_rng_mode(False)
+
     px = W * rows * features.num_samples_in_reservoir
+    dt = timed(False, rows)
+    # the reference's generators serialise on glibc's rand() lock (~100x slower on 16 threads): an eighth of the
+    # rows keeps the leg near 5 s
+    rows_ref = max(32, rows // 8)
+    dt_ref = timed(True, rows_ref)
+    px_ref = W * rows_ref * features.num_samples_in_reservoir
     return {"value": round(px / dt / 1e6, 6), "unit": "Mpixel-reservoirs/s", "cores": threads, "kind": "port",
             "sample": f"oracle/restir_oracle.c frame (primary+RIS+spatial+final) owning rows {y0}..{y0 + rows - 1} "
                       f"of the {W}x{H} workload ({W * rows} px counted, +{2 * g} ghost rows computed, {dt:.2f} s, "
-                      f"OpenMP {threads} threads)"}
+                      f"OpenMP {threads} threads, keyed counter RNG)",
+            # the same frame with the reference's own generators (per-pixel std::random_device + std::mt19937,
+            # process-wide rand(); light.cpp:49-51, reservoir.cpp:24, render_utils.cpp:89-91) -- how the
+            # reference itself runs; not reproducible, so timed only
+            "reference_rng": {"value": round(px_ref / dt_ref / 1e6, 6), "unit": "Mpixel-reservoirs/s", "cores": threads,
+                              "seconds": round(dt_ref, 3), "rows": rows_ref, "ghost_rows_computed": 2 * g,
+                              "rng": "per-pixel std::random_device + std::mt19937, global rand() (oracle/ref_rng.cpp)"}}
 
 
 # BASELINE.json configs.  "weak": each rank owns a tile x tile_h tile of a (tx*tile) x (ty*tile_h) image;
@@ -310,6 +330,21 @@ def main():
 
     kernels = {k: {"us_per_launch": round(v[0] / v[1] * 1e3, 2) if v[1] else None, "launches": int(v[1])}
                for k, v in kt_all.items()}
+    # roofline of initial RIS (the frame's largest kernel): SURVEY.md §8(d) prices a candidate at ~160 flop
+    # (target pdf incl. sqrt, divisions and powf, the weight and the reservoir update); candidates per launch =
+    # the launch's pixels x M.  The fused k_primary_ris also traces the primary rays, which are not counted.
+    # Its time comes from the separate all-kernel run above (HIP events on the kernel's own dispatch).
+    roofline_ris = None
+    rk = "primary_ris" if kt_all.get("primary_ris", (0, 0))[1] else "ris"
+    rms, rn = kt_all.get(rk, (0.0, 0))
+    if rn:
+        cand = tile.width * tile.height * cf["M"]
+        avg_s = rms / rn / 1e3
+        tf = cand * RIS_FLOP_PER_CANDIDATE / avg_s / 1e12
+        roofline_ris = {"kernel": "k_primary_ris" if rk == "primary_ris" else "k_ris", "bound": "valu",
+                        "achieved": round(tf, 2), "peak": FP32_VECTOR_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": round(tf / FP32_VECTOR_PEAK_TFS, 4), "flop_per_candidate": RIS_FLOP_PER_CANDIDATE,
+                        "candidates_per_launch": cand, "avg_launch_us": round(avg_s * 1e6, 2)}
     kernels["note"] = "separate run after the timed region, every kernel's dispatch recording HIP events"
     if rank == 0:
         out = {
@@ -327,6 +362,7 @@ def main():
             "data": f"synthetic ({DATA[cf['scene']]}, keyed RNG seed 0x5EED0001)",
             "config": cfg,
             "roofline": roofline,
+            "roofline_ris": roofline_ris,
             "cpu_baseline": cpu,
             "kernels": kernels,
         }

@@ -49,6 +49,7 @@ def lib() -> C.CDLL:
             "or_scene_num_triangles": (u32, [P]),
             "or_scene_miss_material": (u32, [P]),
             "or_rng_key": (u32, [u32, u32, u32, u32]),
+            "or_set_rng_mode": (None, [C.c_int]),
             "or_rng_draw": (u32, [u32, u32, u32]),
             "or_glm_probe": (None, [FP, FP, C.c_float, FP, FP]),
             "or_tonemap": (None, [FP, C.c_float, C.c_float, FP]),
@@ -84,6 +85,12 @@ def lib() -> C.CDLL:
             fn.argtypes = args
         _lib = l
     return _lib
+
+
+def set_rng_mode(reference: bool) -> None:
+    """CPU-baseline timing mode: the reference's own generators (oracle/ref_rng.cpp) instead of the keyed draws.
+    Results are then not reproducible; bench.py only times it."""
+    lib().or_set_rng_mode(1 if reference else 0)
 
 
 def fp(a: np.ndarray | None):

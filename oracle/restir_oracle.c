@@ -80,6 +80,18 @@ static inline float rand01(uint32_t d) {
 static inline uint32_t uniform_index(uint32_t d, uint32_t n) { return (uint32_t)(((uint64_t)d * n) >> 32); }
 static inline int uniform_offset(uint32_t d, uint32_t r) { return (int)uniform_index(d, 2u * r + 1u) - (int)r; }
 
+/* CPU-baseline timing mode (or_set_rng_mode(1)): the reference's own generators (oracle/ref_rng.cpp --
+ * per-pixel std::random_device + std::mt19937 + uniform_int_distribution, process-wide rand()) replace the keyed
+ * draws at the same call sites.  Not reproducible, never used for parity: bench.py times it beside the keyed mode. */
+void or_refrng_pixel_seed(void);
+int or_refrng_uniform(int lo, int hi);
+void or_refrng_shared_seed(void);
+int or_refrng_shared_uniform(int lo, int hi);
+float or_refrng_rand01(void);
+static int g_ref_rng = 0;
+void or_set_rng_mode(int mode) { g_ref_rng = mode != 0; }
+#define U01(ps, slot) (g_ref_rng ? or_refrng_rand01() : rand01(draw((ps), (slot))))
+
 /* ------------------------------------------------------------------------------------------------------ */
 /* Scene: flat triangle list + material table (+1 miss material) + lights                                 */
 struct or_scene {
@@ -447,28 +459,30 @@ void or_ris(const or_scene* s, const restir_features* f, uint32_t key, const flo
             if (L != 0) {
                 or_px px = load_px(s, n_t, p_mat, p, origin);
                 uint32_t ps = pix_state(key, y * W + x);
+                if (g_ref_rng) or_refrng_pixel_seed();   /* light.cpp:49-51 */
                 for (uint32_t j = 0; j < N; j++) r[j].M = 0u;   /* light.cpp:58-60 */
                 for (uint32_t c = 0; c < f->initial_light_samples; c++) {
-                    const restir_light* light = &s->lights[uniform_index(draw(ps, 4u * c), L)];
+                    const uint32_t li = g_ref_rng ? (uint32_t)or_refrng_uniform(0, (int)L - 1) : uniform_index(draw(ps, 4u * c), L);
+                    const restir_light* light = &s->lights[li];
                     v3 pos, col;
                     if (light->type == RESTIR_LIGHT_POINT) {
                         pos = ld3(light->p0); col = ld3(light->c0);
                     } else if (light->type == RESTIR_LIGHT_SEGMENT) {
                         /* sampleSegmentLight (light.cpp:19-23) */
-                        float fr = rand01(draw(ps, 4u * c + 1u));
+                        float fr = U01(ps, 4u * c + 1u);
                         pos = vmix(ld3(light->p0), ld3(light->p1), fr);
                         col = vmix(ld3(light->c0), ld3(light->c1), fr);
                     } else {
                         /* sampleParallelogramLight (light.cpp:27-34) */
-                        float a = rand01(draw(ps, 4u * c + 1u));
-                        float b = rand01(draw(ps, 4u * c + 2u));
+                        float a = U01(ps, 4u * c + 1u);
+                        float b = U01(ps, 4u * c + 2u);
                         pos = vadd(vadd(ld3(light->p0), vscale(ld3(light->p1), a)), vscale(ld3(light->p2), b));
                         v3 l01 = vmix(ld3(light->c0), ld3(light->c1), a);
                         v3 l23 = vmix(ld3(light->c2), ld3(light->c3), a);
                         col = vmix(l01, l23, b);
                     }
                     float w = target_pdf(f, &px, pos, col) / (1.0f / (float)L);   /* light.cpp:80 */
-                    res_update(r, N, pos, col, w, rand01(draw(ps, 4u * c + 3u)));
+                    res_update(r, N, pos, col, w, U01(ps, 4u * c + 3u));
                 }
                 for (uint32_t j = 0; j < N; j++) {   /* light.cpp:85-95 */
                     if (f->initial_samples_visibility_check && !visible(s, px.P, r[j].pos)) {
@@ -495,7 +509,7 @@ static void combine_biased(const restir_features* f, const or_px* cur, const or_
             const or_sub* in = &stream[i * N + j];
             float p = target_pdf(f, cur, in->pos, in->col);
             float w = (p * in->W) * (float)in->M;
-            uint32_t k = res_update(out, N, in->pos, in->col, w, rand01(draw(ps, slot0 + t)));
+            uint32_t k = res_update(out, N, in->pos, in->col, w, U01(ps, slot0 + t));
             t++;
             macc[k] += in->M;
         }
@@ -552,6 +566,7 @@ int or_spatial_pass(const or_scene* s, const restir_features* f, uint32_t key, c
     const size_t npx = (size_t)view.w * view.h;
     const v3 origin = ld3(origin_);
     int bad = 0;
+    if (g_ref_rng) or_refrng_shared_seed();
 #pragma omp parallel for schedule(guided) reduction(| : bad)
     for (int yy = 0; yy < (int)rect.h; yy++) {
         uint32_t y = rect.y0 + (uint32_t)yy;
@@ -563,9 +578,9 @@ int or_spatial_pass(const or_scene* s, const restir_features* f, uint32_t key, c
             or_px cur = load_px(s, n_t, p_mat, p, origin);
             uint32_t ps = pix_state(key, y * W + x);
             uint32_t nsel = 0;
-            for (uint32_t n = 0; n < K; n++) {
-                int nx = (int)x + uniform_offset(draw(ps, 2u * n), R);
-                int ny = (int)y + uniform_offset(draw(ps, 2u * n + 1u), R);
+            for (uint32_t n = 0; n < K; n++) {   /* the shared generator of render_utils.cpp:89-91 */
+                int nx = (int)x + (g_ref_rng ? or_refrng_shared_uniform(-(int)R, (int)R) : uniform_offset(draw(ps, 2u * n), R));
+                int ny = (int)y + (g_ref_rng ? or_refrng_shared_uniform(-(int)R, (int)R) : uniform_offset(draw(ps, 2u * n + 1u), R));
                 nx = nx < 0 ? 0 : (nx > (int)W - 1 ? (int)W - 1 : nx);   /* std::clamp to the image */
                 ny = ny < 0 ? 0 : (ny > (int)H - 1 ? (int)H - 1 : ny);
                 if (nx < (int)view.x0 || nx >= (int)(view.x0 + view.w) || ny < (int)view.y0 ||
@@ -598,7 +613,7 @@ int or_spatial_pass(const or_scene* s, const restir_features* f, uint32_t key, c
                         const or_sub* in = &stream[i * N + j];
                         float pd = target_pdf(f, &cur, in->pos, in->col);
                         float w = (pd * in->W) * (float)in->M;
-                        uint32_t k = res_update(out, N, in->pos, in->col, w, rand01(draw(ps, slot0 + t)));
+                        uint32_t k = res_update(out, N, in->pos, in->col, w, U01(ps, slot0 + t));
                         t++;
                         macc[k] += in->M;
                     }

@@ -291,8 +291,26 @@ __device__ __forceinline__ v3 shade(const SceneDev& s, const FeaturesDev& f, con
 }
 
 // target pdf = glm::length(computeShading(...)) (light.cpp:84, reservoir.cpp:49)
-__device__ __forceinline__ float target_pdf(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol) {
-    return vlength(shade_ref(s, f, px, lpos, lcol));
+__device__ __forceinline__ float target_pdf(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,
+                                            const GlTabs& tb = gl_global_tabs()) {
+    return vlength(shade_ref(s, f, px, lpos, lcol, tb));
+}
+
+// The block's LDS copy of powf's two tables (512 B): every p-hat evaluation indexes them twice per lane, and from
+// __constant__ memory each index is a vector-memory round trip in the middle of the dependent chain (two per
+// target pdf); from LDS it is a ds_read.  Every thread of the block must call this (it ends with a barrier).
+__device__ __forceinline__ GlTabs gl_stage_tables() {
+    __shared__ double s_gl_log2[32];
+    __shared__ unsigned long long s_gl_exp2[32];
+    if (threadIdx.x < 32u) {
+        s_gl_log2[threadIdx.x] = kGlLog2Tab[threadIdx.x];
+        s_gl_exp2[threadIdx.x] = kGlExp2Tab[threadIdx.x];
+    }
+    __syncthreads();
+    GlTabs t;
+    t.log2 = s_gl_log2;
+    t.exp2 = s_gl_exp2;
+    return t;
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -537,7 +555,7 @@ template <int NT>
 __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                           const float4* lights, const Bvh& bvh, float4 nt, float4 pm, uint32_t x,
                                           uint32_t y, size_t p, float4* __restrict__ ra, float4* __restrict__ rb,
-                                          float2* __restrict__ rdbg, float* __restrict__ rp) {
+                                          float2* __restrict__ rdbg, float* __restrict__ rp, const GlTabs& tb) {
     const uint32_t L = s.num_lights;
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
@@ -587,18 +605,18 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
             for (; c < c_end; c++) {
                 v3 pos, col;
                 sample(c, pos, col);
-                const float pd = target_pdf(s, f, px, pos, col);
+                const float pd = target_pdf(s, f, px, pos, col, tb);
                 res_update<NT>(r, N, pos, col, weight(pd), rand01(draw(ps, 4u * c + 3u)), pd);
             }
             for (uint32_t j = 0; j < N; j++) {
                 // the held sample's target pdf: W's p-hat (light.cpp:90-93) and, N = 1, the pdf cache rp
-                const float pj = r[j].has_pd ? r[j].pd : target_pdf(s, f, px, r[j].pos, r[j].col);
+                const float pj = r[j].has_pd ? r[j].pd : target_pdf(s, f, px, r[j].pos, r[j].col, tb);
                 if (f.initial_vis && !visible(bvh, px.P, r[j].pos)) r[j].W = 0.0f;
                 else r[j].W = contribution_weight(pj, r[j].M, r[j].wsum);
                 if (NT == 1 && rp) rp[p] = pj;
             }
         } else if (NT == 1 && rp) {
-            rp[p] = target_pdf(s, f, make_px(s, nt, pm, origin, p), r[0].pos, r[0].col);   // no lights: the initial sample
+            rp[p] = target_pdf(s, f, make_px(s, nt, pm, origin, p), r[0].pos, r[0].col, tb);   // no lights: the initial sample
         }
         for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, ridx(rg, j, p), j * npx + p);
     }
@@ -619,13 +637,14 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
         lights = g_lds;
     }
     const Bvh bvh = global_bvh(s);
+    const GlTabs tb = gl_stage_tables();
     const uint32_t items = work_items(rg);
     WorkCursor cur(wq);
     for (uint32_t item = cur.first(); item < items; item = cur.next()) {
         uint32_t x, y;
         size_t p;
         if (!work_pixel(rg, item, x, y, p)) continue;
-        ris_pixel<NT>(s, rg, f, key, origin, lights, bvh, n_t[gidx(rg, p)], p_mat[p], x, y, p, ra, rb, rdbg, rp);
+        ris_pixel<NT>(s, rg, f, key, origin, lights, bvh, n_t[gidx(rg, p)], p_mat[p], x, y, p, ra, rb, rdbg, rp, tb);
     }
 }
 
@@ -646,6 +665,7 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         lights = g_lds + bvh_f4;
     }
     const Bvh bvh = stage_bvh(s, g_lds);   // ends with the barrier that also covers the light copy
+    const GlTabs tb = gl_stage_tables();
     const v3 origin = mk(cam.origin[0], cam.origin[1], cam.origin[2]);
     const uint32_t items = work_items(rg);
     for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {
@@ -654,7 +674,7 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         if (!work_pixel(rg, item, x, y, p)) continue;
         float4 nt, pm;
         primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, nt, pm);
-        ris_pixel<NT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp);
+        ris_pixel<NT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb);
     }
 }
 
@@ -995,7 +1015,7 @@ __device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& 
                                                const float4* __restrict__ ia, const float4* __restrict__ ib,
                                                float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
                                                const float* __restrict__ rp_in, float* __restrict__ rp_out,
-                                               uint32_t x, uint32_t y) {
+                                               uint32_t x, uint32_t y, const GlTabs& tb) {
     const uint32_t K = f.K;   // <= kLeanK (host check)
     const int rx = (int)(x - rg.vx0), ry = (int)(y - rg.vy0);
     const uint32_t pofs = ((uint32_t)ry * rg.vw + (uint32_t)rx) << 4;
@@ -1058,7 +1078,7 @@ __device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& 
     if (ok[0]) { na[0] = ld_at(ia, qo[0]); nb[0] = ld_at(ib, qo[0]); }
     // the pixel's own sample is consumed last; its target pdf does not depend on the stream, and when the
     // input's producer stored it (the pdf cache rp: same pixel, same G-buffer, same sample) it is read back
-    const float pd_cur = rp_in ? ld_at(rp_in, pofs >> 2) : target_pdf(s, f, cur, xyz(ca), xyz(cb));
+    const float pd_cur = rp_in ? ld_at(rp_in, pofs >> 2) : target_pdf(s, f, cur, xyz(ca), xyz(cb), tb);
     Comb1 cmb;
     cmb.pos = mk(0.0f, 0.0f, 0.0f); cmb.col = mk(0.0f, 0.0f, 0.0f);
     cmb.wsum = ROMIS_FLT_MIN; cmb.chosen = 0.0f; cmb.pd = 0.0f; cmb.macc = 0u; cmb.has_pd = false;
@@ -1068,7 +1088,7 @@ __device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& 
         if (n + 1 < kLeanK && ok[n + 1]) { na[n + 1] = ld_at(ia, qo[n + 1]); nb[n + 1] = ld_at(ib, qo[n + 1]); }
         if (ok[n]) {
             const v3 p = xyz(na[n]), c = xyz(nb[n]);
-            cmb.take(target_pdf(s, f, cur, p, c), na[n].w, __float_as_uint(nb[n].w), p, c);
+            cmb.take(target_pdf(s, f, cur, p, c, tb), na[n].w, __float_as_uint(nb[n].w), p, c);
         }
     }
     cmb.take(pd_cur, ca.w, __float_as_uint(cb.w), xyz(ca), xyz(cb));
@@ -1076,7 +1096,7 @@ __device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& 
     // nothing accepted: the held sample is the initial (0, 0) one, whose shaded value is +-0 at any pixel with
     // a non-NaN position (zero colour; NaN terms are zeroed; d >= 1e-5 or d = 1), so W = 0 (reservoir.cpp:62)
     float p = cmb.pd;
-    if (!cmb.has_pd) p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, cmb.pos, cmb.col);
+    if (!cmb.has_pd) p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, cmb.pos, cmb.col, tb);
     const float W = contribution_weight(p, cmb.macc, cmb.wsum);
     st_at(oa, pofs, make_float4(cmb.pos.x, cmb.pos.y, cmb.pos.z, W));
     st_at(ob, pofs, make_float4(cmb.col.x, cmb.col.y, cmb.col.z, __uint_as_float(cmb.macc)));
@@ -1112,8 +1132,9 @@ __device__ __forceinline__ void spatial1_body(const SceneDev& s, const Region& r
     // 32x8 tiles in the XCD order above, one per block; waves of 8x8 pixels (rg.map2d = 2)
     uint32_t tile, x, y;
     size_t p;
+    const GlTabs tb = gl_stage_tables();
     if (xcd_tile(rg, num_tiles(rg), blockIdx.x, tile) && tile_pixel_of(rg, tile, x, y, p))
-        spatial1_pixel<DBG>(s, rg, f, key, origin, n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out, x, y);
+        spatial1_pixel<DBG>(s, rg, f, key, origin, n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out, x, y, tb);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -1283,6 +1304,154 @@ ROMIS_SPATIAL1_LDS_KERNEL(true, true, ROMIS_SPATIAL1_LDS_WPE, k_spatial1_lds_dbg
 ROMIS_SPATIAL1_LDS_KERNEL(false, false, 3, k_spatial1_ldsr)
 ROMIS_SPATIAL1_LDS_KERNEL(true, false, 3, k_spatial1_ldsr_dbg)
 
+// k_spatial1_ntl: the N = 1 biased pass with only the tile's n_t neighbourhood staged in LDS.  The rocprof
+// counters of k_spatial1 (profiles/r2/r2q) put its bound in the vector-memory pipeline, not in HBM or VALU:
+// TA busy 66 %, TD busy 76 %, TA address path stalled by the L1 40 % of the time -- each 16-byte gather
+// instruction touches ~50 distinct 128-byte lines (one TA/L1 cycle each), against 8 for a coalesced one.
+// The five neighbour n_t gathers are the only ones every lane issues (the reservoir gathers follow only the
+// accepted neighbours), so they are the ones replaced: the block copies the (32 + 2R) x (8 + 2R) n_t window
+// (23 KB at R = 10, 6 blocks per CU) with row-coalesced loads, issued together with the pixel's own records.
+// The accepted neighbours' reservoirs stay global gathers, one neighbour ahead of the consume sequence (as in
+// spatial1_pixel).  Same arithmetic, RNG slots and update order as spatial1_pixel; R <= kLdsSpatialR.
+template <bool DBG>
+__device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
+                                                  v3 origin, const float4* __restrict__ n_t,
+                                                  const float4* __restrict__ p_mat, const float4* __restrict__ ia,
+                                                  const float4* __restrict__ ib, float4* __restrict__ oa,
+                                                  float4* __restrict__ ob, float2* __restrict__ odbg,
+                                                  const float* __restrict__ rp_in, float* __restrict__ rp_out) {
+    const GlTabs tb = gl_stage_tables();
+    float4* const l_nt = g_lds;
+    uint32_t tile;
+    if (!xcd_tile(rg, num_tiles(rg), blockIdx.x, tile)) return;   // block-uniform
+    const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
+    const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTileH);
+    // neighbour clamp bounds (render_utils.cpp:109-110: the image; here also the stored view), global coords
+    const int xlo = max(0, (int)rg.vx0), xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1;
+    const int ylo = max(0, (int)rg.vy0), yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1;
+    const int R = (int)f.R;
+    const int ax0 = max(tx0 - R, xlo), ax1 = min(tx0 + (int)kTileW - 1 + R, xhi);
+    const int ay0 = max(ty0 - R, ylo), ay1 = min(ty0 + (int)kTileH - 1 + R, yhi);
+    const uint32_t AW = (uint32_t)(ax1 - ax0 + 1), n_apron = AW * (uint32_t)(ay1 - ay0 + 1);
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    const int x = tx0 + (int)(w * 8u + (l & 7u)), y = ty0 + (int)(l >> 3);
+    const bool live = x < (int)(rg.rx0 + rg.rw) && y < (int)(rg.ry0 + rg.rh);
+    const uint32_t pofs = ((uint32_t)(y - (int)rg.vy0) * rg.vw + (uint32_t)(x - (int)rg.vx0)) << 4;
+    // the pixel's own records (coalesced), issued first
+    float4 cpm = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ca = cpm, cb = cpm;
+    float pd_cached = 0.0f;
+    if (live) {
+        cpm = ld_at(p_mat, pofs);
+        ca = ld_at(ia, pofs);
+        cb = ld_at(ib, pofs);
+        if (rp_in) pd_cached = ld_at(rp_in, pofs >> 2);
+    }
+    {
+        constexpr uint32_t kPer = (kApronMax + 255u) / 256u;
+        const uint32_t magic = 0xFFFFFFFFu / AW + 1u;   // i / AW for i < 2^16
+        float4 vn[kPer];
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++) {
+            const uint32_t i = threadIdx.x + 256u * k;
+            if (i < n_apron) {
+                uint32_t r = __umulhi(i, magic);
+                if (r * AW > i) r--;
+                const uint32_t c = i - r * AW;
+                vn[k] = ld_at(n_t, (((uint32_t)(ay0 - (int)rg.vy0) + r) * rg.vw + (uint32_t)(ax0 - (int)rg.vx0) + c) << 4);
+            }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++) {
+            const uint32_t i = threadIdx.x + 256u * k;
+            if (i < n_apron) l_nt[i] = vn[k];
+        }
+    }
+    // neighbour draws while the loads are in flight
+    const uint32_t K = f.K;   // <= kLeanK (host check)
+    const uint32_t ps = pix_state(key, (uint32_t)y * rg.W + (uint32_t)x);
+    const uint32_t span = 2u * f.R + 1u;
+    uint32_t qi[kLeanK], qo[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        qi[n] = 0u;
+        qo[n] = pofs;
+        if (n < K) {
+            const int nx = min(max(x - R + (int)__umulhi(draw(ps, 2u * n), span), xlo), xhi);
+            const int ny = min(max(y - R + (int)__umulhi(draw(ps, 2u * n + 1u), span), ylo), yhi);
+            qi[n] = (uint32_t)(ny - ay0) * AW + (uint32_t)(nx - ax0);
+            qo[n] = ((uint32_t)(ny - (int)rg.vy0) * rg.vw + (uint32_t)(nx - (int)rg.vx0)) << 4;
+        }
+    }
+    __syncthreads();
+    if (!live) return;   // no barrier follows
+    const float4 cn = l_nt[(uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0)];
+    const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
+    // primary-ray miss: the pass's result is known (spatial1_pixel)
+    if (cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z) &&
+        __builtin_isfinite(ca.w) && __builtin_isfinite(cb.x + cb.y + cb.z)) {
+        st_at(oa, pofs, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+        st_at(ob, pofs, make_float4(0.0f, 0.0f, 0.0f, cb.w));
+        if (DBG) st_at(odbg, pofs >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
+        if (rp_out) st_at(rp_out, pofs >> 2, 0.0f);
+        return;
+    }
+    // depth / normal heuristic (render_utils.cpp:114-118), one shared reciprocal of the pixel's depth
+    const double rt = rcp_d(cur.t);
+    const bool rt_ok = div_fast_ok(cur.t);
+    bool ok[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        ok[n] = false;
+        if (n < K) {
+            const float4 g = l_nt[qi[n]];
+            const float nd = vdot(xyz(g), cur.N);
+            bool rej = nd < 0.90630778703f;
+            if (!rej) {
+                float q = div_by_rcp_d(g.w, rt);
+                if (!rt_ok) q = g.w / cur.t;
+                rej = fabsf(1.0f - q) > 0.1f;
+            }
+            ok[n] = !rej;
+        }
+    }
+    float4 na[kLeanK], nb[kLeanK];
+    if (ok[0]) { na[0] = ld_at(ia, qo[0]); nb[0] = ld_at(ib, qo[0]); }
+    const float pd_cur = rp_in ? pd_cached : target_pdf(s, f, cur, xyz(ca), xyz(cb), tb);
+    Comb1 cmb;
+    cmb.pos = mk(0.0f, 0.0f, 0.0f); cmb.col = mk(0.0f, 0.0f, 0.0f);
+    cmb.wsum = ROMIS_FLT_MIN; cmb.chosen = 0.0f; cmb.pd = 0.0f; cmb.macc = 0u; cmb.has_pd = false;
+    cmb.h = ps + 2u * K * 0x9E3779B9u;
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        if (n + 1 < kLeanK && ok[n + 1]) { na[n + 1] = ld_at(ia, qo[n + 1]); nb[n + 1] = ld_at(ib, qo[n + 1]); }
+        if (ok[n]) {
+            const v3 p = xyz(na[n]), c = xyz(nb[n]);
+            cmb.take(target_pdf(s, f, cur, p, c, tb), na[n].w, __float_as_uint(nb[n].w), p, c);
+        }
+    }
+    cmb.take(pd_cur, ca.w, __float_as_uint(cb.w), xyz(ca), xyz(cb));
+    float p = cmb.pd;
+    if (!cmb.has_pd) p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, cmb.pos, cmb.col, tb);
+    const float W = contribution_weight(p, cmb.macc, cmb.wsum);
+    st_at(oa, pofs, make_float4(cmb.pos.x, cmb.pos.y, cmb.pos.z, W));
+    st_at(ob, pofs, make_float4(cmb.col.x, cmb.col.y, cmb.col.z, __uint_as_float(cmb.macc)));
+    if (DBG) st_at(odbg, pofs >> 1, make_float2(cmb.wsum, cmb.chosen));
+    if (rp_out) st_at(rp_out, pofs >> 2, p);
+}
+
+#ifndef ROMIS_SPATIAL1_NTL_WPE
+#define ROMIS_SPATIAL1_NTL_WPE 5
+#endif
+#define ROMIS_SPATIAL1_NTL_KERNEL(DBG, NAME)                                                                          \
+    extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL1_NTL_WPE))) void     \
+    NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
+         const float4* p_mat, const float4* ia, const float4* ib, float4* oa, float4* ob, float2* odbg,               \
+         const float* rp_in, float* rp_out) {                                                                         \
+        spatial1_ntl_body<DBG>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);       \
+    }
+ROMIS_SPATIAL1_NTL_KERNEL(false, k_spatial1_ntl)
+ROMIS_SPATIAL1_NTL_KERNEL(true, k_spatial1_ntl_dbg)
+
 #define ROMIS_SPATIAL1_KERNEL(DBG, NAME)                                                                              \
     extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL1_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f,     \
                                                                             uint32_t key, float ox, float oy, float oz, \
@@ -1305,6 +1474,7 @@ __device__ __forceinline__ void final_body(const SceneDev& s, const Region& rg, 
                                            const float4* __restrict__ ra, const float4* __restrict__ rb,
                                            float* __restrict__ rgb) {
     const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
+    const GlTabs tb = gl_stage_tables();
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
     const uint32_t nt = work_items(rg);
@@ -1318,7 +1488,7 @@ __device__ __forceinline__ void final_body(const SceneDev& s, const Region& rg, 
         for (uint32_t j = 0; j < N; j++) {
             Sub r;
             sub_load(r, ra, rb, ridx(rg, j, p));
-            v3 sc = shade(s, f, px, r.pos, r.col);
+            v3 sc = shade(s, f, px, r.pos, r.col, tb);
             // The visibility test can only matter when the shaded value is non-zero: (vis ? sc : 0) * W equals
             // sc * W when sc == 0 (both are 0 * W), so the shadow ray is skipped exactly then.
             if ((sc.x != 0.0f || sc.y != 0.0f || sc.z != 0.0f) && !visible(bvh, px.P, r.pos)) sc = mk(0.0f, 0.0f, 0.0f);
@@ -1328,9 +1498,9 @@ __device__ __forceinline__ void final_body(const SceneDev& s, const Region& rg, 
         color = vdivs(color, (float)N);
         if (f.tone_map) {
             v3 e = vscale(mk(-color.x, -color.y, -color.z), f.exposure);
-            v3 mapped = mk(1.0f - pm_expf(e.x), 1.0f - pm_expf(e.y), 1.0f - pm_expf(e.z));
+            v3 mapped = mk(1.0f - gl_expf(tb, e.x), 1.0f - gl_expf(tb, e.y), 1.0f - gl_expf(tb, e.z));
             // pm_powf(x, 1) == x for every x (gamma = 1, the Features default): skip the call
-            color = g == 1.0f ? mapped : mk(pm_powf(mapped.x, g), pm_powf(mapped.y, g), pm_powf(mapped.z, g));
+            color = g == 1.0f ? mapped : mk(gl_powf(tb, mapped.x, g), gl_powf(tb, mapped.y, g), gl_powf(tb, mapped.z, g));
         }
         const uint32_t row = rg.rh - 1u - (y - rg.ry0);
         float* o = rgb + 3 * ((size_t)row * rg.rw + (x - rg.rx0));
@@ -2216,7 +2386,10 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
             const uint32_t chunks = (nty + rg.xcd_rows - 1) / rg.xcd_rows;
             grid = 8u * ((chunks + 7u) / 8u) * rg.xcd_rows * ntx;
         }
-        if (tu.spatial_lds == 2u && f.R <= kLdsSpatialR) {
+        if (tu.spatial_lds == 3u && f.R <= kLdsSpatialR) {
+            ROMIS_LAUNCH(odbg ? k_spatial1_ntl_dbg : k_spatial1_ntl, dim3(grid), dim3(kBlock), kApronMax * 16u, stream,
+                         s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
+        } else if (tu.spatial_lds == 2u && f.R <= kLdsSpatialR) {
             ROMIS_LAUNCH(odbg ? k_spatial1_ldsr_dbg : k_spatial1_ldsr, dim3(grid), dim3(kBlock), 2u * kApronMax * 16u, stream,
                          s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
         } else if (tu.spatial_lds && f.R <= kLdsSpatialR) {

@@ -90,8 +90,8 @@ struct Tuning {
     uint32_t ris_lds = 1;          // stage the light table in LDS when it fits
     uint32_t ris_queue = 0;        // persistent blocks (this many) pulling tiles from a WorkQueue; 0 = off
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
-    uint32_t spatial_lds = 0;      // k_spatial1: stage the tile's neighbourhood in LDS (R <= 10): 1 n_t + reservoirs,
-                                   // 2 reservoirs only; both measured slower than the gathers
+    uint32_t spatial_lds = 3;      // k_spatial1: stage the tile's neighbourhood in LDS (R <= 10): 3 n_t only (default,
+                                   // k_spatial1_ntl), 1 n_t + reservoirs, 2 reservoirs only, 0 none (all gathers)
     uint32_t spatial_xcd_rows = 4; // k_spatial1: XCD x takes every 8th chunk of this many tile rows (0: one band)
     uint32_t spatial_blocks = 0;
     uint32_t spatial_wave8 = 1;

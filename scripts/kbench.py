@@ -21,7 +21,7 @@ import numpy as np  # noqa: E402
 from romis_amd import _abi, restir, scene  # noqa: E402
 
 DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 1, "ris.queue": 0,
-            "spatial.xcd": 1, "spatial.xcd_rows": 4, "spatial.lds": 0, "spatial.blocks": 0, "spatial.wave8": 1, "spatial.lean": 1, "fuse.primary_ris": 1, "bvh.max_leaf": 2, "final.blocks": 0, "final.lds": 1, "final.2d": 1,
+            "spatial.xcd": 1, "spatial.xcd_rows": 4, "spatial.lds": 3, "spatial.blocks": 0, "spatial.wave8": 1, "spatial.lean": 1, "fuse.primary_ris": 1, "bvh.max_leaf": 2, "final.blocks": 0, "final.lds": 1, "final.2d": 1,
             "final.sort": 0, "layout.records": 0}
 
 VARIANTS = {
@@ -42,6 +42,7 @@ VARIANTS = {
     "spatial_band": {"spatial.xcd_rows": 0},
     "spatial_lds": {"spatial.lds": 1},
     "spatial_ldsr": {"spatial.lds": 2},
+    "spatial_gather": {"spatial.lds": 0},
 
     "spatial_rows1": {"spatial.xcd_rows": 1},
     "spatial_rows2": {"spatial.xcd_rows": 2},

@@ -198,13 +198,15 @@ def test_temporal_bit_exact(gpu, oracle, N, clamp):
 
 
 # spatial kernels of an N = 1 biased pass: k_spatial1 (gathers; XCD order in 4-row chunks or one band),
-# k_spatial1_lds (n_t + reservoirs staged in LDS), k_spatial1_ldsr (reservoirs staged), the general kernel
+# k_spatial1_lds (n_t + reservoirs staged in LDS), k_spatial1_ldsr (reservoirs staged), k_spatial1_ntl (n_t
+# staged, the default), the general kernel
 SPATIAL_VARIANTS = {"gather": {"spatial.lean": 1, "spatial.lds": 0},
                     "gather_band": {"spatial.lean": 1, "spatial.lds": 0, "spatial.xcd_rows": 0},
                     "lds": {"spatial.lean": 1, "spatial.lds": 1},
                     "ldsr": {"spatial.lean": 1, "spatial.lds": 2},
+                    "ntl": {"spatial.lean": 1, "spatial.lds": 3},
                     "general": {"spatial.lean": 0}}
-SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 0, "spatial.xcd_rows": 4}
+SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 4}
 
 
 @pytest.mark.parametrize("name", ["nightclub_128pt", "cornell_parallelogram"])

@@ -232,7 +232,10 @@ def main():
     else:
         GW, GH, scaling = cf["image"][0], cf["image"][1], "strong"
     # multi-GPU temporal reuse needs the predecessor's reservoirs around each tile: halo-exchange frames
-    halo = world > 1 and (args.mode == "halo" or (args.mode == "auto" and cf["temporal"]))
+    # strong-scaling configs (c4 / c5: one image split over the ranks) and temporal ones exchange the reservoir
+    # halo before each spatial pass (the library's RCCL transport, overlapped with the pass's interior); weak-
+    # scaling c2 recomputes a ghost zone instead (no data-path communication)
+    halo = world > 1 and (args.mode == "halo" or (args.mode == "auto" and (cf["temporal"] or scaling == "strong")))
     sc = scene.bench_scene(cf["scene"])
     cam = scene.camera_for(cf["scene"], GW, GH)
     passes = cf["passes"]
@@ -308,7 +311,8 @@ def main():
     if sp_n:
         sp_px = tile.width * tile.height if halo else spatial_px_per_launch(tile, passes, args.r)
         bytes_per_launch = int(sp_px * (32 + 32 * args.N + 32 * args.N))
-        avg_s = sp_ms / sp_n / 1e3
+        # a halo pass is 1-5 launches (interior + border strips): average over passes, not launches
+        avg_s = sp_ms / (args.steps * passes if halo else sp_n) / 1e3
         achieved = bytes_per_launch / avg_s / 1e9
         traffic, traffic_src = (pmc_traffic(args.traffic_csv), args.traffic_csv) if args.traffic_csv else (None, None)
         if traffic is None:

@@ -46,8 +46,9 @@
 extern "C" {
 #endif
 
-#define RESTIR_ABI_VERSION 3   /* 2: restir_features gained the R-MIS / R-OMIS fields;
-                                  3: textures (restir_texture, restir_material.kd_texture, restir_mesh.texcoords) */
+#define RESTIR_ABI_VERSION 4   /* 2: restir_features gained the R-MIS / R-OMIS fields;
+                                  3: textures (restir_texture, restir_material.kd_texture, restir_mesh.texcoords);
+                                  4: halo passes split into interior / border, native RCCL halo transport */
 
 #define RESTIR_STAGE_RIS      1u
 #define RESTIR_STAGE_TEMPORAL 2u
@@ -352,7 +353,7 @@ restir_status restir_debug_math(restir_ctx* ctx, const float* x, const float* y,
  *                       returns the pack / unpack buffer sizes
  *   per spatial pass:   restir_halo_pack(send) -> move segment i of send to rank send[i].rank and receive
  *                       recv[i] from rank recv[i].rank (RCCL ncclSend/ncclRecv, torch.distributed, ...) ->
- *                       restir_halo_unpack(recv) -> restir_halo_spatial
+ *                       restir_halo_unpack(recv) -> restir_halo_spatial (or the split / native forms below)
  *   restir_halo_end     final shading of the owned tile; *out_next = the grid for the next frame's temporal reuse
  * Bit-identical to the same pixels of a single-GPU restir_render frame.  Buffers are device memory (or host
  * memory when host_memory != 0, staged by the library); pack returns after the buffer is written, unpack
@@ -364,6 +365,29 @@ restir_status restir_halo_pack(restir_ctx* ctx, void* send_buf, uint64_t bytes, 
 restir_status restir_halo_unpack(restir_ctx* ctx, const void* recv_buf, uint64_t bytes, int host_memory);
 restir_status restir_halo_spatial(restir_ctx* ctx);
 restir_status restir_halo_end(restir_ctx* ctx, restir_frame** out_next, float* out_rgb);
+
+/* A spatial pass in two launches, so that the exchange overlaps computation: the interior of the owned tile
+ * (pixels more than `radius` from every side that faces another tile: their neighbourhoods never reach the
+ * ring) reads no exchanged reservoir and may run as soon as the pass's pack is issued; the border strips run
+ * after the unpack.  Per pass: pack -> spatial_interior -> (exchange) -> unpack -> spatial_border.
+ * restir_halo_spatial == spatial_interior + spatial_border.  Same results either way. */
+restir_status restir_halo_spatial_interior(restir_ctx* ctx);
+restir_status restir_halo_spatial_border(restir_ctx* ctx);
+
+/* Native RCCL transport of the halo (the exchange runs inside the library, no host round trip).  One rank
+ * calls restir_rccl_unique_id and hands the RESTIR_RCCL_ID_BYTES bytes to every rank (any side channel);
+ * every rank then calls restir_halo_attach_rccl(ctx, id, nranks, rank) once (ncclCommInitRank on the context's
+ * device; the communicator lives with the context), or restir_halo_attach_comm with the caller's own
+ * ncclComm_t (not owned, it must outlive the context's use).  restir_halo_pass then runs one spatial pass of
+ * the frame begun by restir_halo_begin: pack on the context's stream; ncclGroupStart / ncclSend+ncclRecv per
+ * plan segment / ncclGroupEnd on the context's communication stream, ordered after the pack by an event; the
+ * interior pass on the context's stream concurrently with the transfer; unpack and border pass after it.
+ * Nothing synchronises the host.  librccl is loaded on first use (RESTIR_ERR_UNSUPPORTED when absent). */
+#define RESTIR_RCCL_ID_BYTES 128u
+restir_status restir_rccl_unique_id(void* out, size_t bytes);
+restir_status restir_halo_attach_rccl(restir_ctx* ctx, const void* unique_id, uint32_t nranks, uint32_t rank);
+restir_status restir_halo_attach_comm(restir_ctx* ctx, void* nccl_comm);
+restir_status restir_halo_pass(restir_ctx* ctx);
 
 /* Measured HBM read bandwidth of this device (the roofline's practical ceiling next to the 8 TB/s spec): a
  * streaming-read kernel over `bytes` (rounded down to 16 B; pass >= 1 GiB to defeat the 256 MB Infinity

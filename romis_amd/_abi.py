@@ -18,6 +18,7 @@ RESTIR_STAGE_NEIGHBOURS = 4
 RESTIR_DEFAULT_SEED = 0x5EED0001
 RESTIR_MAX_N = 32
 RESTIR_ROMIS_MAX_TECHNIQUES = 8
+RESTIR_RCCL_ID_BYTES = 128
 
 LIGHT_POINT, LIGHT_SEGMENT, LIGHT_PARALLELOGRAM = 0, 1, 2
 MODE_RESTIR, MODE_RMIS, MODE_ROMIS = 0, 1, 2
@@ -170,6 +171,12 @@ SIGNATURES = {
     "restir_halo_pack": (C.c_int, [_P, _P, C.c_uint64, C.c_int]),
     "restir_halo_unpack": (C.c_int, [_P, _P, C.c_uint64, C.c_int]),
     "restir_halo_spatial": (C.c_int, [_P]),
+    "restir_halo_spatial_interior": (C.c_int, [_P]),
+    "restir_halo_spatial_border": (C.c_int, [_P]),
+    "restir_rccl_unique_id": (C.c_int, [_P, C.c_size_t]),
+    "restir_halo_attach_rccl": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32]),
+    "restir_halo_attach_comm": (C.c_int, [_P, _P]),
+    "restir_halo_pass": (C.c_int, [_P]),
     "restir_halo_end": (C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_float)]),
     "restir_measure_read_bandwidth": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
     "restir_enable_timing": (C.c_int, [_P, C.c_int]),

@@ -5,6 +5,8 @@
 // buffers; every pass is one hand-written gfx950 kernel (kernels.hip) enqueued on the context's stream.
 #include "restir_c.h"
 
+#include <rccl/rccl.h>
+
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -14,6 +16,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <dlfcn.h>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -230,11 +233,22 @@ struct restir_ctx {
         CameraDev camd{};
         HaloSegs send{}, recv{};
         uint64_t send_bytes = 0, recv_bytes = 0;
+        uint32_t send_rank[RESTIR_MAX_HALO_SEGS] = {}, recv_rank[RESTIR_MAX_HALO_SEGS] = {};
         int cur = 0;
         bool fb_records = true;
-        bool rp_ok = false;   // the current grid's target-pdf cache is valid (restir_render's rp_ok)
+        bool rp_ok = false;          // the current grid's target-pdf cache is valid (restir_render's rp_ok)
+        bool interior_done = false;  // the current pass's interior launch is issued (restir_halo_spatial_interior)
+        bool part_rp = false;        // every launch of the current pass wrote the pdf cache
     } halo;
     DevBuf halo_scratch;
+    // native RCCL halo transport (restir_halo_attach_rccl / _comm, restir_halo_pass)
+    struct {
+        void* comm = nullptr;            // ncclComm_t
+        bool owned = false;              // created by restir_halo_attach_rccl (destroyed with the context)
+        hipStream_t stream = nullptr;    // communication stream
+        hipEvent_t packed = nullptr, moved = nullptr;
+        DevBuf send, recv;
+    } rccl;
 
     // stage API region
     Region stage_rg{};
@@ -695,6 +709,8 @@ restir_status restir_create(int device, restir_ctx** out) {
     return RESTIR_OK;
 }
 
+static void release_rccl(restir_ctx* c);   // (halo section)
+
 void restir_destroy(restir_ctx* c) {
     if (!c) return;
     {
@@ -708,6 +724,7 @@ void restir_destroy(restir_ctx* c) {
         for (Pending& p : c->pending) { (void)hipEventDestroy(p.start); (void)hipEventDestroy(p.stop); }
         for (hipEvent_t ev : c->free_events) (void)hipEventDestroy(ev);
         c->pool->close();   // frames still alive free their records themselves on release
+        release_rccl(c);
         (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -1515,6 +1532,8 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
     ST_TRY(ensure_records(c, t.gwidth, t.gheight, f.N, fb));
     c->stage_ok = false;
     h.send = send; h.recv = recv; h.send_bytes = send_b; h.recv_bytes = recv_b;
+    for (uint32_t i = 0; i < n; i++) { h.send_rank[i] = sg[i].rank; h.recv_rank[i] = rg_[i].rank; }
+    h.interior_done = false;
     ST_TRY(c->rgb.ensure((size_t)t.width * t.height * 12));
     c->rgb_w = t.width; c->rgb_h = t.height;
     h.W = width; h.H = height;
@@ -1585,23 +1604,242 @@ restir_status restir_halo_unpack(restir_ctx* c, const void* buf, uint64_t bytes,
     return RESTIR_OK;
 }
 
-restir_status restir_halo_spatial(restir_ctx* c) {
-    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
-    std::lock_guard<std::mutex> lk(c->mu);
+// The owned rectangle of a halo pass split into the interior -- pixels at least R from every side that faces
+// another tile, whose neighbourhoods (+-R, clamped to the image) stay inside the owned rectangle -- and up to
+// four border strips (bottom / top full width, left / right between them) that read the exchanged ring.
+// Per-pixel results do not depend on how the rectangle is split into launches (keyed RNG by global pixel id).
+struct HaloSplit {
+    Region part[5];   // part[0] = interior (may be empty), part[1..nb] = border strips
+    uint32_t nb;
+};
+static HaloSplit halo_split(const Region& owned, uint32_t R) {
+    const uint32_t x0 = owned.rx0, y0 = owned.ry0, x1 = x0 + owned.rw, y1 = y0 + owned.rh;
+    const uint32_t l = x0 > 0 ? R : 0u, r = x1 < owned.W ? R : 0u, b = y0 > 0 ? R : 0u, t = y1 < owned.H ? R : 0u;
+    const uint32_t ix0 = x0 + std::min(l, owned.rw), ix1 = std::max(ix0, x1 - std::min(r, owned.rw));
+    const uint32_t iy0 = y0 + std::min(b, owned.rh), iy1 = std::max(iy0, y1 - std::min(t, owned.rh));
+    auto rect = [&](uint32_t ax0, uint32_t ay0, uint32_t ax1, uint32_t ay1) {
+        Region q = owned;
+        q.rx0 = ax0; q.ry0 = ay0; q.rw = ax1 - ax0; q.rh = ay1 - ay0;
+        return q;
+    };
+    HaloSplit hs{};
+    hs.part[0] = rect(ix0, iy0, ix1, iy1);
+    hs.nb = 0;
+    if (iy0 > y0) hs.part[1 + hs.nb++] = rect(x0, y0, x1, iy0);
+    if (y1 > iy1) hs.part[1 + hs.nb++] = rect(x0, iy1, x1, y1);
+    if (iy1 > iy0 && ix0 > x0) hs.part[1 + hs.nb++] = rect(x0, iy0, ix0, iy1);
+    if (iy1 > iy0 && x1 > ix1) hs.part[1 + hs.nb++] = rect(ix1, iy0, x1, iy1);
+    return hs;
+}
+
+// one launch of the current pass over `rg` (a part of the owned rectangle); the pdf cache stays valid only if
+// every part wrote it
+static restir_status halo_spatial_part(restir_ctx* c, const Region& rg, bool& rp_written) {
     auto& h = c->halo;
-    if (!h.active || h.pass >= h.passes) return fail(RESTIR_ERR_STATE, "restir_halo_spatial: no pass left");
-    HIP_TRY(hipSetDevice(c->device));
     const int nxt = h.cur ^ 1;
     const FrameBufs fb{c, h.fb_records, (size_t)h.view.vw * h.view.vh, h.f.N};
     SceneDev sd;
     ST_TRY(scene_for(c, h.f, (size_t)h.view.vw * h.view.vh, sd));
+    bool wrote = false;
     TIMED(c, RESTIR_K_SPATIAL,
-          launch_spatial(sd, h.owned, h.f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_SPATIAL, h.pass), h.camd.origin,
+          launch_spatial(sd, rg, h.f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_SPATIAL, h.pass), h.camd.origin,
                          fb.nt(h.cur), c->p_mat.as<float4>(), fb.ra(h.cur), fb.rb(h.cur), fb.ra(nxt), fb.rb(nxt), nullptr,
-                         h.rp_ok ? fb.rp(h.cur) : nullptr, fb.rp(nxt), &h.rp_ok, c->tuning, c->stream));
-    h.cur = nxt;
-    h.pass++;
+                         h.rp_ok ? fb.rp(h.cur) : nullptr, fb.rp(nxt), &wrote, c->tuning, c->stream));
+    rp_written = rp_written && wrote;
     return RESTIR_OK;
+}
+
+static restir_status halo_interior_locked(restir_ctx* c) {
+    auto& h = c->halo;
+    if (!h.active || h.pass >= h.passes || h.interior_done)
+        return fail(RESTIR_ERR_STATE, "restir_halo_spatial_interior: no pass pending");
+    HIP_TRY(hipSetDevice(c->device));
+    const HaloSplit hs = halo_split(h.owned, h.f.R);
+    h.part_rp = true;
+    if (hs.part[0].rw && hs.part[0].rh) ST_TRY(halo_spatial_part(c, hs.part[0], h.part_rp));
+    h.interior_done = true;
+    return RESTIR_OK;
+}
+
+static restir_status halo_border_locked(restir_ctx* c) {
+    auto& h = c->halo;
+    if (!h.active || h.pass >= h.passes || !h.interior_done)
+        return fail(RESTIR_ERR_STATE, "restir_halo_spatial_border before the pass's interior");
+    HIP_TRY(hipSetDevice(c->device));
+    const HaloSplit hs = halo_split(h.owned, h.f.R);
+    for (uint32_t i = 1; i <= hs.nb; i++) ST_TRY(halo_spatial_part(c, hs.part[i], h.part_rp));
+    h.rp_ok = h.part_rp;
+    h.cur ^= 1;
+    h.pass++;
+    h.interior_done = false;
+    return RESTIR_OK;
+}
+
+restir_status restir_halo_spatial_interior(restir_ctx* c) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    return halo_interior_locked(c);
+}
+
+restir_status restir_halo_spatial_border(restir_ctx* c) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    return halo_border_locked(c);
+}
+
+restir_status restir_halo_spatial(restir_ctx* c) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->halo.interior_done) ST_TRY(halo_interior_locked(c));
+    return halo_border_locked(c);
+}
+
+// ---- native RCCL transport ----------------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+struct RcclApi {
+    bool ok = false;
+    std::string why;
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const RcclApi& rccl_api() {
+    static RcclApi api = [] {
+        RcclApi a;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) { a.why = dlerror() ? dlerror() : "librccl.so.1 not found"; return a; }
+        bool all = true;
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            all = all && fn != nullptr;
+        };
+        sym(a.get_unique_id, "ncclGetUniqueId");
+        sym(a.comm_init_rank, "ncclCommInitRank");
+        sym(a.comm_destroy, "ncclCommDestroy");
+        sym(a.send, "ncclSend");
+        sym(a.recv, "ncclRecv");
+        sym(a.group_start, "ncclGroupStart");
+        sym(a.group_end, "ncclGroupEnd");
+        sym(a.error_string, "ncclGetErrorString");
+        a.ok = all;
+        if (!all) a.why = "librccl lacks a symbol";
+        return a;
+    }();
+    return api;
+}
+}  // namespace
+
+extern "C" {
+
+#define RCCL_TRY(expr)                                                                                            \
+    do {                                                                                                          \
+        const ncclResult_t rc_ = (expr);                                                                          \
+        if (rc_ != ncclSuccess)                                                                                   \
+            return fail(RESTIR_ERR_COMM, "%s: %s", #expr, rccl_api().error_string(rc_));                           \
+    } while (0)
+
+static void release_rccl(restir_ctx* c) {
+    auto& q = c->rccl;
+    if (q.comm && q.owned && rccl_api().ok) (void)rccl_api().comm_destroy(static_cast<ncclComm_t>(q.comm));
+    q.comm = nullptr;
+    q.owned = false;
+    if (q.packed) (void)hipEventDestroy(q.packed);
+    if (q.moved) (void)hipEventDestroy(q.moved);
+    if (q.stream) (void)hipStreamDestroy(q.stream);
+    q.packed = q.moved = nullptr;
+    q.stream = nullptr;
+    q.send.release();
+    q.recv.release();
+}
+
+static restir_status attach_comm_locked(restir_ctx* c, void* comm, bool owned) {
+    auto& q = c->rccl;
+    if (!q.stream) HIP_TRY(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+    if (!q.packed) HIP_TRY(hipEventCreateWithFlags(&q.packed, hipEventDisableTiming));
+    if (!q.moved) HIP_TRY(hipEventCreateWithFlags(&q.moved, hipEventDisableTiming));
+    if (q.comm && q.owned) RCCL_TRY(rccl_api().comm_destroy(static_cast<ncclComm_t>(q.comm)));
+    q.comm = comm;
+    q.owned = owned;
+    return RESTIR_OK;
+}
+
+restir_status restir_rccl_unique_id(void* out, size_t bytes) {
+    if (!out || bytes < RESTIR_RCCL_ID_BYTES) return fail(RESTIR_ERR_INVALID, "restir_rccl_unique_id: need %u bytes", RESTIR_RCCL_ID_BYTES);
+    static_assert(sizeof(ncclUniqueId) == RESTIR_RCCL_ID_BYTES, "ncclUniqueId size");
+    const RcclApi& api = rccl_api();
+    if (!api.ok) return fail(RESTIR_ERR_UNSUPPORTED, "RCCL unavailable: %s", api.why.c_str());
+    ncclUniqueId id;
+    RCCL_TRY(api.get_unique_id(&id));
+    std::memcpy(out, &id, sizeof(id));
+    return RESTIR_OK;
+}
+
+restir_status restir_halo_attach_rccl(restir_ctx* c, const void* unique_id, uint32_t nranks, uint32_t rank) {
+    if (!c || !unique_id || nranks == 0 || rank >= nranks) return fail(RESTIR_ERR_INVALID, "restir_halo_attach_rccl: bad argument");
+    const RcclApi& api = rccl_api();
+    if (!api.ok) return fail(RESTIR_ERR_UNSUPPORTED, "RCCL unavailable: %s", api.why.c_str());
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof(id));
+    ncclComm_t comm = nullptr;
+    RCCL_TRY(api.comm_init_rank(&comm, (int)nranks, id, (int)rank));
+    return attach_comm_locked(c, comm, true);
+}
+
+restir_status restir_halo_attach_comm(restir_ctx* c, void* nccl_comm) {
+    if (!c || !nccl_comm) return fail(RESTIR_ERR_INVALID, "restir_halo_attach_comm: null argument");
+    const RcclApi& api = rccl_api();
+    if (!api.ok) return fail(RESTIR_ERR_UNSUPPORTED, "RCCL unavailable: %s", api.why.c_str());
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    return attach_comm_locked(c, nccl_comm, false);
+}
+
+restir_status restir_halo_pass(restir_ctx* c) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    auto& h = c->halo;
+    auto& q = c->rccl;
+    if (!q.comm) return fail(RESTIR_ERR_STATE, "restir_halo_pass before restir_halo_attach_rccl / _comm");
+    if (!h.active || h.pass >= h.passes || h.interior_done) return fail(RESTIR_ERR_STATE, "restir_halo_pass: no pass pending");
+    const RcclApi& api = rccl_api();
+    HIP_TRY(hipSetDevice(c->device));
+    ST_TRY(q.send.ensure(std::max<uint64_t>(h.send_bytes, 16)));
+    ST_TRY(q.recv.ensure(std::max<uint64_t>(h.recv_bytes, 16)));
+    const FrameBufs fb{c, h.fb_records, (size_t)h.view.vw * h.view.vh, h.f.N};
+    // context stream: pack (after the previous pass's transfer released the send buffer -- stream order:
+    // the previous pass waited on q.moved before its unpack)
+    HIP_TRY(launch_halo_pack(h.view, h.send, h.f.N, fb.ra(h.cur), fb.rb(h.cur), q.send.as<float4>(), c->stream));
+    HIP_TRY(hipEventRecord(q.packed, c->stream));
+    // communication stream: the grouped point-to-point transfer of every plan segment
+    HIP_TRY(hipStreamWaitEvent(q.stream, q.packed, 0));
+    const ncclComm_t comm = static_cast<ncclComm_t>(q.comm);
+    if (h.send.n) {
+        RCCL_TRY(api.group_start());
+        for (uint32_t i = 0; i < h.send.n; i++) {
+            const uint64_t so = (uint64_t)h.send.px0[i] * h.f.N * 32u, sb = (uint64_t)h.send.w[i] * h.send.h[i] * h.f.N * 32u;
+            const uint64_t ro = (uint64_t)h.recv.px0[i] * h.f.N * 32u, rb = (uint64_t)h.recv.w[i] * h.recv.h[i] * h.f.N * 32u;
+            RCCL_TRY(api.send(static_cast<const char*>(q.send.p) + so, sb, ncclUint8, (int)h.send_rank[i], comm, q.stream));
+            RCCL_TRY(api.recv(static_cast<char*>(q.recv.p) + ro, rb, ncclUint8, (int)h.recv_rank[i], comm, q.stream));
+        }
+        RCCL_TRY(api.group_end());
+    }
+    HIP_TRY(hipEventRecord(q.moved, q.stream));
+    // context stream: the interior overlaps the transfer; unpack + border strips after it
+    ST_TRY(halo_interior_locked(c));
+    HIP_TRY(hipStreamWaitEvent(c->stream, q.moved, 0));
+    HIP_TRY(launch_halo_unpack(h.view, h.recv, h.f.N, q.recv.as<float4>(), fb.ra(h.cur), fb.rb(h.cur), c->stream));
+    return halo_border_locked(c);
 }
 
 restir_status restir_halo_end(restir_ctx* c, restir_frame** out_next, float* out_rgb) {

@@ -14,10 +14,16 @@ from . import restir
 
 
 class HaloFrames:
-    """Renders this rank's tile of successive frames (restir_halo_begin .. restir_halo_end)."""
+    """Renders this rank's tile of successive frames (restir_halo_begin .. restir_halo_end).
+
+    transport "native" (default with the nccl backend): the library's own RCCL communicator moves the halo on a
+    communication stream while the pass's interior runs (restir_halo_pass) -- no host round trip, no device
+    synchronisation.  transport "torch": torch.distributed batch_isend_irecv on device tensors (nccl) or host
+    tensors (gloo, the CPU / single-GPU tests); the pass's interior is issued before the exchange and runs on the
+    GPU while the host drives it, the border strips after the unpack."""
 
     def __init__(self, renderer: "restir.Renderer", width: int, height: int, tiles: tuple, rank: int, features,
-                 group=None):
+                 group=None, transport: str | None = None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -30,6 +36,17 @@ class HaloFrames:
         self.send, self.recv = restir.halo_plan(width, height, tiles[0], tiles[1], rank, radius,
                                                 features.num_samples_in_reservoir)
         self.on_device = dist.get_backend(group) == "nccl"
+        self.transport = transport or ("native" if self.on_device else "torch")
+        if self.transport == "native":
+            # one rank draws the communicator id, every rank receives it over the torch group
+            idt = torch.zeros(restir._abi.RESTIR_RCCL_ID_BYTES, dtype=torch.uint8)
+            if dist.get_rank(group) == 0:
+                idt[:] = torch.frombuffer(bytearray(restir.rccl_unique_id()), dtype=torch.uint8)
+            if self.on_device:
+                idt = idt.to(torch.device("cuda", torch.cuda.current_device()))
+            dist.broadcast(idt, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+            self.r.halo_attach_rccl(bytes(idt.cpu().numpy().tobytes()), dist.get_world_size(group), dist.get_rank(group))
+            return
         dev = torch.device("cuda", torch.cuda.current_device()) if self.on_device else torch.device("cpu")
         sb = sum(s.bytes for s in self.send)
         rb = sum(s.bytes for s in self.recv)
@@ -51,10 +68,15 @@ class HaloFrames:
     def render(self, prev, camera, want_rgb: bool = True, want_grid: bool = True):
         """One frame: (rgb of the owned tile [h][w][3], row 0 = top, or None; ReservoirGrid for temporal reuse)."""
         sb, rb = self.r.halo_begin(prev, camera, self.W, self.H, self.f, self.tiles, self.rank)
+        if self.transport == "native":
+            for _ in range(self.passes):
+                self.r.halo_pass()
+            return self.r.halo_end(self.tile, want_rgb, want_grid)
         host = not self.on_device
         for _ in range(self.passes):
             self.r.halo_pack(self.sendbuf.data_ptr(), sb, host)
+            self.r.halo_spatial_interior()   # runs on the GPU while the exchange below is in flight
             self._exchange()
             self.r.halo_unpack(self.recvbuf.data_ptr(), rb, host)
-            self.r.halo_spatial()
+            self.r.halo_spatial_border()
         return self.r.halo_end(self.tile, want_rgb, want_grid)

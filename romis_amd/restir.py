@@ -126,6 +126,24 @@ class Renderer:
     def halo_spatial(self) -> None:
         check(self.lib, self.lib.restir_halo_spatial(self.ctx), "restir_halo_spatial")
 
+    def halo_spatial_interior(self) -> None:
+        """The current pass's interior (reads no exchanged reservoir): issue it before waiting on the exchange."""
+        check(self.lib, self.lib.restir_halo_spatial_interior(self.ctx), "restir_halo_spatial_interior")
+
+    def halo_spatial_border(self) -> None:
+        """The current pass's border strips (after the unpack); completes the pass."""
+        check(self.lib, self.lib.restir_halo_spatial_border(self.ctx), "restir_halo_spatial_border")
+
+    def halo_attach_rccl(self, unique_id: bytes, nranks: int, rank: int) -> None:
+        """Native RCCL halo transport: ncclCommInitRank on this context's device (restir_halo_attach_rccl)."""
+        buf = C.create_string_buffer(bytes(unique_id), _abi.RESTIR_RCCL_ID_BYTES)
+        check(self.lib, self.lib.restir_halo_attach_rccl(self.ctx, C.cast(buf, C.c_void_p), nranks, rank),
+              "restir_halo_attach_rccl")
+
+    def halo_pass(self) -> None:
+        """One spatial pass with the exchange over the attached communicator, overlapped with the interior."""
+        check(self.lib, self.lib.restir_halo_pass(self.ctx), "restir_halo_pass")
+
     def halo_end(self, tile, want_rgb: bool = True, want_grid: bool = True):
         out = C.c_void_p()
         rgb = np.zeros((tile.height, tile.width, 3), np.float32) if want_rgb else None
@@ -274,6 +292,14 @@ class Renderer:
 
 def rng_key(seed: int, frame: int, stage: int, pass_: int = 0) -> int:
     return _abi.load_library().restir_rng_key(seed, frame, stage, pass_)
+
+
+def rccl_unique_id() -> bytes:
+    """restir_rccl_unique_id: the RESTIR_RCCL_ID_BYTES bytes one rank hands to all (ncclGetUniqueId)."""
+    lib = _abi.load_library()
+    buf = C.create_string_buffer(_abi.RESTIR_RCCL_ID_BYTES)
+    check(lib, lib.restir_rccl_unique_id(C.cast(buf, C.c_void_p), _abi.RESTIR_RCCL_ID_BYTES), "restir_rccl_unique_id")
+    return buf.raw
 
 
 def halo_plan(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, radius: int, N: int):

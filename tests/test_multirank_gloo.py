@@ -64,7 +64,7 @@ def _worker(rank, world, port, tiles, passes, result_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,tiles,passes", [(2, (2, 1), 1), (2, (1, 2), 2), (4, (2, 2), 1)])
+@pytest.mark.parametrize("world,tiles,passes", [(2, (2, 1), 1), (2, (1, 2), 2), (4, (2, 2), 1), (8, (4, 2), 1)])
 def test_tiles_over_gloo_ranks_match_single_frame(tmp_path, world, tiles, passes, abi_lib, oracle):
     result = str(tmp_path / "result.txt")
     mp.spawn(_worker, args=(world, _free_port(), tiles, passes, result), nprocs=world, join=True)
@@ -73,7 +73,7 @@ def test_tiles_over_gloo_ranks_match_single_frame(tmp_path, world, tiles, passes
 
 
 # ---- halo-exchange mode (restir_halo_plan) with temporal reuse ------------------------------------------------
-def _halo_worker(rank, world, port, tiles, passes, frames, result_path):
+def _halo_worker(rank, world, port, tiles, passes, frames, result_path, name="nightclub_128pt"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
@@ -86,7 +86,6 @@ def _halo_worker(rank, world, port, tiles, passes, frames, result_path):
     R = f.spatial_resample_radius
     t = restir.tile_plan(W, H, tiles[0], tiles[1], rank, R)
     send, recv = restir.halo_plan(W, H, tiles[0], tiles[1], rank, R, N)
-    name = "nightclub_128pt"
     sc = scene.bench_scene(name)
     cam = scene.camera_for(name, W, H)
     osc = pyoracle.OracleScene(sc)
@@ -158,11 +157,13 @@ def _halo_worker(rank, world, port, tiles, passes, frames, result_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,tiles,passes", [(2, (2, 1), 2), (4, (2, 2), 1), (4, (2, 2), 2)])
-def test_halo_exchange_with_temporal_matches_single_frames(tmp_path, world, tiles, passes, abi_lib, oracle):
+@pytest.mark.parametrize("world,tiles,passes,name", [(2, (2, 1), 2, "nightclub_128pt"), (4, (2, 2), 1, "nightclub_128pt"),
+                                                    (4, (2, 2), 2, "nightclub_128pt"), (8, (4, 2), 2, "nightclub_128pt"),
+                                                    (8, (4, 2), 1, "cornell_1024")])
+def test_halo_exchange_with_temporal_matches_single_frames(tmp_path, world, tiles, passes, name, abi_lib, oracle):
     """The halo protocol (restir_halo_plan segments, pack order [pixel][res_a, res_b], ring refilled before every
     pass) reproduces a 3-frame temporal sequence of single-process frames bit-for-bit."""
     result = str(tmp_path / "result.txt")
-    mp.spawn(_halo_worker, args=(world, _free_port(), tiles, passes, 3, result), nprocs=world, join=True)
+    mp.spawn(_halo_worker, args=(world, _free_port(), tiles, passes, 3, result, name), nprocs=world, join=True)
     with open(result) as fh:
         assert fh.read() == "ok"

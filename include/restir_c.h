@@ -48,7 +48,8 @@ extern "C" {
 
 #define RESTIR_ABI_VERSION 4   /* 2: restir_features gained the R-MIS / R-OMIS fields;
                                   3: textures (restir_texture, restir_material.kd_texture, restir_mesh.texcoords);
-                                  4: halo passes split into interior / border, native RCCL halo transport */
+                                  4: halo passes split into interior / border, native RCCL halo transport,
+                                     frame output (8-bit BMP, Features JSON record) */
 
 #define RESTIR_STAGE_RIS      1u
 #define RESTIR_STAGE_TEMPORAL 2u
@@ -388,6 +389,32 @@ restir_status restir_rccl_unique_id(void* out, size_t bytes);
 restir_status restir_halo_attach_rccl(restir_ctx* ctx, const void* unique_id, uint32_t nranks, uint32_t rank);
 restir_status restir_halo_attach_comm(restir_ctx* ctx, void* nccl_comm);
 restir_status restir_halo_pass(restir_ctx* ctx);
+
+/* ---- frame output (pure host, no device needed) --------------------------------------------------------
+ * restir_rgb_to_rgba8: Screen::writeBitmapToFile's conversion (screen.cpp:45-51): glm::clamp(c, 0, 1), then
+ * glm::u8vec4(vec4(c, 1) * 255) (truncation toward zero), for `pixels` float RGB triples -> RGBA bytes.
+ * restir_encode_bmp / restir_write_bmp: that conversion of a width x height float RGB image (row 0 = top, the
+ * layout restir_render returns) written as stbi_write_bmp(path, w, h, 4, data) writes it (screen.cpp:55):
+ * BITMAPV4 header, 32 bpp BGRA rows bottom-up.  encode: out == NULL queries *length.
+ * restir_features_json: the configuration record renderRayTraced saves per render (render.cpp:281-287,
+ * cereal::JSONOutputArchive of struct Features, common.h:138-147), byte for byte; `extra` carries the Features
+ * fields the ReSTIR path does not read (NULL: the struct's defaults).  out == NULL queries *length (without the
+ * terminating NUL, which is written).  Non-finite gamma / exposure: RESTIR_ERR_INVALID (cereal throws). */
+typedef struct restir_features_record_extra {
+    uint8_t  enable_recursive;         /* false */
+    uint8_t  enable_hard_shadow;       /* true  */
+    uint8_t  enable_soft_shadow;       /* true  */
+    uint8_t  enable_normal_interp;     /* true  */
+    uint8_t  enable_accel_structure;   /* true  */
+    uint8_t  reserved[3];
+    uint32_t max_reflection_recursion; /* 5 */
+} restir_features_record_extra;
+restir_status restir_rgb_to_rgba8(const float* rgb, size_t pixels, uint8_t* rgba);
+restir_status restir_encode_bmp(const float* rgb, uint32_t width, uint32_t height, uint8_t* out, size_t capacity,
+                                size_t* length);
+restir_status restir_write_bmp(const char* path, const float* rgb, uint32_t width, uint32_t height);
+restir_status restir_features_json(const restir_features* features, const restir_features_record_extra* extra,
+                                   char* out, size_t capacity, size_t* length);
 
 /* Measured HBM read bandwidth of this device (the roofline's practical ceiling next to the 8 TB/s spec): a
  * streaming-read kernel over `bytes` (rounded down to 16 B; pass >= 1 GiB to defeat the 256 MB Infinity

@@ -12,9 +12,14 @@
 // The Scene / EmbreeInterface pair becomes Renderer::setScene (uploads materials, lights and the BVH once).
 #pragma once
 
+#include <ctime>
+#include <filesystem>
+#include <fstream>
+#include <iomanip>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <sstream>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -108,7 +113,32 @@ struct Screen {
     std::vector<float> rgb;
     Screen(int w, int h) : width(w), height(h), rgb(size_t(w) * size_t(h) * 3, 0.0f) {}
     float* pixel(int x, int yFromTop) { return &rgb[(size_t(yFromTop) * width + x) * 3]; }
+    // Screen::writeBitmapToFile (screen.cpp:45-56): clamp, x255, truncate, stbi_write_bmp byte for byte
+    void writeBitmapToFile(const std::filesystem::path& filePath) const {
+        check(restir_write_bmp(filePath.string().c_str(), rgb.data(), uint32_t(width), uint32_t(height)),
+              "restir_write_bmp");
+    }
 };
+
+// The configuration record renderRayTraced saves per render (render.cpp:281-287): <dir>/<currentTime()>.json,
+// currentTime() = "%d-%m-%Y %H-%M-%S" local time (utils.cpp:16-22), cereal's bytes (restir_features_json).
+inline std::filesystem::path saveFeaturesRecord(const restir_features& features, const std::filesystem::path& dir,
+                                                const restir_features_record_extra* extra = nullptr) {
+    size_t n = 0;
+    check(restir_features_json(&features, extra, nullptr, 0, &n), "restir_features_json");
+    std::string json(n + 1, '\0');
+    check(restir_features_json(&features, extra, json.data(), json.size(), &n), "restir_features_json");
+    json.resize(n);
+    if (!std::filesystem::exists(dir)) std::filesystem::create_directory(dir);
+    const std::time_t t = std::time(nullptr);
+    std::ostringstream name;
+    name << std::put_time(std::localtime(&t), "%d-%m-%Y %H-%M-%S") << ".json";
+    const std::filesystem::path path = dir / name.str();
+    std::ofstream out(path, std::ios::binary);
+    out << json;
+    if (!out) throw RestirError("saveFeaturesRecord: cannot write " + path.string());
+    return path;
+}
 
 // One sub-reservoir's state as reservoir.h:18-32 keeps it: outputSamples[j] = {position, color, W},
 // sampleNums[j] = M.

@@ -85,6 +85,13 @@ class Features(C.Structure):
                 ("mis_weight_rmis", C.c_uint32), ("progressive_update_mod", C.c_uint32)]
 
 
+class FeaturesRecordExtra(C.Structure):
+    """restir_features_record_extra: the Features fields only the configuration record carries."""
+    _fields_ = [("enable_recursive", C.c_uint8), ("enable_hard_shadow", C.c_uint8), ("enable_soft_shadow", C.c_uint8),
+                ("enable_normal_interp", C.c_uint8), ("enable_accel_structure", C.c_uint8),
+                ("reserved", C.c_uint8 * 3), ("max_reflection_recursion", C.c_uint32)]
+
+
 class HaloSegment(C.Structure):
     _fields_ = [("rank", C.c_uint32), ("x0", C.c_uint32), ("y0", C.c_uint32), ("width", C.c_uint32),
                 ("height", C.c_uint32), ("offset", C.c_uint64), ("bytes", C.c_uint64)]
@@ -177,6 +184,11 @@ SIGNATURES = {
     "restir_halo_attach_rccl": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32]),
     "restir_halo_attach_comm": (C.c_int, [_P, _P]),
     "restir_halo_pass": (C.c_int, [_P]),
+    "restir_rgb_to_rgba8": (C.c_int, [_P, C.c_size_t, _P]),
+    "restir_encode_bmp": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "restir_write_bmp": (C.c_int, [C.c_char_p, _P, C.c_uint32, C.c_uint32]),
+    "restir_features_json": (C.c_int, [C.POINTER(Features), C.POINTER(FeaturesRecordExtra), C.c_char_p, C.c_size_t,
+                                       C.POINTER(C.c_size_t)]),
     "restir_halo_end": (C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_float)]),
     "restir_measure_read_bandwidth": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
     "restir_enable_timing": (C.c_int, [_P, C.c_int]),

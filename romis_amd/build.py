@@ -30,8 +30,9 @@ SOURCES = [
     ("kernels.hip", ["-x", "hip"] + DEVICE),
     ("restir.cpp", ["-x", "hip"] + DEVICE),
     ("bvh.cpp", ["-x", "c++"]),
+    ("screen.cpp", ["-x", "c++"]),
 ]
-HEADERS = ["device_math.h", "restir_types.h", "launch.h", "bvh.h"]
+HEADERS = ["device_math.h", "restir_types.h", "launch.h", "bvh.h", "pow10_table.h"]
 
 
 def source_hash() -> str:

@@ -131,3 +131,39 @@ def test_threads_one_camera_each_match_oracle(tmp_path):
         assert np.array_equal(g[3 * n:6 * n].reshape(n, 3), b[:, :3]), f"camera {i} grid colour"
         assert np.array_equal(g[6 * n:7 * n], a[:, 3]), f"camera {i} grid W"
         assert np.array_equal(g[7 * n:8 * n], b[:, 3]), f"camera {i} grid M"
+
+
+SRC_OUT = os.path.join(ROOT, "tests", "cpp", "write_outputs.cpp")
+BIN_OUT = os.path.join(ROOT, "romis_amd", "_build", "write_outputs")
+
+
+def test_wrapper_frame_output(tmp_path, abi_lib):
+    """Screen::writeBitmapToFile and saveFeaturesRecord through the C++ wrapper (host only): the files hold exactly
+    restir_encode_bmp's / restir_features_json's bytes (both pinned to the reference in test_screen_output.py)."""
+    import ctypes as C
+    exe = build_cpp(SRC_OUT, BIN_OUT)
+    bmp = str(tmp_path / "out.bmp")
+    rec_dir = tmp_path / "renders"
+    out = subprocess.run([exe, bmp, str(rec_dir)], capture_output=True, text=True, check=True).stdout.strip()
+    rgb = np.zeros((3, 5, 3), np.float32)
+    for y in range(3):
+        for x in range(5):
+            rgb[y, x] = [np.float32(0.1) * x - np.float32(0.05), np.float32(0.4) * y, np.float32(1.2) - np.float32(0.2) * x]
+    n = C.c_size_t()
+    abi_lib.restir_encode_bmp(rgb.ctypes.data, 5, 3, None, 0, C.byref(n))
+    want = (C.c_uint8 * n.value)()
+    assert abi_lib.restir_encode_bmp(rgb.ctypes.data, 5, 3, want, n.value, C.byref(n)) == 0
+    with open(bmp, "rb") as fh:
+        assert fh.read() == bytes(want)
+    # <dir>/<dd-mm-YYYY HH-MM-SS>.json
+    name = os.path.basename(out)
+    assert os.path.dirname(out) == str(rec_dir) and len(name) == len("16-10-2026 18-58-00.json")
+    f = _abi.Features()
+    abi_lib.restir_features_default(C.byref(f))
+    f.gamma = 2.2
+    f.num_samples_in_reservoir = 4
+    abi_lib.restir_features_json(C.byref(f), None, None, 0, C.byref(n))
+    buf = C.create_string_buffer(n.value + 1)
+    assert abi_lib.restir_features_json(C.byref(f), None, buf, n.value + 1, C.byref(n)) == 0
+    with open(out, "rb") as fh:
+        assert fh.read() == buf.value

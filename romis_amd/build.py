@@ -26,8 +26,14 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f
           f"-I{CSRC}"]
 DEVICE = [f"--offload-arch={ARCH}", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-rdc"]
 
+# -fno-slp-vectorize: the SLP pass packs independent f32 multiplies / adds into v_pk_* ops, which issue at the
+# cost of an FMA (≈4.5 cycles per wave instruction on gfx950) instead of ≈2.4 for each scalar op, and need
+# v_mov shuffles to assemble their operand pairs; without it: RIS 354 -> 340 us, spatial 85 -> 81, final 104 -> 92
+# (kbench, profiles/r2/noslp), fewer VGPRs and no RIS scratch spill.  Results are identical (no contraction).
+KERNEL_FLAGS = ["-fno-slp-vectorize"]
+
 SOURCES = [
-    ("kernels.hip", ["-x", "hip"] + DEVICE),
+    ("kernels.hip", ["-x", "hip"] + DEVICE + KERNEL_FLAGS),
     ("restir.cpp", ["-x", "hip"] + DEVICE),
     ("bvh.cpp", ["-x", "c++"]),
     ("screen.cpp", ["-x", "c++"]),
@@ -43,7 +49,7 @@ def source_hash() -> str:
     for f in [SOURCES[0][0]] + HEADERS:
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(f.encode() + b"\0" + fh.read())
-    h.update(" ".join([c for c in COMMON + DEVICE if not c.startswith("-I")]).encode())   # flags, not paths
+    h.update(" ".join([c for c in COMMON + DEVICE + KERNEL_FLAGS if not c.startswith("-I")]).encode())   # flags, not paths
     return h.hexdigest()[:16]
 
 
@@ -81,14 +87,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
-def build_variant(name: str, defines: list[str]) -> str:
+def build_variant(name: str, defines: list[str], flags: list[str] | None = None) -> str:
     """Build _build/variants/<name>/libromis_amd.so with kernels.hip compiled under extra -D defines (launch-bound
-    knobs such as ROMIS_SPATIAL_WPE).  The host objects are the shipped ones."""
+    knobs such as ROMIS_SPATIAL_WPE) and compiler flags.  The host objects are the shipped ones."""
     build()
     vdir = os.path.join(OUT, "variants", name)
     os.makedirs(vdir, exist_ok=True)
     obj = os.path.join(vdir, "kernels.hip.o")
-    subprocess.check_call([HIPCC] + COMMON + SOURCES[0][1] + [f"-D{d}" for d in defines] +
+    subprocess.check_call([HIPCC] + COMMON + SOURCES[0][1] + [f"-D{d}" for d in defines] + list(flags or []) +
                           ["-c", os.path.join(CSRC, "kernels.hip"), "-o", obj])
     lib = os.path.join(vdir, "libromis_amd.so")
     objs = [obj] + [os.path.join(OUT, s + ".o") for s, _ in SOURCES[1:]]

@@ -227,31 +227,43 @@ __device__ __forceinline__ Px load_px(const SceneDev& s, const Region& rg, const
 //  - y = +-0 / NaN / +-inf are glibc's zeroinfnan(y) returns; otherwise of its special cases only a NaN base
 //    (whose NaN the caller's clean-up zeroes whatever its payload: cosTheta is never a signalling NaN), a
 //    negative base (invalid unless y is an integer, sign from y's parity) and a zero / subnormal base remain.
-__device__ __forceinline__ float material_pow(const GlTabs& tb, float x, const Px& px) {
+// material_pow in two parts.  pow_pre decides every case glibc settles without its log2 / exp2 core (returns
+// true with the power in pw); otherwise it returns false with the core's input in job: the (subnormal-adjusted)
+// bits of |x| and, in bit 31, glibc's sign_bias (negative base, odd integer exponent).  pow_core(job, y) is the
+// rest of __powf.  (Evaluating only the cores some lane needs, wave-compacted through LDS across batches of
+// candidates, was measured slower in RIS: 345 -> 393-591 us, the batch state costing occupancy -- DESIGN §6.)
+__device__ __forceinline__ bool pow_pre(float x, const Px& px, float& pw, uint32_t& job) {
     const uint32_t mode = __float_as_uint(px.ks_pm.w);
-    if (mode == ROMIS_POW_SKIP) return 1.0f;
+    if (mode == ROMIS_POW_SKIP) { pw = 1.0f; return true; }
     const uint32_t cls = __float_as_uint(px.pw.y);
     const float ax = fabsf(x);
     if (__builtin_expect(cls & ROMIS_PWC_SPECIAL, 0)) {
-        if (cls & ROMIS_PWC_ZERO) return 1.0f;
-        if (cls & ROMIS_PWC_NAN) return x == 1.0f ? 1.0f : __builtin_nanf("");
-        if (__builtin_isnan(x)) return x;
-        if (ax == 1.0f) return 1.0f;
-        return ((ax < 1.0f) == ((cls & ROMIS_PWC_PINF) != 0u)) ? 0.0f : __builtin_inff();
+        if (cls & ROMIS_PWC_ZERO) pw = 1.0f;
+        else if (cls & ROMIS_PWC_NAN) pw = x == 1.0f ? 1.0f : __builtin_nanf("");
+        else if (__builtin_isnan(x)) pw = x;
+        else if (ax == 1.0f) pw = 1.0f;
+        else pw = ((ax < 1.0f) == ((cls & ROMIS_PWC_PINF) != 0u)) ? 0.0f : __builtin_inff();
+        return true;
     }
     const bool neg_odd = __builtin_signbit(x) && (cls & ROMIS_PWC_ODD);
-    if (!(ax >= px.pw.x)) return __builtin_isnan(x) ? x : (neg_odd ? -0.0f : 0.0f);
-    if (x < 0.0f && !(cls & ROMIS_PWC_INT)) return __uint_as_float(0xffc00000u);
+    if (!(ax >= px.pw.x)) { pw = __builtin_isnan(x) ? x : (neg_odd ? -0.0f : 0.0f); return true; }
+    if (x < 0.0f && !(cls & ROMIS_PWC_INT)) { pw = __uint_as_float(0xffc00000u); return true; }
     uint32_t ix = __float_as_uint(ax);
     if (__builtin_expect(ix < 0x00800000u, 0)) {
         if (ix == 0u) {
             const float z = neg_odd ? -0.0f : 0.0f;
-            return (cls & ROMIS_PWC_NEG) ? 1.0f / z : z;
+            pw = (cls & ROMIS_PWC_NEG) ? 1.0f / z : z;
+            return true;
         }
         ix = (__float_as_uint(ax * 0x1p23f) & 0x7fffffffu) - (23u << 23);
     }
-    const double ylogx = (double)px.kd_sh.w * gl_log2_inline(tb, ix);
-    const uint32_t sign_bias = neg_odd ? 0x10000u : 0u;
+    job = ix | (neg_odd ? 0x80000000u : 0u);
+    return false;
+}
+
+__device__ __forceinline__ float pow_core(const GlTabs& tb, uint32_t job, float y) {
+    const double ylogx = (double)y * gl_log2_inline(tb, job & 0x7fffffffu);
+    const uint32_t sign_bias = (job >> 31) ? 0x10000u : 0u;
     if (__builtin_expect(((unsigned long long)__double_as_longlong(ylogx) >> 47 & 0xffffu) >= 0x80bfu, 0)) {
         if (ylogx > 0x1.fffffffd1d571p+6) return gl_xflowf(sign_bias, 0x1p97f);
         if (ylogx <= -150.0) return gl_xflowf(sign_bias, 0x1p-95f);
@@ -260,19 +272,30 @@ __device__ __forceinline__ float material_pow(const GlTabs& tb, float x, const P
     return gl_exp2_inline(tb, ylogx, sign_bias);
 }
 
-// computeShading (shading.cpp:7-34), general form: every IEEE special case, any material
-__device__ __forceinline__ v3 shade_ref(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,
-                                        const GlTabs& tb = gl_global_tabs()) {
-    if (!f.shading) return xyz(s.materials[3 * px.mat]);   // material.kd, not the albedo (shading.cpp:8)
-    v3 kd = xyz(px.kd_sh);
-    float d;   // glm::distance(hitPos, lightPos) == |lightPos - hitPos|, the length normalize() takes
-    v3 L = vnormalize_len(vsub(lpos, px.P), d);
-    float dotNL = vdot(px.N, L);
-    if (dotNL < 0.0f) return mk(0.0f, 0.0f, 0.0f);
-    v3 R = vnormalize(vsub(vscale(px.N, 2.0f * dotNL), L));
-    float cosTheta = vdot(R, px.V);
-    const float pw = material_pow(tb, cosTheta, px);
-    v3 diffuse = vscale(vmul(lcol, kd), dotNL);
+__device__ __forceinline__ float material_pow(const GlTabs& tb, float x, const Px& px) {
+    float pw;
+    uint32_t job;
+    return pow_pre(x, px, pw, job) ? pw : pow_core(tb, job, px.kd_sh.w);
+}
+
+// computeShading (shading.cpp:7-34) in two parts around the power.  shade_pre: the light direction and distance,
+// dotNL (a back-facing light, dotNL < 0, shades to exactly 0) and the power's argument cosTheta.
+struct ShadePre {
+    float d, dotNL, cosTheta;
+};
+__device__ __forceinline__ ShadePre shade_pre(const Px& px, v3 lpos) {
+    ShadePre r;
+    v3 L = vnormalize_len(vsub(lpos, px.P), r.d);   // d = glm::distance(hitPos, lightPos), the length normalize() takes
+    r.dotNL = vdot(px.N, L);
+    r.cosTheta = 0.0f;
+    if (r.dotNL < 0.0f) return r;
+    v3 R = vnormalize(vsub(vscale(px.N, 2.0f * r.dotNL), L));
+    r.cosTheta = vdot(R, px.V);
+    return r;
+}
+// shade_post: the terms, the reference's NaN clean-up and the distance falloff
+__device__ __forceinline__ v3 shade_post(const SceneDev& s, const Px& px, v3 lcol, float dotNL, float d, float pw) {
+    v3 diffuse = vscale(vmul(lcol, xyz(px.kd_sh)), dotNL);
     v3 specular = vscale(vmul(lcol, xyz(px.ks_pm)), pw);
     // The reference zeroes a term holding a NaN.  When every colour x reflectance product is finite (host
     // check, SceneDev::shade_finite), a term can only hold one through a non-finite dotNL / pow factor, so
@@ -283,6 +306,15 @@ __device__ __forceinline__ v3 shade_ref(const SceneDev& s, const FeaturesDev& f,
     }
     if (fabsf(d) < 1e-5f) d = 1.0f;
     return vdivs(vadd(diffuse, specular), d * d);
+}
+
+// computeShading (shading.cpp:7-34), general form: every IEEE special case, any material
+__device__ __forceinline__ v3 shade_ref(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,
+                                        const GlTabs& tb = gl_global_tabs()) {
+    if (!f.shading) return xyz(s.materials[3 * px.mat]);   // material.kd, not the albedo (shading.cpp:8)
+    const ShadePre sp = shade_pre(px, lpos);
+    if (sp.dotNL < 0.0f) return mk(0.0f, 0.0f, 0.0f);
+    return shade_post(s, px, lcol, sp.dotNL, sp.d, material_pow(tb, sp.cosTheta, px));
 }
 
 __device__ __forceinline__ v3 shade(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,

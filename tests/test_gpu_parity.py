@@ -467,11 +467,22 @@ def test_full_1080p_spatial_properties_and_sampled_parity(gpu, oracle):
         sl = slice(y0 * Wf, (y0 + 8) * Wf)
         assert_bits(a1[:, sl], a2[:, sl], f"band {y0} res_a")
         assert_bits(b1[:, sl], b2[:, sl], f"band {y0} res_b")
-    # G-buffer + RIS on sampled bands too
+    # initial RIS at full size on sampled bands: the GPU's own G-buffer fed to the oracle's RIS for those rows
+    import ctypes as C
+    from oracle import pyoracle
+    for y0 in (0, 391, 806, Hf - 4):
+        rect = oracle.Rect(0, y0, Wf, 4)
+        view = oracle.Rect(0, 0, Wf, Hf)
+        a_or = np.zeros_like(a0)
+        b_or = np.zeros_like(b0)
+        pyoracle.lib().or_ris(osc.handle, C.byref(f), key(_abi.RESTIR_STAGE_RIS), pyoracle.fp(o), Wf, Hf, view, rect,
+                              pyoracle.fp(n_t), pyoracle.fp(p_mat), pyoracle.fp(a_or), pyoracle.fp(b_or), None)
+        sl = slice(y0 * Wf, (y0 + 4) * Wf)
+        assert_bits(a0[:, sl], a_or[:, sl], f"RIS band {y0} res_a")
+        assert_bits(b0[:, sl], b_or[:, sl], f"RIS band {y0} res_b")
+    # G-buffer on sampled bands too
     n_t_or = np.zeros_like(n_t)
     p_mat_or = np.zeros_like(p_mat)
-    from oracle import pyoracle
-    import ctypes as C
     cf = pyoracle.camera_frame(cam)
     for y0 in (3, 700):
         rect = oracle.Rect(0, y0, Wf, 4)
@@ -625,3 +636,29 @@ def test_textured_frames_match_oracle(gpu, oracle, texture):
                                enable_texture_mapping=1 - texture)
     other, _, _ = oracle.render_frame(osc, cam, f0, W, H, SEED, 0, prev=None)
     assert not np.array_equal(other, first)
+
+
+# C4 (4K, 1024 parallelogram lights, k = 5 x1 biased) and C5 (8K, 4096 lights, M = 64, unbiased + spatial
+# visibility reuse) at their full sizes: the GPU frame's RGB on sampled row bands against the oracle rendering
+# those rows (with the ghost rows its spatial pass reads), bit for bit.
+@pytest.mark.parametrize("cfg", ["c4", "c5"])
+def test_full_size_frames_c4_c5_band_parity(gpu, oracle, cfg):
+    name, Wf, Hf, M, unb = {"c4": ("cornell_1024", 3840, 2160, 32, 0), "c5": ("cornell_4096", 7680, 4320, 64, 1)}[cfg]
+    s = get_scene(name)
+    gpu.set_scene(s)
+    gpu.set_seed(SEED, 0)
+    cam = scene.camera_for(name, Wf, Hf)
+    f = _abi.default_features(initial_light_samples=M, num_samples_in_reservoir=1, spatial_resampling_passes=1,
+                              temporal_reuse=0, unbiased_combination=unb, spatial_reuse_visibility_check=unb)
+    rgb, _ = gpu.render_restir(None, cam, Wf, Hf, f, want_grid=False)
+    assert rgb.shape == (Hf, Wf, 3) and np.isfinite(rgb).all()
+    osc = oracle.OracleScene(s)
+    g = f.spatial_resample_radius
+    for y0 in (0, Hf // 2 - 3, Hf - 4):
+        rows = 4
+        vy0 = max(0, y0 - g)
+        view = oracle.Rect(0, vy0, Wf, min(Hf, y0 + rows + g) - vy0)
+        rect = oracle.Rect(0, y0, Wf, rows)
+        want, _, _ = oracle.render_frame(osc, cam, f, Wf, Hf, view=view, rect=rect, threads=16)
+        r0 = Hf - (y0 + rows)          # RGB row 0 = top of the image
+        assert_bits(rgb[r0:r0 + rows], want, f"{cfg} rows {y0}..{y0 + rows - 1}")

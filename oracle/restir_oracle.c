@@ -947,14 +947,56 @@ void or_rmis_accumulate(const or_scene* s, const restir_features* f, const float
  * ColPivHouseholderQR::computeInPlace (ColPivHouseholderQR.h:482-571), CompleteOrthogonalDecomposition::
  * computeInPlace / _solve_impl / applyZAdjointOnTheLeftInPlace (CompleteOrthogonalDecomposition.h:430-560),
  * makeHouseholder / applyHouseholderOnTheLeft / OnTheRight (Householder.h, HouseholderSequence.h:361-412), the
- * upper-triangular back substitution (TriangularSolverVector.h, one panel for n <= 16).  Reductions (norms, the
- * Householder dot products) are evaluated in index order; Eigen evaluates them with SIMD packets, so the two
- * agree to rounding (tests/golden/cod_fixtures.json, generated by oracle/_ref/cod_ref against the reference's
- * vendored Eigen) while oracle and device agree bit for bit. */
+ * upper-triangular back substitution (TriangularSolverVector.h, one panel for n <= 16), with the reductions
+ * (norms, the Householder dot products) in Eigen's SIMD packet order below: bit-exact with the reference's
+ * vendored Eigen on every system of tests/golden/cod_fixtures.json (oracle/_ref/cod_ref); the device is
+ * bit-exact with this. */
 #define OR_COD_MAX 8
+/* Eigen's reductions of n products a[i] * b[i] with SSE2 Packet4f arithmetic (the image's x86-64 default; no FMA:
+ * pmadd = padd(pmul)).  Contiguous operands only; predux(p) = (p0 + p2) + (p1 + p3) (PacketMath.h:987-998).
+ * redux: DenseBase::redux, LinearVectorizedTraversal with alignedStart 0 (a cwise expression has no direct access,
+ *   Redux.h:205-250): first packet loaded, a second one for 8+ elements, then the scalar tail; n < 4: in order.
+ * gemv: one row of general_matrix_vector_product<RowMajor> (GeneralMatrixVector.h:327-515): a zeroed packet
+ *   accumulates the 4-blocks, predux, then the tail onto it (so an all-tail row starts from +0). */
+static float or_dot_redux(const float* a, int sa, const float* b, int sb, int n) {
+    if (n < 4) {
+        float r = a[0] * b[0];
+        for (int i = 1; i < n; i++) r = r + a[i * sa] * b[i * sb];
+        return r;
+    }
+    float p[4], q[4];
+    const int full = n / 4 * 4, end2 = n / 8 * 8;
+    for (int l = 0; l < 4; l++) p[l] = a[l * sa] * b[l * sb];
+    if (full > 4) {
+        for (int l = 0; l < 4; l++) q[l] = a[(4 + l) * sa] * b[(4 + l) * sb];
+        for (int i = 8; i < end2; i += 8)
+            for (int l = 0; l < 4; l++) {
+                p[l] = p[l] + a[(i + l) * sa] * b[(i + l) * sb];
+                q[l] = q[l] + a[(i + 4 + l) * sa] * b[(i + 4 + l) * sb];
+            }
+        for (int l = 0; l < 4; l++) p[l] = p[l] + q[l];
+        if (full > end2)
+            for (int l = 0; l < 4; l++) p[l] = p[l] + a[(end2 + l) * sa] * b[(end2 + l) * sb];
+    }
+    float r = (p[0] + p[2]) + (p[1] + p[3]);
+    for (int i = full; i < n; i++) r = r + a[i * sa] * b[i * sb];
+    return r;
+}
+static float or_dot_gemv(const float* a, const float* b, int n) {
+    float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    int j = 0;
+    for (; j + 4 <= n; j += 4)
+        for (int l = 0; l < 4; l++) c[l] = c[l] + a[j + l] * b[j + l];
+    float r = (c[0] + c[2]) + (c[1] + c[3]);
+    for (; j < n; j++) r = r + a[j] * b[j];
+    return r;
+}
+/* squaredNorm: vectorised over a contiguous segment, in index order over a strided one (a row of the
+ * column-major matrix has no packet access: DefaultTraversal) */
 static float or_sqnorm(const float* v, int n, int stride) {
-    float s = 0.0f;
-    for (int i = 0; i < n; i++) s = i == 0 ? v[0] * v[0] : s + v[i * stride] * v[i * stride];
+    if (stride == 1) return or_dot_redux(v, 1, v, 1, n);
+    float s = v[0] * v[0];
+    for (int i = 1; i < n; i++) s = s + v[i * stride] * v[i * stride];
     return s;
 }
 /* makeHouseholder on v[0], v[stride], ... (m entries): essential written over v[stride..], returns tau, beta */
@@ -973,8 +1015,13 @@ static void or_make_householder(float* v, int m, int stride, float* tau, float* 
         *beta = b;
     }
 }
-/* H = I - tau [1 e][1 e]^T from the left on the rows r0..r0+m-1 of columns c0..c0+nc-1 of column-major M (ld) */
-static void or_householder_left(float* M, int ld, int r0, int c0, int m, int nc, const float* e, int estride, float tau) {
+/* H = I - tau [1 e][1 e]^T from the left on the rows r0..r0+m-1 of columns c0..c0+nc-1 of column-major M (ld).
+ * tmp = essential^* bottom is, by Eigen's compile-time product selection: a row-major GEMV when bottom is a
+ * matrix block (the QR sweep, OR_HH_GEMV), an inner product (redux) when it is a vector block (Q^* applied to
+ * the right-hand side, OR_HH_DOT), in index order when the essential part is a strided row (Z^*, OR_HH_SEQ). */
+enum { OR_HH_GEMV = 0, OR_HH_DOT = 1, OR_HH_SEQ = 2 };
+static void or_householder_left(float* M, int ld, int r0, int c0, int m, int nc, const float* e, int estride, float tau,
+                                int kind) {
     if (m == 1) {
         for (int j = 0; j < nc; j++) M[r0 + (c0 + j) * ld] *= 1.0f - tau;
         return;
@@ -982,14 +1029,22 @@ static void or_householder_left(float* M, int ld, int r0, int c0, int m, int nc,
     if (tau == 0.0f) return;
     for (int j = 0; j < nc; j++) {
         float* col = &M[(c0 + j) * ld + r0];
-        float t = 0.0f;
-        for (int i = 0; i < m - 1; i++) t = i == 0 ? e[0] * col[1] : t + e[i * estride] * col[1 + i];
+        float t;
+        if (kind == OR_HH_GEMV) {
+            t = or_dot_gemv(e, col + 1, m - 1);
+        } else if (kind == OR_HH_DOT) {
+            t = or_dot_redux(e, 1, col + 1, 1, m - 1);
+        } else {
+            t = e[0] * col[1];
+            for (int i = 1; i < m - 1; i++) t = t + e[i * estride] * col[1 + i];
+        }
         t += col[0];
         col[0] -= tau * t;
         for (int i = 0; i < m - 1; i++) col[1 + i] -= (tau * e[i * estride]) * t;
     }
 }
-/* H from the right on rows r0..r0+nr-1 of columns c0..c0+m-1 */
+/* H from the right on rows r0..r0+nr-1 of columns c0..c0+m-1: tmp = right * essential is a column-major GEMV,
+ * each row summed in index order onto a zeroed accumulator */
 static void or_householder_right(float* M, int ld, int r0, int c0, int nr, int m, const float* e, int estride, float tau) {
     if (m == 1) {
         for (int i = 0; i < nr; i++) M[r0 + i + c0 * ld] *= 1.0f - tau;
@@ -998,7 +1053,7 @@ static void or_householder_right(float* M, int ld, int r0, int c0, int nr, int m
     if (tau == 0.0f) return;
     for (int i = 0; i < nr; i++) {
         float t = 0.0f;
-        for (int j = 0; j < m - 1; j++) t = j == 0 ? M[r0 + i + (c0 + 1) * ld] * e[0] : t + M[r0 + i + (c0 + 1 + j) * ld] * e[j * estride];
+        for (int j = 0; j < m - 1; j++) t = t + M[r0 + i + (c0 + 1 + j) * ld] * e[j * estride];
         t += M[r0 + i + c0 * ld];
         M[r0 + i + c0 * ld] -= tau * t;
         for (int j = 0; j < m - 1; j++) M[r0 + i + (c0 + 1 + j) * ld] -= (tau * t) * e[j * estride];
@@ -1033,7 +1088,7 @@ void or_cod_solve(uint32_t n_, const float* A, const float* b, float* x) {
         or_make_householder(&qr[k + k * n], n - k, 1, &hc[k], &beta);
         qr[k + k * n] = beta;
         if (fabsf(beta) > maxpivot) maxpivot = fabsf(beta);
-        or_householder_left(qr, n, k, k + 1, n - k, n - k - 1, &qr[k + 1 + k * n], 1, hc[k]);
+        or_householder_left(qr, n, k, k + 1, n - k, n - k - 1, &qr[k + 1 + k * n], 1, hc[k], OR_HH_GEMV);
         for (int j = k + 1; j < n; j++) {
             if (nU[j] != 0.0f) {
                 float temp = fabsf(qr[k + j * n]) / nU[j];
@@ -1080,7 +1135,7 @@ void or_cod_solve(uint32_t n_, const float* A, const float* b, float* x) {
     if (rank == 0) { for (int i = 0; i < n; i++) x[i] = 0.0f; return; }
     for (int i = 0; i < n; i++) c[i] = b[i];
     for (int k = 0; k < rank; k++)   /* Q^* c: H_0 first */
-        or_householder_left(c, n, k, 0, n - k, 1, &qr[k + 1 + k * n], 1, hc[k]);
+        or_householder_left(c, n, k, 0, n - k, 1, &qr[k + 1 + k * n], 1, hc[k], OR_HH_DOT);
     for (int i = 0; i < n; i++) y[i] = i < rank ? c[i] : 0.0f;
     for (int i = rank - 1; i >= 0; i--) {   /* upper-triangular back substitution, column sweep */
         if (y[i] != 0.0f) {
@@ -1091,7 +1146,7 @@ void or_cod_solve(uint32_t n_, const float* A, const float* b, float* x) {
     if (rank < n) {   /* applyZAdjointOnTheLeftInPlace */
         for (int k = 0; k < rank; k++) {
             if (k != rank - 1) { float t = y[k]; y[k] = y[rank - 1]; y[rank - 1] = t; }
-            or_householder_left(y, n, rank - 1, 0, n - rank + 1, 1, &qr[k + rank * n], n, zc[k]);
+            or_householder_left(y, n, rank - 1, 0, n - rank + 1, 1, &qr[k + rank * n], n, zc[k], OR_HH_SEQ);
             if (k != rank - 1) { float t = y[k]; y[k] = y[rank - 1]; y[rank - 1] = t; }
         }
     }

@@ -1914,11 +1914,50 @@ extern "C" __global__ __launch_bounds__(256) void k_rmis_accum_lds(SceneDev s, u
 // ColPivHouseholderQR::computeInPlace (ColPivHouseholderQR.h:482-571), CompleteOrthogonalDecomposition::
 // computeInPlace / _solve_impl / applyZAdjointOnTheLeftInPlace (CompleteOrthogonalDecomposition.h:430-560),
 // makeHouseholder / applyHouseholderOnTheLeft / OnTheRight (Householder.h), HouseholderSequence::applyThisOnTheLeft
-// (HouseholderSequence.h:369-412) and the one-panel upper back substitution.  Reductions in index order (Eigen uses
-// SIMD packets: agreement to rounding, pinned by tests/golden/cod_fixtures.json); correctly rounded sqrt / division.
+// (HouseholderSequence.h:369-412) and the one-panel upper back substitution, with Eigen's SIMD reduction orders
+// (bit-exact with the reference's Eigen on tests/golden/cod_fixtures.json); correctly rounded sqrt / division.
+// Eigen's reductions with SSE2 Packet4f arithmetic (the reference's x86-64 build; no FMA), as oracle/restir_oracle.c
+// restates them: redux = DenseBase::redux with alignedStart 0 (first packet loaded, a second for 8+ elements, then
+// the tail; n < 4 in order), gemv = one row of the row-major general_matrix_vector_product (a zeroed packet over
+// the 4-blocks, then the tail); predux(p) = (p0 + p2) + (p1 + p3).
+__device__ __forceinline__ float cod_dot_redux(const float* a, const float* b, int n) {
+    if (n < 4) {
+        float r = a[0] * b[0];
+        for (int i = 1; i < n; i++) r = r + a[i] * b[i];
+        return r;
+    }
+    float p[4], q[4];
+    const int full = n / 4 * 4, end2 = n / 8 * 8;
+    for (int l = 0; l < 4; l++) p[l] = a[l] * b[l];
+    if (full > 4) {
+        for (int l = 0; l < 4; l++) q[l] = a[4 + l] * b[4 + l];
+        for (int i = 8; i < end2; i += 8)
+            for (int l = 0; l < 4; l++) {
+                p[l] = p[l] + a[i + l] * b[i + l];
+                q[l] = q[l] + a[i + 4 + l] * b[i + 4 + l];
+            }
+        for (int l = 0; l < 4; l++) p[l] = p[l] + q[l];
+        if (full > end2)
+            for (int l = 0; l < 4; l++) p[l] = p[l] + a[end2 + l] * b[end2 + l];
+    }
+    float r = (p[0] + p[2]) + (p[1] + p[3]);
+    for (int i = full; i < n; i++) r = r + a[i] * b[i];
+    return r;
+}
+__device__ __forceinline__ float cod_dot_gemv(const float* a, const float* b, int n) {
+    float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    int j = 0;
+    for (; j + 4 <= n; j += 4)
+        for (int l = 0; l < 4; l++) c[l] = c[l] + a[j + l] * b[j + l];
+    float r = (c[0] + c[2]) + (c[1] + c[3]);
+    for (; j < n; j++) r = r + a[j] * b[j];
+    return r;
+}
+// squaredNorm: vectorised over a contiguous segment, in index order over a strided row
 __device__ __forceinline__ float cod_sqnorm(const float* v, int n, int stride) {
-    float s = 0.0f;
-    for (int i = 0; i < n; i++) s = i == 0 ? v[0] * v[0] : s + v[i * stride] * v[i * stride];
+    if (stride == 1) return cod_dot_redux(v, v, n);
+    float s = v[0] * v[0];
+    for (int i = 1; i < n; i++) s = s + v[i * stride] * v[i * stride];
     return s;
 }
 __device__ __forceinline__ void cod_make_householder(float* v, int m, int stride, float& tau, float& beta) {
@@ -1936,8 +1975,11 @@ __device__ __forceinline__ void cod_make_householder(float* v, int m, int stride
         beta = b;
     }
 }
+// tmp = essential^* bottom: a row-major GEMV in the QR sweep (COD_HH_GEMV), an inner product when applying Q^* to
+// the right-hand side (COD_HH_DOT), in index order for Z^*'s strided essential rows (COD_HH_SEQ)
+enum { COD_HH_GEMV = 0, COD_HH_DOT = 1, COD_HH_SEQ = 2 };
 __device__ __forceinline__ void cod_householder_left(float* M, int ld, int r0, int c0, int m, int nc, const float* e,
-                                                     int estride, float tau) {
+                                                     int estride, float tau, int kind) {
     if (m == 1) {
         for (int j = 0; j < nc; j++) M[r0 + (c0 + j) * ld] *= 1.0f - tau;
         return;
@@ -1945,13 +1987,21 @@ __device__ __forceinline__ void cod_householder_left(float* M, int ld, int r0, i
     if (tau == 0.0f) return;
     for (int j = 0; j < nc; j++) {
         float* col = &M[(c0 + j) * ld + r0];
-        float t = 0.0f;
-        for (int i = 0; i < m - 1; i++) t = i == 0 ? e[0] * col[1] : t + e[i * estride] * col[1 + i];
+        float t;
+        if (kind == COD_HH_GEMV) {
+            t = cod_dot_gemv(e, col + 1, m - 1);
+        } else if (kind == COD_HH_DOT) {
+            t = cod_dot_redux(e, col + 1, m - 1);
+        } else {
+            t = e[0] * col[1];
+            for (int i = 1; i < m - 1; i++) t = t + e[i * estride] * col[1 + i];
+        }
         t += col[0];
         col[0] -= tau * t;
         for (int i = 0; i < m - 1; i++) col[1 + i] -= (tau * e[i * estride]) * t;
     }
 }
+// tmp = right * essential: a column-major GEMV, each row summed in index order onto a zeroed accumulator
 __device__ __forceinline__ void cod_householder_right(float* M, int ld, int r0, int c0, int nr, int m, const float* e,
                                                       int estride, float tau) {
     if (m == 1) {
@@ -1961,8 +2011,7 @@ __device__ __forceinline__ void cod_householder_right(float* M, int ld, int r0, 
     if (tau == 0.0f) return;
     for (int i = 0; i < nr; i++) {
         float t = 0.0f;
-        for (int j = 0; j < m - 1; j++)
-            t = j == 0 ? M[r0 + i + (c0 + 1) * ld] * e[0] : t + M[r0 + i + (c0 + 1 + j) * ld] * e[j * estride];
+        for (int j = 0; j < m - 1; j++) t = t + M[r0 + i + (c0 + 1 + j) * ld] * e[j * estride];
         t += M[r0 + i + c0 * ld];
         M[r0 + i + c0 * ld] -= tau * t;
         for (int j = 0; j < m - 1; j++) M[r0 + i + (c0 + 1 + j) * ld] -= (tau * t) * e[j * estride];
@@ -1999,7 +2048,7 @@ __device__ void cod_solve_dev(const float* A, const float* b, float* x) {
         cod_make_householder(&qr[k + k * n], n - k, 1, hc[k], beta);
         qr[k + k * n] = beta;
         if (fabsf(beta) > maxpivot) maxpivot = fabsf(beta);
-        cod_householder_left(qr, n, k, k + 1, n - k, n - k - 1, &qr[k + 1 + k * n], 1, hc[k]);
+        cod_householder_left(qr, n, k, k + 1, n - k, n - k - 1, &qr[k + 1 + k * n], 1, hc[k], COD_HH_GEMV);
         for (int j = k + 1; j < n; j++) {
             if (nU[j] != 0.0f) {
                 float temp = fabsf(qr[k + j * n]) / nU[j];
@@ -2040,7 +2089,7 @@ __device__ void cod_solve_dev(const float* A, const float* b, float* x) {
     }
     if (rank == 0) { for (int i = 0; i < n; i++) x[i] = 0.0f; return; }
     for (int i = 0; i < n; i++) c[i] = b[i];
-    for (int k = 0; k < rank; k++) cod_householder_left(c, n, k, 0, n - k, 1, &qr[k + 1 + k * n], 1, hc[k]);
+    for (int k = 0; k < rank; k++) cod_householder_left(c, n, k, 0, n - k, 1, &qr[k + 1 + k * n], 1, hc[k], COD_HH_DOT);
     for (int i = 0; i < n; i++) y[i] = i < rank ? c[i] : 0.0f;
     for (int i = rank - 1; i >= 0; i--) {
         if (y[i] != 0.0f) {
@@ -2051,7 +2100,7 @@ __device__ void cod_solve_dev(const float* A, const float* b, float* x) {
     if (rank < n) {
         for (int k = 0; k < rank; k++) {
             if (k != rank - 1) { const float t = y[k]; y[k] = y[rank - 1]; y[rank - 1] = t; }
-            cod_householder_left(y, n, rank - 1, 0, n - rank + 1, 1, &qr[k + rank * n], n, zc[k]);
+            cod_householder_left(y, n, rank - 1, 0, n - rank + 1, 1, &qr[k + rank * n], n, zc[k], COD_HH_SEQ);
             if (k != rank - 1) { const float t = y[k]; y[k] = y[rank - 1]; y[rank - 1] = t; }
         }
     }

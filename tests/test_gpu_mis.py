@@ -1,8 +1,8 @@
 """GPU parity of R-MIS / R-OMIS (renderRMIS / renderROMIS, render.cpp:64-265) against the oracle, through the C ABI.
 Stage-isolated like test_gpu_parity.py: each stage gets the oracle's inputs, so a mismatch points at one kernel.
 Bar: bit-exact (neighbourhood indices, accumulators, least-squares solutions, RGB) -- device and oracle evaluate
-the same float operations in the same order.  Against the reference's own Eigen the solve agrees to COD_TOL
-(tests/test_mis_oracle.py).
+the same float operations in the same order.  The solve is also bit-exact against the reference's own Eigen
+(tests/golden/cod_fixtures.json, test_mis_oracle.py).
 """
 import numpy as np
 import pytest
@@ -13,7 +13,6 @@ pytestmark = pytest.mark.gpu
 
 W, H = 48, 32
 SEED = _abi.RESTIR_DEFAULT_SEED
-COD_TOL = 2e-4
 
 
 @pytest.fixture(scope="module")
@@ -62,7 +61,7 @@ def test_cod_solve_bit_exact_with_oracle(gpu, oracle):
         xg = gpu.debug_cod_solve(A, b)
         for i, (Ai, bi, xe) in enumerate(cs):
             bits_equal(xg[i], oracle.cod_solve(Ai, bi), f"n={n} case {i}")
-            assert np.abs(xg[i] - xe).max() <= COD_TOL * max(float(np.abs(xe).max()), 1e-30)
+            bits_equal(xg[i], xe, f"n={n} case {i} vs the reference's Eigen")
 
 
 @pytest.mark.parametrize("name", ["nightclub_128pt", "cornell_parallelogram"])

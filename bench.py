@@ -59,21 +59,30 @@ def parse():
                     help="kernels bracketed by HIP events in the timed region")
     ap.add_argument("--cpu-rows", type=int, default=None, help="rows of the workload the CPU baseline renders "
                     "(default: ~1 Mpx worth)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group of the multi-rank bench (nccl = RCCL, the real run; gloo = a rehearsal with "
+                         "several ranks sharing one GPU)")
     ap.add_argument("--traffic-csv", default=None,
                     help="rocprofv3 --pmc CSV (FETCH_SIZE / WRITE_SIZE) of this command for roofline.traffic")
     return ap.parse_args()
 
 
-def dist_setup(n_gpus):
-    """(rank, world, local_rank, torch or None).  torch is imported before libromis_amd so both share one HIP runtime."""
+def dist_setup(n_gpus, backend="nccl"):
+    """(rank, world, device, torch).  torch is imported before libromis_amd so both share one HIP runtime.
+    backend "gloo" (a rehearsal of the multi-rank path on a box with fewer GPUs than ranks): the ranks share the
+    visible GPUs round-robin and the barrier / max-over-ranks run on the CPU."""
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            local = local % max(1, torch.cuda.device_count())
+            dist.init_process_group("gloo")
     if world != n_gpus and rank == 0:
         print(f"warning: --gpus {n_gpus} but WORLD_SIZE {world}", file=sys.stderr)
     return rank, world, local, torch
@@ -90,7 +99,8 @@ def barrier_sync(torch, world, renderer):
 def max_over_ranks(torch, world, value, local):
     if world == 1:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=torch.device("cuda", local))
+    on_gpu = torch.distributed.get_backend() == "nccl"
+    t = torch.tensor([value], dtype=torch.float64, device=torch.device("cuda", local) if on_gpu else "cpu")
     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     return float(t.item())
 
@@ -218,7 +228,7 @@ def spatial_px_per_launch(tile, passes, r):
 
 def main():
     args = parse()
-    rank, world, local, torch = dist_setup(args.gpus)
+    rank, world, local, torch = dist_setup(args.gpus, args.dist_backend)
     from romis_amd import _abi, restir, scene
 
     cf = dict(CONFIGS[args.config])

@@ -33,7 +33,7 @@ __device__ __forceinline__ bool tri_hit(float4 v0, float4 e1_, float4 e2_, v3 o,
     v3 pvec = vcross(d, e2);
     float det = vdot(e1, pvec);
     if (det == 0.0f) return false;
-    float inv = 1.0f / det;
+    const float inv = rcp_rn(det);   // == 1.0f / det (the exact fast form, library division outside its range)
     v3 tvec = vsub(o, xyz(v0));
     float u = vdot(tvec, pvec) * inv;
     if (!(u >= 0.0f && u <= 1.0f)) return false;
@@ -44,6 +44,21 @@ __device__ __forceinline__ bool tri_hit(float4 v0, float4 e1_, float4 e2_, v3 o,
     if (!(t > 0.0f && t <= tfar)) return false;
     t_out = t; u_out = u; v_out = v;
     return true;
+}
+
+// The same test as an any-hit predicate without early exits (shadow rays): the same float expressions, so the
+// same decision, but straight-line code the compiler can interleave across a leaf's triangles.
+__device__ __forceinline__ bool tri_any(float4 v0, float4 e1_, float4 e2_, v3 o, v3 d, float tfar) {
+    const v3 e1 = xyz(e1_), e2 = xyz(e2_);
+    const v3 pvec = vcross(d, e2);
+    const float det = vdot(e1, pvec);
+    const float inv = rcp_rn(det);
+    const v3 tvec = vsub(o, xyz(v0));
+    const float u = vdot(tvec, pvec) * inv;
+    const v3 qvec = vcross(tvec, e1);
+    const float v = vdot(d, qvec) * inv;
+    const float t = vdot(e2, qvec) * inv;
+    return det != 0.0f && (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t <= tfar);
 }
 
 // Conservative slab test (boxes are padded on the host, the interval is widened): it may accept extra boxes,
@@ -105,9 +120,10 @@ __device__ __forceinline__ bool occluded(const Bvh& b, v3 o, v3 d, float tfar) {
         if (box_hit(lo, hi, o, invd, tb)) {
             if (leaf) {
                 uint32_t first = leaf & 0xFFFFFFu, cnt = leaf >> 24;
-                for (uint32_t k = 0; k < cnt; k++) {
-                    float t, u, v;
-                    if (tri_hit(b.v0[first + k], b.e1[first + k], b.e2[first + k], o, d, tfar, t, u, v)) return true;
+                for (uint32_t k = 0; k < cnt; k += 2) {   // two triangles per step (leaves hold 2 by default)
+                    bool h = tri_any(b.v0[first + k], b.e1[first + k], b.e2[first + k], o, d, tfar);
+                    if (k + 1 < cnt) h = tri_any(b.v0[first + k + 1], b.e1[first + k + 1], b.e2[first + k + 1], o, d, tfar) || h;
+                    if (h) return true;
                 }
                 i = miss;
             } else {
@@ -1567,6 +1583,7 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
     __shared__ float4 s_from[256], s_to[256];
     __shared__ uint32_t s_vis[256];
     const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
+    const GlTabs tb = gl_stage_tables();
     const float g = 1.0f / f.gamma;
     const uint32_t t = threadIdx.x;
     uint32_t x, y;
@@ -1579,7 +1596,7 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
     if (valid) {
         px = load_px(s, rg, n_t, p_mat, p, origin);
         sub_load(r, ra, rb, ridx(rg, 0, p));
-        sc = shade(s, f, px, r.pos, r.col);
+        sc = shade(s, f, px, r.pos, r.col, tb);
         need = sc.x != 0.0f || sc.y != 0.0f || sc.z != 0.0f;   // see final_body: no ray when sc == 0
     }
     s_hist[t] = 0u;
@@ -1620,8 +1637,8 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
     color = vdivs(color, 1.0f);
     if (f.tone_map) {
         v3 e = vscale(mk(-color.x, -color.y, -color.z), f.exposure);
-        v3 mapped = mk(1.0f - pm_expf(e.x), 1.0f - pm_expf(e.y), 1.0f - pm_expf(e.z));
-        color = g == 1.0f ? mapped : mk(pm_powf(mapped.x, g), pm_powf(mapped.y, g), pm_powf(mapped.z, g));
+        v3 mapped = mk(1.0f - gl_expf(tb, e.x), 1.0f - gl_expf(tb, e.y), 1.0f - gl_expf(tb, e.z));
+        color = g == 1.0f ? mapped : mk(gl_powf(tb, mapped.x, g), gl_powf(tb, mapped.y, g), gl_powf(tb, mapped.z, g));
     }
     const uint32_t row = rg.rh - 1u - (y - rg.ry0);
     float* o = rgb + 3 * ((size_t)row * rg.rw + (x - rg.rx0));

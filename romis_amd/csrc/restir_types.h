@@ -103,7 +103,7 @@ struct Tuning {
     uint32_t final_blocks = 0;
     uint32_t final_lds = 1;
     uint32_t final_2d = 1;
-    uint32_t final_sort = 0;       // N = 1: bin each tile's shadow rays by target before tracing
+    uint32_t final_sort = 1;       // N = 1: bin each tile's shadow rays by target before tracing (-2.4 %, r2ah)
     uint32_t mis_chunk = 0;        // R-OMIS samples per k_romis_samples / k_romis_accum pair; 0 = the scratch budget
 };
 

@@ -22,7 +22,7 @@ from romis_amd import _abi, restir, scene  # noqa: E402
 
 DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 1, "ris.queue": 0,
             "spatial.xcd": 1, "spatial.xcd_rows": 4, "spatial.lds": 3, "spatial.blocks": 0, "spatial.wave8": 1, "spatial.lean": 1, "fuse.primary_ris": 1, "bvh.max_leaf": 2, "final.blocks": 0, "final.lds": 1, "final.2d": 1,
-            "final.sort": 0, "layout.records": 0}
+            "final.sort": 1, "layout.records": 0}
 
 VARIANTS = {
     "default": {},
@@ -49,7 +49,7 @@ VARIANTS = {
     "spatial_rows8": {"spatial.xcd_rows": 8},
     "spatial_general": {"spatial.lean": 0},
     "unfused": {"fuse.primary_ris": 0},
-    "final_sort": {"final.sort": 1},
+    "final_unsorted": {"final.sort": 0},
     "layout_records": {"layout.records": 1},
     "spatial_rows": {"spatial.wave8": 0},
     "bvh_leaf1": {"bvh.max_leaf": 1},

@@ -272,19 +272,21 @@ def test_final_shading(gpu, oracle, N, tonemap):
 
 
 @pytest.mark.parametrize("name", ["nightclub_128pt", "cornell_1024"])
-def test_final_shading_binned_rays(gpu, oracle, name):
-    """final.sort (N = 1): rays traced in target-bin order by other lanes -- the image must not change."""
+@pytest.mark.parametrize("binned", [1, 0])
+def test_final_shading_binned_rays(gpu, oracle, name, binned):
+    """final.sort (N = 1, the default): rays traced in target-bin order by other lanes -- the image must not
+    change; final.sort 0: the unbinned kernel."""
     _, osc, cam = setup(gpu, oracle, name, 1)
     n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
     f = _abi.default_features(num_samples_in_reservoir=1)
     a, b, _ = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
     for which, arr in [(_abi.BUF_GBUF_N_T, n_t), (_abi.BUF_GBUF_P_MAT, p_mat), (_abi.BUF_RES_A, a), (_abi.BUF_RES_B, b)]:
         gpu.upload(which, arr)
-    gpu.set_tuning("final.sort", 1)
+    gpu.set_tuning("final.sort", binned)
     try:
         gpu.stage_final(cam, f)
     finally:
-        gpu.set_tuning("final.sort", 0)
+        gpu.set_tuning("final.sort", 1)
     want = oracle.final(osc, f, origin(oracle, cam), W, H, n_t, p_mat, (a, b))
     assert_bits(gpu.download(_abi.BUF_RGB), want, "rgb")
 

@@ -46,6 +46,22 @@ __device__ __forceinline__ bool tri_hit(float4 v0, float4 e1_, float4 e2_, v3 o,
     return true;
 }
 
+// tri_hit without early exits: the same expressions (u, v, t computed for every triangle), the decision as a
+// predicate; straight-line code for the closest-hit leaf loop
+__device__ __forceinline__ bool tri_test(float4 v0, float4 e1_, float4 e2_, v3 o, v3 d, float tfar, float& t, float& u,
+                                         float& v) {
+    const v3 e1 = xyz(e1_), e2 = xyz(e2_);
+    const v3 pvec = vcross(d, e2);
+    const float det = vdot(e1, pvec);
+    const float inv = rcp_rn(det);
+    const v3 tvec = vsub(o, xyz(v0));
+    u = vdot(tvec, pvec) * inv;
+    const v3 qvec = vcross(tvec, e1);
+    v = vdot(d, qvec) * inv;
+    t = vdot(e2, qvec) * inv;
+    return det != 0.0f && (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t <= tfar);
+}
+
 // The same test as an any-hit predicate without early exits (shadow rays): the same float expressions, so the
 // same decision, but straight-line code the compiler can interleave across a leaf's triangles.
 __device__ __forceinline__ bool tri_any(float4 v0, float4 e1_, float4 e2_, v3 o, v3 d, float tfar) {
@@ -151,13 +167,12 @@ __device__ __forceinline__ bool closest(const Bvh& b, v3 o, v3 d, float& t_best,
             if (leaf) {
                 uint32_t first = leaf & 0xFFFFFFu, cnt = leaf >> 24;
                 for (uint32_t k = 0; k < cnt; k++) {
-                    float4 v0 = b.v0[first + k];
+                    const float4 v0 = b.v0[first + k];
                     float t, u, v;
-                    if (tri_hit(v0, b.e1[first + k], b.e2[first + k], o, d, ROMIS_FLT_MAX, t, u, v)) {
-                        uint32_t orig = __float_as_uint(v0.w);
-                        if (!found || t < t_best || (t == t_best && orig < tri_best)) {
-                            found = true; t_best = t; u_best = u; v_best = v; tri_best = orig;
-                        }
+                    const bool h = tri_test(v0, b.e1[first + k], b.e2[first + k], o, d, ROMIS_FLT_MAX, t, u, v);
+                    const uint32_t orig = __float_as_uint(v0.w);
+                    if (h && (!found || t < t_best || (t == t_best && orig < tri_best))) {
+                        found = true; t_best = t; u_best = u; v_best = v; tri_best = orig;
                     }
                 }
                 i = miss;

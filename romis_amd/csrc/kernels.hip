@@ -265,7 +265,20 @@ __device__ __forceinline__ Px load_px(const SceneDev& s, const Region& rg, const
 // candidates, was measured slower in RIS: 345 -> 393-591 us, the batch state costing occupancy -- DESIGN §6.)
 __device__ __forceinline__ bool pow_pre(float x, const Px& px, float& pw, uint32_t& job) {
     const uint32_t mode = __float_as_uint(px.ks_pm.w);
-    if (mode == ROMIS_POW_SKIP) { pw = 1.0f; return true; }
+    if (mode != ROMIS_POW_GLIBC) {
+        // ROMIS_POW_SKIP, or ROMIS_POW_SIMPLE: every base glibc settles before its core is under the threshold
+        // (+-0, NaN passed through) or a negative base with a non-integer exponent (invalid), as selects
+        const uint32_t cls = __float_as_uint(px.pw.y);
+        const float ax = fabsf(x);
+        const bool neg_odd = __builtin_signbit(x) && (cls & ROMIS_PWC_ODD);
+        const bool under = !(ax >= px.pw.x);
+        const bool invalid = x < 0.0f && !(cls & ROMIS_PWC_INT);
+        float r = under ? (__builtin_isnan(x) ? x : (neg_odd ? -0.0f : 0.0f)) : __uint_as_float(0xffc00000u);
+        const bool skip = mode == ROMIS_POW_SKIP;
+        pw = skip ? 1.0f : r;
+        job = __float_as_uint(ax) | (neg_odd ? 0x80000000u : 0u);
+        return skip || under || invalid;
+    }
     const uint32_t cls = __float_as_uint(px.pw.y);
     const float ax = fabsf(x);
     if (__builtin_expect(cls & ROMIS_PWC_SPECIAL, 0)) {

@@ -822,8 +822,10 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
             thr = (float)std::exp2(-150.0 * (1.0 + 0x1p-20) / y);
             if ((double)thr > std::exp2(-150.0 * (1.0 + 0x1p-20) / y)) thr = std::nextafter(thr, 0.0f);
         }
+        const uint32_t cls = pw_class(mt.shininess);
+        if (mode == ROMIS_POW_GLIBC && !(cls & (ROMIS_PWC_SPECIAL | ROMIS_PWC_NEG)) && thr >= FLT_MIN) mode = ROMIS_POW_SIMPLE;
         o[7] = u2f(mode);
-        o[8] = thr; o[9] = u2f(pw_class(mt.shininess)); o[10] = mt.transparency; o[11] = u2f(mt.kd_texture);
+        o[8] = thr; o[9] = u2f(cls); o[10] = mt.transparency; o[11] = u2f(mt.kd_texture);
     };
     for (uint32_t m = 0; m < num_meshes; m++) put_material(m, meshes[m].material);
     {

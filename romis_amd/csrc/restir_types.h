@@ -10,6 +10,9 @@
 // material pow modes (std::pow(cosTheta, shininess), shading.cpp:26)
 #define ROMIS_POW_SKIP 0u      // ks == 0: the specular term is +-0 whatever pow returns
 #define ROMIS_POW_GLIBC 1u     // glibc's powf specialised to the material's exponent (kernels.hip material_pow)
+#define ROMIS_POW_SIMPLE 2u    // ROMIS_POW_GLIBC for a finite exponent y > 0 whose underflow threshold is >= 2^-126:
+                               // a zero or subnormal base is always under the threshold, so the cases before the
+                               // log2 / exp2 core reduce to three selects (pow_pre)
 // exponent classes of ROMIS_POW_GLIBC (materials[3m + 2].y)
 #define ROMIS_PWC_ODD 1u       // glibc checkint(y) == 1: odd integer
 #define ROMIS_PWC_INT 2u       // checkint(y) != 0: integer

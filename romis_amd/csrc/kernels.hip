@@ -375,6 +375,7 @@ __device__ __forceinline__ float target_pdf(const SceneDev& s, const FeaturesDev
 // The block's LDS copy of powf's two tables (512 B): every p-hat evaluation indexes them twice per lane, and from
 // __constant__ memory each index is a vector-memory round trip in the middle of the dependent chain (two per
 // target pdf); from LDS it is a ds_read.  Every thread of the block must call this (it ends with a barrier).
+template <bool SYNC = true>
 __device__ __forceinline__ GlTabs gl_stage_tables() {
     __shared__ double s_gl_log2[32];
     __shared__ unsigned long long s_gl_exp2[32];
@@ -382,7 +383,7 @@ __device__ __forceinline__ GlTabs gl_stage_tables() {
         s_gl_log2[threadIdx.x] = kGlLog2Tab[threadIdx.x];
         s_gl_exp2[threadIdx.x] = kGlExp2Tab[threadIdx.x];
     }
-    __syncthreads();
+    if (SYNC) __syncthreads();   // SYNC = false: the caller's next barrier precedes every table read
     GlTabs t;
     t.log2 = s_gl_log2;
     t.exp2 = s_gl_exp2;
@@ -1386,8 +1387,9 @@ ROMIS_SPATIAL1_LDS_KERNEL(true, false, 3, k_spatial1_ldsr_dbg)
 // instruction touches ~50 distinct 128-byte lines (one TA/L1 cycle each), against 8 for a coalesced one.
 // The five neighbour n_t gathers are the only ones every lane issues (the reservoir gathers follow only the
 // accepted neighbours), so they are the ones replaced: the block copies the (32 + 2R) x (8 + 2R) n_t window
-// (23 KB at R = 10, 6 blocks per CU) with row-coalesced loads, issued together with the pixel's own records.
-// The accepted neighbours' reservoirs stay global gathers, one neighbour ahead of the consume sequence (as in
+// (23 KB at R = 10, 6 blocks per CU) with row-coalesced LDS-DMA loads (global_load_lds_dwordx4: no VGPR staging,
+// no ds_write pass), issued together with the pixel's own records; the powf tables are staged in the same phase,
+// so the block passes one barrier (81.3-82.5 -> 81.3 us in kbench, profiles/r2/glds).  The accepted neighbours' reservoirs stay global gathers, one neighbour ahead of the consume sequence (as in
 // spatial1_pixel).  Same arithmetic, RNG slots and update order as spatial1_pixel; R <= kLdsSpatialR.
 template <bool DBG>
 __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
@@ -1396,7 +1398,7 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
                                                   const float4* __restrict__ ib, float4* __restrict__ oa,
                                                   float4* __restrict__ ob, float2* __restrict__ odbg,
                                                   const float* __restrict__ rp_in, float* __restrict__ rp_out) {
-    const GlTabs tb = gl_stage_tables();
+    const GlTabs tb = gl_stage_tables<false>();   // made visible by the window's barrier below
     float4* const l_nt = g_lds;
     uint32_t tile;
     if (!xcd_tile(rg, num_tiles(rg), blockIdx.x, tile)) return;   // block-uniform
@@ -1423,23 +1425,23 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
         if (rp_in) pd_cached = ld_at(rp_in, pofs >> 2);
     }
     {
+        // LDS-DMA: each wave's 64 consecutive window entries l_nt[256k + 64w + lane] are written straight from
+        // global memory (global_load_lds_dwordx4, lane l at the wave-uniform base + 16 l), no VGPR round trip;
+        // __syncthreads() below waits for them (vmcnt(0) before s_barrier)
         constexpr uint32_t kPer = (kApronMax + 255u) / 256u;
-        const uint32_t magic = 0xFFFFFFFFu / AW + 1u;   // i / AW for i < 2^16
-        float4 vn[kPer];
+        const uint32_t magic = 0xFFFFFFFFu / AW + 1u;
+        const uint32_t w64 = (threadIdx.x >> 6) << 6;
 #pragma unroll
         for (uint32_t k = 0; k < kPer; k++) {
             const uint32_t i = threadIdx.x + 256u * k;
             if (i < n_apron) {
-                uint32_t r = __umulhi(i, magic);
+                uint32_t r = __umulhi(i, magic);   // i / AW for i < 2^16
                 if (r * AW > i) r--;
                 const uint32_t c = i - r * AW;
-                vn[k] = ld_at(n_t, (((uint32_t)(ay0 - (int)rg.vy0) + r) * rg.vw + (uint32_t)(ax0 - (int)rg.vx0) + c) << 4);
+                const float4* src = n_t + (((uint32_t)(ay0 - (int)rg.vy0) + r) * rg.vw + (uint32_t)(ax0 - (int)rg.vx0) + c);
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                                 (__attribute__((address_space(3))) void*)(l_nt + 256u * k + w64), 16, 0, 0);
             }
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; k++) {
-            const uint32_t i = threadIdx.x + 256u * k;
-            if (i < n_apron) l_nt[i] = vn[k];
         }
     }
     // neighbour draws while the loads are in flight

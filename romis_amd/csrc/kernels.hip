@@ -2510,6 +2510,11 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         // one block per tile, grid rounded to the XCD that owns the most tiles (xcd_tile)
         const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
         rg.xcd_rows = tu.spatial_xcd_rows;
+        if (rg.xcd_rows == kXcdRowsAuto) {
+            // a chunk's records (n_t, p_mat, res_a, res_b: 64 B/px over 8-px tile rows) within one XCD's 4 MB L2:
+            // 4 tile rows at 1920 px, 2 at 3840 (kbench: 4K 239 -> 225 us with 2, 1080p best with 4; r2bb)
+            rg.xcd_rows = std::max(1u, std::min(8u, 8192u / std::max(rg.rw, 1u)));
+        }
         if (rg.xcd_rows) {
             const uint32_t chunks = (nty + rg.xcd_rows - 1) / rg.xcd_rows;
             grid = 8u * ((chunks + 7u) / 8u) * rg.xcd_rows * ntx;

@@ -85,6 +85,7 @@ struct Region {
 };
 
 // Launch-shape knobs (restir_set_tuning); they never change results, only speed.
+constexpr uint32_t kXcdRowsAuto = 255u;
 struct Tuning {
     uint32_t primary_blocks = 0;   // grid cap (persistent blocks); 0 = one block per work item
     uint32_t primary_lds = 1;      // stage the BVH in LDS when it fits
@@ -95,7 +96,8 @@ struct Tuning {
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
     uint32_t spatial_lds = 3;      // k_spatial1: stage the tile's neighbourhood in LDS (R <= 10): 3 n_t only (default,
                                    // k_spatial1_ntl), 1 n_t + reservoirs, 2 reservoirs only, 0 none (all gathers)
-    uint32_t spatial_xcd_rows = 4; // k_spatial1: XCD x takes every 8th chunk of this many tile rows (0: one band)
+    uint32_t spatial_xcd_rows = 255; // k_spatial1: XCD x takes every 8th chunk of this many tile rows (0: one band;
+                                     // 255 = kXcdRowsAuto: as many as keep a chunk's records in one XCD's L2)
     uint32_t spatial_blocks = 0;
     uint32_t spatial_wave8 = 1;    // waves cover 8x8 pixel blocks instead of 32x2 rows (-2..4 %, kbench)
     uint32_t fuse_primary_ris = 1; // restir_render: k_primary_ris instead of k_primary + k_ris when the BVH fits LDS

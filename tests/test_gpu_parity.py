@@ -205,8 +205,9 @@ SPATIAL_VARIANTS = {"gather": {"spatial.lean": 1, "spatial.lds": 0},
                     "lds": {"spatial.lean": 1, "spatial.lds": 1},
                     "ldsr": {"spatial.lean": 1, "spatial.lds": 2},
                     "ntl": {"spatial.lean": 1, "spatial.lds": 3},
+                    "ntl_rows2": {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 2},
                     "general": {"spatial.lean": 0}}
-SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 4}
+SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 255}
 
 
 @pytest.mark.parametrize("name", ["nightclub_128pt", "cornell_parallelogram"])

@@ -259,20 +259,29 @@ inline void renderMIS(Renderer& r, const Camera& camera, Screen& screen, const F
 }
 
 // renderRayTraced (render.cpp:268-290): the grid for temporal reuse in ReSTIR mode, nullptr (std::nullopt) for
-// R-MIS / R-OMIS.
+// R-MIS / R-OMIS.  Like the reference, every render then saves its configuration record to
+// <rendersDir>/<currentTime()>.json (render.cpp:281-287, saveFeaturesRecord); the reference's RENDERS_DIR is a
+// build-time constant, here the caller passes it -- an empty path skips the record.
 inline std::shared_ptr<ReservoirGrid> renderRayTraced(Renderer& r, const std::shared_ptr<ReservoirGrid>& prev,
-                                                      const Camera& camera, Screen& screen, const Features& features) {
+                                                      const Camera& camera, Screen& screen, const Features& features,
+                                                      const std::filesystem::path& rendersDir = {},
+                                                      const restir_features_record_extra* extra = nullptr) {
+    std::shared_ptr<ReservoirGrid> next;
     switch (features.ray_trace_mode) {
-        case RESTIR_MODE_RESTIR: return renderReSTIR(r, prev, camera, screen, features);
+        case RESTIR_MODE_RESTIR: next = renderReSTIR(r, prev, camera, screen, features); break;
         case RESTIR_MODE_RMIS:
-        case RESTIR_MODE_ROMIS: renderMIS(r, camera, screen, features); return nullptr;
+        case RESTIR_MODE_ROMIS: renderMIS(r, camera, screen, features); break;
         default: throw RestirError("Unsupported ray-tracing render mode requested from entry point");
     }
+    if (!rendersDir.empty()) saveFeaturesRecord(features, rendersDir, extra);
+    return next;
 }
 // ... from any thread: the calling thread's context of the pool
 inline std::shared_ptr<ReservoirGrid> renderRayTraced(RendererPool& pool, const std::shared_ptr<ReservoirGrid>& prev,
-                                                      const Camera& camera, Screen& screen, const Features& features) {
-    return renderRayTraced(pool.local(), prev, camera, screen, features);
+                                                      const Camera& camera, Screen& screen, const Features& features,
+                                                      const std::filesystem::path& rendersDir = {},
+                                                      const restir_features_record_extra* extra = nullptr) {
+    return renderRayTraced(pool.local(), prev, camera, screen, features, rendersDir, extra);
 }
 
 }  // namespace romis

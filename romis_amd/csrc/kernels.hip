@@ -1427,7 +1427,8 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     {
         // LDS-DMA: each wave's 64 consecutive window entries l_nt[256k + 64w + lane] are written straight from
         // global memory (global_load_lds_dwordx4, lane l at the wave-uniform base + 16 l), no VGPR round trip;
-        // __syncthreads() below waits for them (vmcnt(0) before s_barrier)
+        // every wave waits for its own copies (explicit s_waitcnt vmcnt(0), below) before the barrier, so after
+        // it every wave may read every entry
         constexpr uint32_t kPer = (kApronMax + 255u) / 256u;
         const uint32_t magic = 0xFFFFFFFFu / AW + 1u;
         const uint32_t w64 = (threadIdx.x >> 6) << 6;
@@ -1460,6 +1461,10 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
             qo[n] = ((uint32_t)(ny - (int)rg.vy0) * rg.vw + (uint32_t)(nx - (int)rg.vx0)) << 4;
         }
     }
+    // Other waves read this wave's LDS-DMA entries after the barrier.  The compiler only waits for a wave's own
+    // DMA before that wave's ds_reads, and a workgroup-scope fence need not drain vmcnt on gfx950, so the wait
+    // is explicit (scripts/kernel_isa.sh k_spatial1_ntl: s_waitcnt vmcnt(0) directly before s_barrier).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (!live) return;   // no barrier follows
     const float4 cn = l_nt[(uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0)];
@@ -2392,6 +2397,9 @@ extern "C" __global__ __launch_bounds__(256) void k_mis_combine(uint32_t W, uint
 
 #include <hip/hip_ext.h>
 
+#include <mutex>
+#include <set>
+
 namespace romis {
 
 // Timed launches: restir.cpp's TIMED hands a start / stop event pair to the next launch, which records them
@@ -2504,10 +2512,10 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
     Region rg = with_map(rg0, tu.spatial_xcd);   // XCD-banded order works on 2D tiles
     if (rg.map2d && tu.spatial_wave8) rg.map2d = 2u;
     uint32_t grid = items_of(rg);
-    if (tu.spatial_blocks) grid = std::min(grid, std::max(8u, tu.spatial_blocks));
     if (tu.spatial_lean && !f.unbiased && f.N == 1 && f.K <= kLeanK && rg.ps == 1u && rg.map2d == 2u &&
         (size_t)rg.vw * rg.vh * 16u <= 0xFFFFFFFFull) {
-        // one block per tile, grid rounded to the XCD that owns the most tiles (xcd_tile)
+        // one block per tile (the lean kernels do not loop over tiles, so spatial.blocks does not apply here),
+        // grid rounded to the XCD that owns the most tiles (xcd_tile)
         const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
         rg.xcd_rows = tu.spatial_xcd_rows;
         if (rg.xcd_rows == kXcdRowsAuto) {
@@ -2526,14 +2534,22 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
             ROMIS_LAUNCH(odbg ? k_spatial1_ldsr_dbg : k_spatial1_ldsr, dim3(grid), dim3(kBlock), 2u * kApronMax * 16u, stream,
                          s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
         } else if (tu.spatial_lds && f.R <= kLdsSpatialR) {
-            static bool attr_set = false;   // > 64 KB of dynamic LDS must be requested per kernel
-            if (!attr_set) {
-                for (const void* k : {(const void*)k_spatial1_lds, (const void*)k_spatial1_lds_dbg}) {
-                    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                             (int)(3u * kApronMax * 16u));
-                    if (e != hipSuccess) return e;
+            // > 64 KB of dynamic LDS must be requested per kernel and device, once (contexts on several threads
+            // may get here together)
+            static std::mutex mu;
+            static std::set<int> devices_set;
+            int dev = 0;
+            hipError_t e = hipGetDevice(&dev);
+            if (e != hipSuccess) return e;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (!devices_set.count(dev)) {
+                    for (const void* k : {(const void*)k_spatial1_lds, (const void*)k_spatial1_lds_dbg}) {
+                        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(3u * kApronMax * 16u));
+                        if (e != hipSuccess) return e;
+                    }
+                    devices_set.insert(dev);
                 }
-                attr_set = true;
             }
             ROMIS_LAUNCH(odbg ? k_spatial1_lds_dbg : k_spatial1_lds, dim3(grid), dim3(kBlock), 3u * kApronMax * 16u, stream,
                          s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
@@ -2544,6 +2560,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         if (rp_written) *rp_written = rp_out != nullptr;
         return hipGetLastError();
     }
+    if (tu.spatial_blocks) grid = std::min(grid, std::max(8u, tu.spatial_blocks));   // the general kernels loop
     auto k = f.unbiased ? (f.N == 1 ? k_spatial_n1_unbiased : (f.N == 2 ? k_spatial_n2_unbiased : k_spatial_n0_unbiased))
                         : (f.N == 1 ? k_spatial_n1_biased : (f.N == 2 ? k_spatial_n2_biased : k_spatial_n0_biased));
     const size_t lds = bvh_lds_bytes(s);

@@ -234,6 +234,7 @@ struct restir_ctx {
         HaloSegs send{}, recv{};
         uint64_t send_bytes = 0, recv_bytes = 0;
         uint32_t send_rank[RESTIR_MAX_HALO_SEGS] = {}, recv_rank[RESTIR_MAX_HALO_SEGS] = {};
+        uint32_t rank = 0, nranks = 0;   // this frame's tile (rank) of tiles_x * tiles_y
         int cur = 0;
         bool fb_records = true;
         bool rp_ok = false;          // the current grid's target-pdf cache is valid (restir_render's rp_ok)
@@ -247,6 +248,7 @@ struct restir_ctx {
         bool owned = false;              // created by restir_halo_attach_rccl (destroyed with the context)
         hipStream_t stream = nullptr;    // communication stream
         hipEvent_t packed = nullptr, moved = nullptr;
+        int nranks = 0, rank = -1;       // the communicator's size and this context's rank in it
         DevBuf send, recv;
     } rccl;
 
@@ -1535,6 +1537,8 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
     c->stage_ok = false;
     h.send = send; h.recv = recv; h.send_bytes = send_b; h.recv_bytes = recv_b;
     for (uint32_t i = 0; i < n; i++) { h.send_rank[i] = sg[i].rank; h.recv_rank[i] = rg_[i].rank; }
+    h.rank = rank;
+    h.nranks = tiles_x * tiles_y;
     h.interior_done = false;
     ST_TRY(c->rgb.ensure((size_t)t.width * t.height * 12));
     c->rgb_w = t.width; c->rgb_h = t.height;
@@ -1711,6 +1715,8 @@ struct RcclApi {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclCommCount) comm_count = nullptr;
+    decltype(&ncclCommUserRank) comm_user_rank = nullptr;
 };
 
 const RcclApi& rccl_api() {
@@ -1732,6 +1738,8 @@ const RcclApi& rccl_api() {
         sym(a.group_start, "ncclGroupStart");
         sym(a.group_end, "ncclGroupEnd");
         sym(a.error_string, "ncclGetErrorString");
+        sym(a.comm_count, "ncclCommCount");
+        sym(a.comm_user_rank, "ncclCommUserRank");
         a.ok = all;
         if (!all) a.why = "librccl lacks a symbol";
         return a;
@@ -1749,8 +1757,23 @@ extern "C" {
             return fail(RESTIR_ERR_COMM, "%s: %s", #expr, rccl_api().error_string(rc_));                           \
     } while (0)
 
+// inside an open ncclGroupStart: close the group before reporting the error, so the thread's RCCL group state
+// does not leak into the next call
+#define RCCL_GROUP_TRY(expr)                                                                                      \
+    do {                                                                                                          \
+        const ncclResult_t rc_ = (expr);                                                                          \
+        if (rc_ != ncclSuccess) {                                                                                 \
+            (void)rccl_api().group_end();                                                                         \
+            return fail(RESTIR_ERR_COMM, "%s: %s", #expr, rccl_api().error_string(rc_));                           \
+        }                                                                                                         \
+    } while (0)
+
 static void release_rccl(restir_ctx* c) {
     auto& q = c->rccl;
+    // the context stream may still hold an unpack that waits on the transfer, and the communication stream the
+    // transfer itself: drain both before the communicator and the streams go
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (q.stream) (void)hipStreamSynchronize(q.stream);
     if (q.comm && q.owned && rccl_api().ok) (void)rccl_api().comm_destroy(static_cast<ncclComm_t>(q.comm));
     q.comm = nullptr;
     q.owned = false;
@@ -1759,6 +1782,8 @@ static void release_rccl(restir_ctx* c) {
     if (q.stream) (void)hipStreamDestroy(q.stream);
     q.packed = q.moved = nullptr;
     q.stream = nullptr;
+    q.nranks = 0;
+    q.rank = -1;
     q.send.release();
     q.recv.release();
 }
@@ -1771,6 +1796,11 @@ static restir_status attach_comm_locked(restir_ctx* c, void* comm, bool owned) {
     if (q.comm && q.owned) RCCL_TRY(rccl_api().comm_destroy(static_cast<ncclComm_t>(q.comm)));
     q.comm = comm;
     q.owned = owned;
+    int n = 0, r = -1;
+    RCCL_TRY(rccl_api().comm_count(static_cast<ncclComm_t>(comm), &n));
+    RCCL_TRY(rccl_api().comm_user_rank(static_cast<ncclComm_t>(comm), &r));
+    q.nranks = n;
+    q.rank = r;
     return RESTIR_OK;
 }
 
@@ -1814,6 +1844,15 @@ restir_status restir_halo_pass(restir_ctx* c) {
     auto& q = c->rccl;
     if (!q.comm) return fail(RESTIR_ERR_STATE, "restir_halo_pass before restir_halo_attach_rccl / _comm");
     if (!h.active || h.pass >= h.passes || h.interior_done) return fail(RESTIR_ERR_STATE, "restir_halo_pass: no pass pending");
+    // the plan's peers are tile ranks: the communicator must hold exactly the tiles, with this context's tile at
+    // its own rank, or the halos would go to the wrong peers
+    if (q.nranks != (int)h.nranks || q.rank != (int)h.rank)
+        return fail(RESTIR_ERR_INVALID, "restir_halo_pass: communicator rank %d of %d, halo frame is tile %u of %u",
+                    q.rank, q.nranks, h.rank, h.nranks);
+    for (uint32_t i = 0; i < h.send.n; i++)
+        if (h.send_rank[i] >= h.nranks || h.recv_rank[i] >= h.nranks || h.send_rank[i] == h.rank)
+            return fail(RESTIR_ERR_INVALID, "restir_halo_pass: segment %u peers %u / %u outside the %u tiles", i,
+                        h.send_rank[i], h.recv_rank[i], h.nranks);
     const RcclApi& api = rccl_api();
     HIP_TRY(hipSetDevice(c->device));
     ST_TRY(q.send.ensure(std::max<uint64_t>(h.send_bytes, 16)));
@@ -1831,8 +1870,8 @@ restir_status restir_halo_pass(restir_ctx* c) {
         for (uint32_t i = 0; i < h.send.n; i++) {
             const uint64_t so = (uint64_t)h.send.px0[i] * h.f.N * 32u, sb = (uint64_t)h.send.w[i] * h.send.h[i] * h.f.N * 32u;
             const uint64_t ro = (uint64_t)h.recv.px0[i] * h.f.N * 32u, rb = (uint64_t)h.recv.w[i] * h.recv.h[i] * h.f.N * 32u;
-            RCCL_TRY(api.send(static_cast<const char*>(q.send.p) + so, sb, ncclUint8, (int)h.send_rank[i], comm, q.stream));
-            RCCL_TRY(api.recv(static_cast<char*>(q.recv.p) + ro, rb, ncclUint8, (int)h.recv_rank[i], comm, q.stream));
+            RCCL_GROUP_TRY(api.send(static_cast<const char*>(q.send.p) + so, sb, ncclUint8, (int)h.send_rank[i], comm, q.stream));
+            RCCL_GROUP_TRY(api.recv(static_cast<char*>(q.recv.p) + ro, rb, ncclUint8, (int)h.recv_rank[i], comm, q.stream));
         }
         RCCL_TRY(api.group_end());
     }

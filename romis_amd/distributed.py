@@ -16,11 +16,12 @@ from . import restir
 class HaloFrames:
     """Renders this rank's tile of successive frames (restir_halo_begin .. restir_halo_end).
 
-    transport "native" (default with the nccl backend): the library's own RCCL communicator moves the halo on a
-    communication stream while the pass's interior runs (restir_halo_pass) -- no host round trip, no device
-    synchronisation.  transport "torch": torch.distributed batch_isend_irecv on device tensors (nccl) or host
-    tensors (gloo, the CPU / single-GPU tests); the pass's interior is issued before the exchange and runs on the
-    GPU while the host drives it, the border strips after the unpack."""
+    transport "torch" (default): torch.distributed batch_isend_irecv on device tensors (nccl) or host tensors
+    (gloo, the CPU / single-GPU tests); the pass's interior is issued before the exchange and runs on the GPU while
+    the host drives it, the border strips after the unpack.  transport "native" (opt-in, nccl backend): the
+    library's own RCCL communicator moves the halo on a communication stream while the pass's interior runs
+    (restir_halo_pass) -- no host round trip, no device synchronisation; the library checks that the
+    communicator's rank and size match the tile plan.  bench.py --mode halo --halo-transport native selects it."""
 
     def __init__(self, renderer: "restir.Renderer", width: int, height: int, tiles: tuple, rank: int, features,
                  group=None, transport: str | None = None):
@@ -35,8 +36,13 @@ class HaloFrames:
         self.tile = restir.tile_plan(width, height, tiles[0], tiles[1], rank, radius if self.passes else 0)
         self.send, self.recv = restir.halo_plan(width, height, tiles[0], tiles[1], rank, radius,
                                                 features.num_samples_in_reservoir)
+        if dist.get_rank(group) != rank or dist.get_world_size(group) != tiles[0] * tiles[1]:
+            raise ValueError(f"HaloFrames: rank {rank} of a {tiles[0]}x{tiles[1]} tile plan, but the group's rank is "
+                             f"{dist.get_rank(group)} of {dist.get_world_size(group)}: the halo peers are tile ranks")
         self.on_device = dist.get_backend(group) == "nccl"
-        self.transport = transport or ("native" if self.on_device else "torch")
+        self.transport = transport or "torch"
+        if self.transport not in ("torch", "native"):
+            raise ValueError(f"HaloFrames: unknown transport {self.transport!r}")
         if self.transport == "native":
             # one rank draws the communicator id, every rank receives it over the torch group
             idt = torch.zeros(restir._abi.RESTIR_RCCL_ID_BYTES, dtype=torch.uint8)
@@ -63,7 +69,10 @@ class HaloFrames:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
         if self.on_device:
-            self.torch.cuda.synchronize()   # the received bytes are complete before the library's stream reads them
+            # the received bytes are complete before the library's stream reads them: wait for torch's current
+            # stream only (req.wait() ordered it behind the transfer), not the whole device -- the pass's interior
+            # launch on the library's stream keeps running
+            self.torch.cuda.current_stream().synchronize()
 
     def render(self, prev, camera, want_rgb: bool = True, want_grid: bool = True):
         """One frame: (rgb of the owned tile [h][w][3], row 0 = top, or None; ReservoirGrid for temporal reuse)."""

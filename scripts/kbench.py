@@ -61,9 +61,6 @@ VARIANTS = {
     "bvh_leaf4": {"bvh.max_leaf": 4},
     "bvh_leaf1_sort": {"bvh.max_leaf": 1, "final.sort": 1},
     "bvh_leaf8": {"bvh.max_leaf": 8},
-    "spatial_p1024": {"spatial.blocks": 1024},
-    "spatial_p2048": {"spatial.blocks": 2048},
-    "spatial_p4096": {"spatial.blocks": 4096},
     "final_1d_global": {"final.2d": 0, "final.lds": 0},
     "final_1d_lds": {"final.2d": 0},
     "final_2d_global": {"final.lds": 0},

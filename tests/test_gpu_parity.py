@@ -210,13 +210,16 @@ SPATIAL_VARIANTS = {"gather": {"spatial.lean": 1, "spatial.lds": 0},
 SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 255}
 
 
-@pytest.mark.parametrize("name", ["nightclub_128pt", "cornell_parallelogram"])
-@pytest.mark.parametrize("N", [1, 2, 3])
-@pytest.mark.parametrize("mode", ["biased", "unbiased", "unbiased_vis"])
-@pytest.mark.parametrize("lean", list(SPATIAL_VARIANTS))
+# every (scene, N, combine mode) through the default knobs ("gather" selects the lean gather kernel for N = 1 biased
+# and the general kernels otherwise); the other variants differ only for N = 1 biased passes, so they run only there
+SPATIAL_CASES = ([("gather", name, N, mode) for name in ("nightclub_128pt", "cornell_parallelogram") for N in (1, 2, 3)
+                  for mode in ("biased", "unbiased", "unbiased_vis")] +
+                 [(lean, name, 1, "biased") for lean in SPATIAL_VARIANTS if lean != "gather"
+                  for name in ("nightclub_128pt", "cornell_parallelogram")])
+
+
+@pytest.mark.parametrize("lean,name,N,mode", SPATIAL_CASES)
 def test_spatial_pass_bit_exact(gpu, oracle, name, N, mode, lean):
-    if lean != "gather" and (N != 1 or mode != "biased"):
-        pytest.skip("the kernel variants differ only for N = 1 biased passes")
     for k, v in SPATIAL_VARIANTS[lean].items():
         gpu.set_tuning(k, v)
     try:

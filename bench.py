@@ -62,6 +62,13 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group of the multi-rank bench (nccl = RCCL, the real run; gloo = a rehearsal with "
                          "several ranks sharing one GPU)")
+    ap.add_argument("--halo-check", default="auto", choices=["auto", "on", "off"],
+                    help="N > 1: before timing, render one frame of this rank's tile through the RCCL reservoir halo "
+                         "(HaloFrames) and through the ghost zone, require them bit-identical (exit 3 otherwise) and "
+                         "time the halo-mode frame and its exchange (auto = on when the frame has spatial passes)")
+    ap.add_argument("--halo-transport", default="auto", choices=["auto", "native", "torch"],
+                    help="halo transport: the library's own RCCL communicator (native), torch.distributed p2p (torch); "
+                         "auto = native under nccl, torch under gloo")
     ap.add_argument("--traffic-csv", default=None,
                     help="rocprofv3 --pmc CSV (FETCH_SIZE / WRITE_SIZE) of this command for roofline.traffic")
     return ap.parse_args()
@@ -226,6 +233,54 @@ def spatial_px_per_launch(tile, passes, r):
     return tot / max(1, passes)
 
 
+def halo_check(torch, r, rank, world, local, cf, f, cam, GW, GH, tx, ty, passes, args, transport):
+    """N > 1: this rank's tile rendered through the reservoir halo exchange (HaloFrames: interior launched while
+    the border reservoirs move, border strips after) must equal, bit for bit, the same tile rendered with a ghost
+    zone (restir_render on tile + passes * r) -- exits 3 on any mismatch.  Then the halo-mode frame and the
+    exchange alone are timed.  Temporal reuse is off in the check (one frame from no predecessor), as in c2."""
+    import numpy as np
+    from romis_amd import _abi, distributed, restir
+    fc = _abi.Features.from_buffer_copy(f)
+    fc.temporal_reuse = 0
+    rec = {"transport": transport}
+    try:
+        hfc = distributed.HaloFrames(r, GW, GH, (tx, ty), rank, fc, transport=transport)
+    except _abi.RestirError as e:    # RCCL unavailable: the torch transport carries the same protocol
+        rec["native_error"] = str(e)[:200]
+        rec["transport"] = transport = "torch"
+        hfc = distributed.HaloFrames(r, GW, GH, (tx, ty), rank, fc, transport=transport)
+    r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
+    rgb_halo, _ = hfc.render(None, cam, want_rgb=True, want_grid=False)
+    r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
+    ghost_tile = restir.tile_plan(GW, GH, tx, ty, rank, passes * args.r)
+    rgb_ghost, _ = r.render_restir(None, cam, GW, GH, fc, tile=ghost_tile, want_grid=False)
+    bad = distributed.tile_mismatches(rgb_halo, rgb_ghost)
+    rec["check"] = "bit-exact" if bad == 0 else f"{bad} mismatching values"
+    if bad:
+        if rank == 0:
+            print(json.dumps({"error": "halo tile differs from the ghost-zone tile", "halo": rec}), flush=True)
+        torch.distributed.barrier()
+        sys.exit(3)
+    # halo-mode frames, timed like the main loop (max over ranks)
+    k = max(5, min(args.steps, 20))
+    for _ in range(2):
+        hfc.render(None, cam, want_rgb=False, want_grid=False)
+    barrier_sync(torch, world, r)
+    t0 = time.perf_counter()
+    for _ in range(k):
+        hfc.render(None, cam, want_rgb=False, want_grid=False)
+    barrier_sync(torch, world, r)
+    dt = max_over_ranks(torch, world, time.perf_counter() - t0, local) / k
+    bytes_pp = max_over_ranks(torch, world, float(sum(s.bytes for s in hfc.send)), local)
+    rec.update({"frame_ms": round(dt * 1e3, 4), "value": round(GW * GH * f.num_samples_in_reservoir / dt / 1e6, 3),
+                "bytes_per_pass": int(bytes_pp), "passes": passes,
+                "exchange_us_per_pass": round(distributed.exchange_probe(hfc.send, hfc.recv), 2),
+                "note": "value/frame_ms: the same frames with the reservoir halo exchanged over the process group "
+                        "before each spatial pass instead of a ghost zone; exchange_us_per_pass: the pass's "
+                        "segments moved alone (torch p2p, max over ranks), which the pass overlaps with its interior"})
+    return rec
+
+
 def main():
     args = parse()
     rank, world, local, torch = dist_setup(args.gpus, args.dist_backend)
@@ -261,11 +316,18 @@ def main():
     r.set_scene(sc)
     r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
     state = {"grid": None}
+    transport = args.halo_transport
+    if transport == "auto":
+        transport = "native" if args.dist_backend == "nccl" else "torch"
     hf = None
     if halo:
         from romis_amd import distributed
-        hf = distributed.HaloFrames(r, GW, GH, (tx, ty), rank, f)
+        hf = distributed.HaloFrames(r, GW, GH, (tx, ty), rank, f, transport=transport)
         tile = hf.tile
+    halo_rec = None
+    if world > 1 and passes > 0 and args.halo_check != "off":
+        halo_rec = halo_check(torch, r, rank, world, local, cf, f, cam, GW, GH, tx, ty, passes, args, transport)
+        r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
 
     def step():
         if hf is not None:   # RCCL halo exchange of the reservoirs before every spatial pass
@@ -380,6 +442,8 @@ def main():
             "cpu_baseline": cpu,
             "kernels": kernels,
         }
+        if halo_rec is not None:
+            out["halo"] = halo_rec
         print(json.dumps(out), flush=True)
     r.close()
     if world > 1:

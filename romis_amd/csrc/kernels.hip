@@ -1076,13 +1076,16 @@ struct Comb1 {
     uint32_t macc;
     bool has_pd;
     uint32_t h;   // ps + slot * 0x9E3779B9 of the next accept draw
-    __device__ __forceinline__ void take(float pd_in, float W, uint32_t M, v3 p, v3 c) {
+    // returns whether the input's sample was accepted
+    __device__ __forceinline__ bool take(float pd_in, float W, uint32_t M, v3 p, v3 c) {
         const float w = (pd_in * W) * (float)M;          // reservoir.cpp:50
         macc += M;
         wsum += w;
         const float u = rand01(mix32(h));
         h += 0x9E3779B9u;
-        if (u < (w / wsum)) { pos = p; col = c; chosen = w; pd = pd_in; has_pd = true; }
+        const bool acc = u < (w / wsum);
+        if (acc) { pos = p; col = c; chosen = w; pd = pd_in; has_pd = true; }
+        return acc;
     }
 };
 
@@ -1478,9 +1481,12 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
         if (rp_out) st_at(rp_out, pofs >> 2, 0.0f);
         return;
     }
-    // depth / normal heuristic (render_utils.cpp:114-118), one shared reciprocal of the pixel's depth
+    // depth / normal heuristic (render_utils.cpp:114-118), one shared reciprocal of the pixel's depth; both tests
+    // for every lane from one ds_read_b128 (a branch around the depth test only saved work on rejected lanes).  The
+    // correctly rounded division for depths outside the reciprocal's range is a wave-uniform branch: left to the
+    // compiler it is if-converted and evaluated for every neighbour of every lane.
     const double rt = rcp_d(cur.t);
-    const bool rt_ok = div_fast_ok(cur.t);
+    const bool rt_all = __all(div_fast_ok(cur.t));
     bool ok[kLeanK];
 #pragma unroll
     for (uint32_t n = 0; n < kLeanK; n++) {
@@ -1488,13 +1494,11 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
         if (n < K) {
             const float4 g = l_nt[qi[n]];
             const float nd = vdot(xyz(g), cur.N);
-            bool rej = nd < 0.90630778703f;
-            if (!rej) {
-                float q = div_by_rcp_d(g.w, rt);
-                if (!rt_ok) q = g.w / cur.t;
-                rej = fabsf(1.0f - q) > 0.1f;
+            float q = div_by_rcp_d(g.w, rt);
+            if (__builtin_expect(!rt_all, 0)) {
+                if (!div_fast_ok(cur.t)) q = g.w / cur.t;
             }
-            ok[n] = !rej;
+            ok[n] = !(nd < 0.90630778703f) && !(fabsf(1.0f - q) > 0.1f);
         }
     }
     float4 na[kLeanK], nb[kLeanK];
@@ -1546,6 +1550,116 @@ ROMIS_SPATIAL1_NTL_KERNEL(true, k_spatial1_ntl_dbg)
     }
 ROMIS_SPATIAL1_KERNEL(false, k_spatial1)
 ROMIS_SPATIAL1_KERNEL(true, k_spatial1_dbg)
+
+// ---------------------------------------------------------------------------------------------------------
+// k_spatial1u: the N = 1 unbiased pass (combineUnbiased, reservoir.cpp:68-104; C5 runs it with visibility reuse).
+// Same arithmetic, RNG slots and order as spatial_pixel<1, true>; what changes is how much of it runs:
+//  - the K neighbours' reservoirs are gathered once (one ahead of the consume sequence) and their M is kept for
+//    the Z sum, instead of being re-read;
+//  - the pixel's own target pdf comes from the producer's pdf cache (rp_in) when there is one;
+//  - Z only matters when the held sample's p-hat at the pixel is non-zero (W = 0 otherwise, reservoir.cpp:99), so
+//    the whole Z loop (K + 1 target pdfs at the inputs' pixels and their shadow rays) is skipped exactly then;
+//  - Z's own-pixel term is p-hat(pixel, held sample) = the value W uses (the same evaluation), and the term of the
+//    input the held sample came from is that input's p-hat of its own sample at its own pixel = the producer's pdf
+//    cache there (rp_in[q], the same evaluation on the same G-buffer record): one target pdf each instead of a
+//    recomputation;
+//  - the shadow rays (VIS) traverse the block's LDS copy of the BVH.
+// Only SoA planes (Region ps = 1) and K <= kLeanK take this path (launch_spatial checks).
+template <bool DBG, bool VIS>
+__device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
+                                               v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                               const float4* __restrict__ ia, const float4* __restrict__ ib,
+                                               float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
+                                               const float* __restrict__ rp_in, float* __restrict__ rp_out) {
+    const Bvh bvh = VIS ? stage_bvh(s, g_lds) : global_bvh(s);   // ends with a barrier (every thread gets here)
+    const GlTabs tb = gl_stage_tables();
+    uint32_t tile;
+    if (!xcd_tile(rg, num_tiles(rg), blockIdx.x, tile)) return;   // block-uniform; no barrier follows
+    const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
+    const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTileH);
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    const int x = tx0 + (int)(w * 8u + (l & 7u)), y = ty0 + (int)(l >> 3);
+    if (x >= (int)(rg.rx0 + rg.rw) || y >= (int)(rg.ry0 + rg.rh)) return;
+    const uint32_t K = f.K;   // <= kLeanK (host check)
+    const int rx = x - (int)rg.vx0, ry = y - (int)rg.vy0;
+    const uint32_t pofs = ((uint32_t)ry * rg.vw + (uint32_t)rx) << 4;
+    const float4 cn = ld_at(n_t, pofs), cpm = ld_at(p_mat, pofs);
+    const float4 ca = ld_at(ia, pofs), cb = ld_at(ib, pofs);
+    const float pd_cached = rp_in ? ld_at(rp_in, pofs >> 2) : 0.0f;
+    // neighbour draws (render_utils.cpp:108-111), clamped to the image, then to the stored view
+    const int xlo = max(0, (int)rg.vx0) - (int)rg.vx0, xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1 - (int)rg.vx0;
+    const int ylo = max(0, (int)rg.vy0) - (int)rg.vy0, yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1 - (int)rg.vy0;
+    const uint32_t ps = pix_state(key, (uint32_t)y * rg.W + (uint32_t)x);
+    const uint32_t span = 2u * f.R + 1u;
+    const int bx = rx - (int)f.R, by = ry - (int)f.R;
+    uint32_t qo[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        qo[n] = pofs;
+        if (n < K) {
+            const int nx = min(max(bx + (int)__umulhi(draw(ps, 2u * n), span), xlo), xhi);
+            const int ny = min(max(by + (int)__umulhi(draw(ps, 2u * n + 1u), span), ylo), yhi);
+            qo[n] = ((uint32_t)ny * rg.vw + (uint32_t)nx) << 4;
+        }
+    }
+    float4 na[kLeanK], nb[kLeanK];
+    na[0] = ld_at(ia, qo[0]);
+    nb[0] = ld_at(ib, qo[0]);
+    const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
+    const float pd_cur = rp_in ? pd_cached : target_pdf(s, f, cur, xyz(ca), xyz(cb), tb);
+    Comb1 cmb;
+    cmb.pos = mk(0.0f, 0.0f, 0.0f); cmb.col = mk(0.0f, 0.0f, 0.0f);
+    cmb.wsum = ROMIS_FLT_MIN; cmb.chosen = 0.0f; cmb.pd = 0.0f; cmb.macc = 0u; cmb.has_pd = false;
+    cmb.h = ps + 2u * K * 0x9E3779B9u;
+    uint32_t Mn[kLeanK];
+    uint32_t src = kLeanK;   // the input the held sample came from (kLeanK = the pixel itself)
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        if (n + 1 < kLeanK && n + 1 < K) { na[n + 1] = ld_at(ia, qo[n + 1]); nb[n + 1] = ld_at(ib, qo[n + 1]); }
+        Mn[n] = 0u;
+        if (n < K) {
+            const v3 p = xyz(na[n]), c = xyz(nb[n]);
+            Mn[n] = __float_as_uint(nb[n].w);
+            if (cmb.take(target_pdf(s, f, cur, p, c, tb), na[n].w, Mn[n], p, c)) src = n;
+        }
+    }
+    if (cmb.take(pd_cur, ca.w, __float_as_uint(cb.w), xyz(ca), xyz(cb))) src = kLeanK;
+    float pc = cmb.pd;
+    if (!cmb.has_pd) pc = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, cmb.pos, cmb.col, tb);
+    float W = 0.0f;
+    if (pc != 0.0f) {   // W = 0 whatever Z is when p-hat(pixel, held sample) == 0 (reservoir.cpp:99)
+        unsigned long long Z = 0ull;
+#pragma unroll
+        for (uint32_t n = 0; n < kLeanK; n++) {
+            if (n < K) {
+                const float4 qn = ld_at(n_t, qo[n]), qp = ld_at(p_mat, qo[n]);
+                const Px rp = make_px(s, qn, qp, origin, qo[n] >> 4);
+                const float pd = (src == n && rp_in) ? ld_at(rp_in, qo[n] >> 2) : target_pdf(s, f, rp, cmb.pos, cmb.col, tb);
+                if (pd > 0.0f && (!VIS || visible(bvh, rp.P, cmb.pos))) Z += Mn[n];
+            }
+        }
+        if (pc > 0.0f && (!VIS || visible(bvh, cur.P, cmb.pos))) Z += __float_as_uint(cb.w);
+        if (Z != 0ull) W = (rcp_rn(pc) * rcp_rn((float)Z)) * cmb.wsum;
+    }
+    st_at(oa, pofs, make_float4(cmb.pos.x, cmb.pos.y, cmb.pos.z, W));
+    st_at(ob, pofs, make_float4(cmb.col.x, cmb.col.y, cmb.col.z, __uint_as_float(cmb.macc)));
+    if (DBG) st_at(odbg, pofs >> 1, make_float2(cmb.wsum, cmb.chosen));
+    if (rp_out) st_at(rp_out, pofs >> 2, pc);
+}
+
+#define ROMIS_SPATIAL1U_KERNEL(DBG, VIS, NAME)                                                                         \
+    extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f,     \
+                                                                           uint32_t key, float ox, float oy, float oz,  \
+                                                                           const float4* n_t, const float4* p_mat,      \
+                                                                           const float4* ia, const float4* ib,          \
+                                                                           float4* oa, float4* ob, float2* odbg,        \
+                                                                           const float* rp_in, float* rp_out) {         \
+        spatial1u_body<DBG, VIS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);      \
+    }
+ROMIS_SPATIAL1U_KERNEL(false, false, k_spatial1u)
+ROMIS_SPATIAL1U_KERNEL(true, false, k_spatial1u_dbg)
+ROMIS_SPATIAL1U_KERNEL(false, true, k_spatial1u_vis)
+ROMIS_SPATIAL1U_KERNEL(true, true, k_spatial1u_vis_dbg)
 
 
 // ---------------------------------------------------------------------------------------------------------
@@ -1751,14 +1865,24 @@ extern "C" __global__ __launch_bounds__(256) void k_halo_unpack(Region rg, HaloS
 // Streaming read (restir_measure_read_bandwidth): grid-stride 16-byte loads, 4 in flight per lane, one partial
 // sum per block so nothing is dead code.
 extern "C" __global__ __launch_bounds__(256) void k_read_stream(const float4* __restrict__ buf, size_t n4, float* sink) {
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    // The HBM read-bandwidth probe (restir_measure_read_bandwidth): each wave sweeps its own contiguous slice in
+    // order, eight 1-KiB non-temporal loads in flight per lane-iteration (8 KiB per wave, 256 KiB per CU at 8
+    // blocks per CU), so DRAM pages are read sequentially and the L2 keeps none of the once-read bytes.
+    const size_t waves = (size_t)gridDim.x * (blockDim.x >> 6);
+    const size_t wave = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const size_t lane = threadIdx.x & 63u;
+    const size_t per = (n4 / waves) & ~(size_t)511;            // whole 8-load steps per wave
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v* p = reinterpret_cast<const f4v*>(buf) + wave * per + lane;
     float acc = 0.0f;
-    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n4; i += 4 * stride) {
-        const float4 a = buf[i], b = buf[i + stride], c = buf[i + 2 * stride], d = buf[i + 3 * stride];
-        acc += ((a.x + b.y) + (c.z + d.w));
+    for (size_t k = 0; k < per; k += 512) {
+        f4v v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = __builtin_nontemporal_load(p + k + 64 * u);
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc += v[u].x + v[u].w;
     }
-    for (; i < n4; i += stride) acc += buf[i].x;
+    for (size_t i = waves * per + wave * 64 + lane; i < n4; i += waves * 64) acc += buf[i].x;   // the remainder
     if (acc == 12345.0f) sink[blockIdx.x % 256u] = acc;   // buffers are zero: never taken, but not provably so
 }
 
@@ -2512,8 +2636,22 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
     Region rg = with_map(rg0, tu.spatial_xcd);   // XCD-banded order works on 2D tiles
     if (rg.map2d && tu.spatial_wave8) rg.map2d = 2u;
     uint32_t grid = items_of(rg);
-    if (tu.spatial_lean && !f.unbiased && f.N == 1 && f.K <= kLeanK && rg.ps == 1u && rg.map2d == 2u &&
-        (size_t)rg.vw * rg.vh * 16u <= 0xFFFFFFFFull) {
+    const size_t bvh_bytes = bvh_lds_bytes(s);
+    const bool lean = tu.spatial_lean && f.N == 1 && f.K <= kLeanK && rg.ps == 1u && rg.map2d == 2u &&
+                      (size_t)rg.vw * rg.vh * 16u <= 0xFFFFFFFFull;
+    if (lean && f.unbiased && (!f.spatial_vis || bvh_bytes <= kLdsBudget)) {
+        // combineUnbiased, N = 1: one block per tile in the XCD order of the biased pass (xcd_tile)
+        const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
+        rg.xcd_rows = tu.spatial_xcd_rows == kXcdRowsAuto ? std::max(1u, std::min(8u, 8192u / std::max(rg.rw, 1u)))
+                                                          : tu.spatial_xcd_rows;
+        if (rg.xcd_rows) grid = 8u * ((((nty + rg.xcd_rows - 1) / rg.xcd_rows) + 7u) / 8u) * rg.xcd_rows * ntx;
+        auto k = f.spatial_vis ? (odbg ? k_spatial1u_vis_dbg : k_spatial1u_vis) : (odbg ? k_spatial1u_dbg : k_spatial1u);
+        ROMIS_LAUNCH(k, dim3(grid), dim3(kBlock), f.spatial_vis ? bvh_bytes : 0, stream, s, rg, f, key, o[0], o[1], o[2],
+                     n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
+        if (rp_written) *rp_written = rp_out != nullptr;
+        return hipGetLastError();
+    }
+    if (lean && !f.unbiased) {
         // one block per tile (the lean kernels do not loop over tiles, so spatial.blocks does not apply here),
         // grid rounded to the XCD that owns the most tiles (xcd_tile)
         const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
@@ -2563,9 +2701,8 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
     if (tu.spatial_blocks) grid = std::min(grid, std::max(8u, tu.spatial_blocks));   // the general kernels loop
     auto k = f.unbiased ? (f.N == 1 ? k_spatial_n1_unbiased : (f.N == 2 ? k_spatial_n2_unbiased : k_spatial_n0_unbiased))
                         : (f.N == 1 ? k_spatial_n1_biased : (f.N == 2 ? k_spatial_n2_biased : k_spatial_n0_biased));
-    const size_t lds = bvh_lds_bytes(s);
-    const uint32_t bvh_lds = (f.unbiased && f.spatial_vis && lds <= kLdsBudget) ? 1u : 0u;
-    ROMIS_LAUNCH(k, dim3(grid), dim3(kBlock), bvh_lds ? lds : 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat,
+    const uint32_t bvh_lds = (f.unbiased && f.spatial_vis && bvh_bytes <= kLdsBudget) ? 1u : 0u;
+    ROMIS_LAUNCH(k, dim3(grid), dim3(kBlock), bvh_lds ? bvh_bytes : 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat,
                        ia, ib, oa, ob, odbg, bvh_lds);
     return hipGetLastError();
 }
@@ -2606,7 +2743,7 @@ hipError_t launch_halo_unpack(const Region& rg, const HaloSegs& hs, uint32_t N, 
 }
 
 hipError_t launch_read_stream(const float4* buf, size_t n4, float* sink, hipStream_t stream) {
-    hipLaunchKernelGGL(k_read_stream, dim3(256 * 16), dim3(kBlock), 0, stream, buf, n4, sink);
+    hipLaunchKernelGGL(k_read_stream, dim3(256 * 8), dim3(kBlock), 0, stream, buf, n4, sink);   // 8 blocks per CU, one round
     return hipGetLastError();
 }
 

@@ -89,3 +89,59 @@ class HaloFrames:
             self.r.halo_unpack(self.recvbuf.data_ptr(), rb, host)
             self.r.halo_spatial_border()
         return self.r.halo_end(self.tile, want_rgb, want_grid)
+
+
+def tile_mismatches(mine, other, group=None) -> int:
+    """Bit-for-bit comparison of two renderings of this rank's tile (float32 arrays of one shape), summed over the
+    group's ranks: the number of 32-bit words that differ anywhere (a shape mismatch counts every word)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    a = np.ascontiguousarray(mine, dtype=np.float32)
+    b = np.ascontiguousarray(other, dtype=np.float32)
+    n = int((a.view(np.uint32) != b.view(np.uint32)).sum()) if a.shape == b.shape else max(a.size, b.size, 1)
+    if not dist.is_initialized():
+        return n
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    t = torch.tensor([n], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return int(t.item())
+
+
+def exchange_probe(send, recv, group=None, iters: int = 20) -> float:
+    """Microseconds of one halo exchange -- the plan's segments (restir_halo_plan: the bytes and peers a spatial pass
+    moves) as one batch of torch.distributed point-to-point transfers on device buffers (nccl = RCCL over xGMI;
+    host buffers under gloo) -- median of `iters`, max over the group's ranks.  The pass itself overlaps this with
+    the interior launch; this is the transfer alone."""
+    import statistics
+    import time
+
+    import torch
+    import torch.distributed as dist
+    on_dev = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_dev else torch.device("cpu")
+    sb = torch.zeros(max(1, sum(s.bytes for s in send)), dtype=torch.uint8, device=dev)
+    rb = torch.zeros(max(1, sum(r.bytes for r in recv)), dtype=torch.uint8, device=dev)
+
+    def once():
+        ops = []
+        for s, r in zip(send, recv):
+            ops.append(dist.P2POp(dist.isend, sb[s.offset:s.offset + s.bytes], s.rank, group))
+            ops.append(dist.P2POp(dist.irecv, rb[r.offset:r.offset + r.bytes], r.rank, group))
+        if ops:
+            for q in dist.batch_isend_irecv(ops):
+                q.wait()
+        if on_dev:
+            torch.cuda.current_stream().synchronize()
+
+    once()
+    times = []
+    for _ in range(iters):
+        dist.barrier(group=group)
+        t0 = time.perf_counter()
+        once()
+        times.append(time.perf_counter() - t0)
+    us = statistics.median(times) * 1e6
+    t = torch.tensor([us], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Instruction-budget variants of the spatial pass (k_spatial1_ntl): copies of kernels.hip with one piece of the
+per-pixel work replaced by a cheap stand-in that keeps its data dependences (results change; only instruction
+counts and time are compared), built into romis_amd/_build/variants/<name>/libromis_amd.so.  The product source is
+never modified.  Run scripts/pmc_kbench.sh / kbench_libs.sh against the variants on the GPU.
+
+    python scripts/budget_variants.py            # builds every variant
+"""
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from romis_amd import build  # noqa: E402
+
+SRC = os.path.join(build.CSRC, "kernels.hip")
+
+
+def body_span(src):
+    a = src.index("__device__ __forceinline__ void spatial1_ntl_body(")
+    b = src.index("#ifndef ROMIS_SPATIAL1_NTL_WPE")
+    return a, b
+
+
+# name -> list of (regex, replacement) applied inside spatial1_ntl_body only
+VARIANTS = {
+    # the K neighbour target pdfs (the combine's p-hat chains) -> a 2-op stand-in on the same inputs
+    "no_phat": [(r"target_pdf\(s, f, cur, p, c, tb\)", "fabsf(p.x + c.y)")],
+    # the neighbour offset draws (2 mix32 + umulhi + clamp each) -> a multiply-add of the pixel state
+    "no_rng": [(r"__umulhi\(draw\(ps, 2u \* n\), span\)", "((ps + 2u * n) % span)"),
+               (r"__umulhi\(draw\(ps, 2u \* n \+ 1u\), span\)", "((ps >> 8) + n) % span")],
+    # the whole combine (takes) -> sums
+    "no_take": [(r"cmb\.take\(target_pdf\(s, f, cur, p, c, tb\), na\[n\]\.w, __float_as_uint\(nb\[n\]\.w\), p, c\);",
+                 "cmb.wsum += target_pdf(s, f, cur, p, c, tb) * na[n].w; cmb.macc += __float_as_uint(nb[n].w);")],
+}
+
+
+def main():
+    src = open(SRC).read()
+    a, b = body_span(src)
+    for name, subs in VARIANTS.items():
+        body = src[a:b]
+        for pat, rep in subs:
+            body, n = re.subn(pat, rep, body)
+            if n == 0:
+                raise SystemExit(f"{name}: pattern not found: {pat}")
+        vdir = os.path.join(build.OUT, "variants", name)
+        os.makedirs(vdir, exist_ok=True)
+        path = os.path.join(vdir, "kernels.hip")
+        with open(path, "w") as fh:
+            fh.write(src[:a] + body + src[b:])
+        obj = os.path.join(vdir, "kernels.hip.o")
+        subprocess.check_call([build.HIPCC] + build.COMMON + build.SOURCES[0][1] + ["-c", path, "-o", obj])
+        objs = [obj] + [os.path.join(build.OUT, s + ".o") for s, _ in build.SOURCES[1:]]
+        subprocess.check_call([build.HIPCC, "-shared", f"--offload-arch={build.ARCH}", "-fno-gpu-rdc", "-o",
+                               os.path.join(vdir, "libromis_amd.so")] + objs)
+        print(name, "built")
+
+
+if __name__ == "__main__":
+    main()

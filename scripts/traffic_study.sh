@@ -1,0 +1,24 @@
+#!/bin/bash
+# HBM traffic of the spatial pass (FETCH_SIZE / WRITE_SIZE, separate --pmc passes) at C2 (1080p) and C4 (4K) for
+# the XCD chunk order (default) and one contiguous band per XCD (spatial.xcd_rows = 0), plus the kernel times of
+# the same variants.   scripts/traffic_study.sh <tag>
+set -o pipefail
+TAG=${1:-traffic}
+REPO=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$REPO/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$REPO" || exit 1
+export TMPDIR=/tmp
+for CFG in c2 c4; do
+    for V in "chunks:spatial.xcd_rows=255" "bands:spatial.xcd_rows=0"; do
+        NAME=${V%%:*}
+        for C in FETCH_SIZE WRITE_SIZE; do
+            timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/${CFG}_${NAME}_$C" -o run -- \
+                python3 scripts/cfg_kbench.py --config $CFG --rounds 1 --frames 3 --variants "$V" \
+                > "$OUT/${CFG}_${NAME}_$C.json" 2> "$OUT/${CFG}_${NAME}_$C.err" || exit 40
+        done
+    done
+    timeout -k 10 200 python3 scripts/cfg_kbench.py --config $CFG --rounds 5 --frames 5 \
+        --variants "chunks:spatial.xcd_rows=255" "bands:spatial.xcd_rows=0" > "$OUT/${CFG}_times.json" 2> "$OUT/${CFG}_times.err" || exit 41
+    cat "$OUT/${CFG}_times.json"
+done

@@ -1,6 +1,8 @@
 """The C++ host wrapper (include/romis_amd/restir.hpp): compiles and links against libromis_amd.so on CPU;
 on the GPU, a C++ program rendering through it reproduces the oracle's frames bit-for-bit."""
+import ctypes as C
 import os
+import re
 import struct
 import subprocess
 
@@ -67,10 +69,21 @@ def test_wrapper_frames_match_oracle(tmp_path, frames, N, passes, temporal):
     cam = scene.camera_for(name, W, H)
     write_scene(tmp_path / "s.bin", sc, cam)
     out = tmp_path / "o.rgb"
+    renders = tmp_path / "renders"
     subprocess.check_call([build_cpp(), str(tmp_path / "s.bin"), str(out), str(W), str(H), str(frames), str(N),
-                           str(passes), str(temporal)], timeout=120)
+                           str(passes), str(temporal), "0", str(renders)], timeout=120)
     got = np.fromfile(out, np.float32).reshape(H, W, 3)
     f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=passes, temporal_reuse=temporal)
+    # renderRayTraced saved the configuration record of its renders (render.cpp:281-287): <time>.json files (one
+    # per second at most, as the reference's names collide within a second) holding restir_features_json's bytes
+    recs = sorted(renders.glob("*.json"))
+    assert recs and all(re.fullmatch(r"\d\d-\d\d-\d{4} \d\d-\d\d-\d\d\.json", p.name) for p in recs)
+    lib = _abi.load_library()
+    n = C.c_size_t(0)
+    lib.restir_features_json(C.byref(f), None, None, 0, C.byref(n))
+    buf = C.create_string_buffer(n.value + 1)
+    assert lib.restir_features_json(C.byref(f), None, buf, n.value + 1, C.byref(n)) == 0
+    assert all(p.read_bytes() == buf.raw[:n.value] for p in recs)
     osc = pyoracle.OracleScene(sc)
     prev = None
     for fr in range(frames):

@@ -668,3 +668,72 @@ def test_full_size_frames_c4_c5_band_parity(gpu, oracle, cfg):
         want, _, _ = oracle.render_frame(osc, cam, f, Wf, Hf, view=view, rect=rect, threads=16)
         r0 = Hf - (y0 + rows)          # RGB row 0 = top of the image
         assert_bits(rgb[r0:r0 + rows], want, f"{cfg} rows {y0}..{y0 + rows - 1}")
+
+
+def test_full_size_c1_frame_matches_oracle(gpu, oracle):
+    """C1 (BASELINE configs[0]) at its full size: CornellBox-Mirror 512x512, 1 parallelogram light, M = 32, RIS
+    only -- the whole frame's RGB and returned grid against the oracle, bit for bit."""
+    name, Wf, Hf = "cornell_parallelogram", 512, 512
+    s = get_scene(name)
+    gpu.set_scene(s)
+    cam = scene.camera_for(name, Wf, Hf)
+    f = _abi.default_features(initial_light_samples=32, num_samples_in_reservoir=1, spatial_resampling_passes=0,
+                              spatial_reuse=0, temporal_reuse=0)
+    gpu.set_seed(SEED, 0)
+    rgb, grid = gpu.render_restir(None, cam, Wf, Hf, f)
+    want, res, _ = oracle.render_frame(oracle.OracleScene(s), cam, f, Wf, Hf, SEED, 0, threads=16)
+    assert_bits(rgb, want, "C1 rgb")
+    assert_grid(grid, res, "C1")
+    assert rgb.mean() > 0.01
+
+
+def test_full_size_c3_sequence_band_parity(gpu, oracle):
+    """C3 at its full size: 1080p nightclub, 128 point lights, M = 32, two spatial passes, temporal reuse over 4
+    frames threaded through the frame pool (each predecessor released as the sequence goes, and an unrelated frame
+    rendered between frames 1 and 2 so recycled records are reused).  Checked on sampled row bands: frame f's rows
+    depend on frame f - 1's grid within passes * r = 20 rows (temporal reuse is same-pixel, render_utils.cpp:155;
+    spatial reuse reads +-r per pass, :91), so the oracle renders frame 0 on the band grown by 4 * 20 = 80 rows,
+    frame 1 on the band grown by 60, ... each frame's view being the previous frame's owned rows.  Every frame's
+    RGB and the last frame's grid are compared on the band, bit for bit."""
+    name, Wf, Hf, P, R, frames = "nightclub_128pt", 1920, 1080, 2, 10, 4
+    s = get_scene(name)
+    gpu.set_scene(s)
+    osc = oracle.OracleScene(s)
+    cam = scene.camera_for(name, Wf, Hf)
+    f = _abi.default_features(initial_light_samples=32, num_samples_in_reservoir=1, spatial_resampling_passes=P,
+                              spatial_resample_radius=R, temporal_reuse=1)
+    gpu.set_seed(SEED, 0)
+    rgbs, grid = [], None
+    for fr in range(frames):
+        rgb, nxt = gpu.render_restir(grid, cam, Wf, Hf, f)
+        grid = nxt                      # the predecessor is released here (records back to the pool)
+        rgbs.append(rgb)
+        if fr == 1:                     # an unrelated frame takes recycled records, then hands them back
+            other, _ = gpu.render_restir(None, scene.camera_for("cornell_1024", Wf, Hf), Wf, Hf, f)
+            del other
+            gpu.set_seed(SEED, fr + 1)
+    pos, col, w, m = grid.download()
+    rows, grow = 6, P * R
+    for y0 in (0, 531, Hf - rows):
+        prev = None
+        for fr in range(frames):
+            g_rect = (frames - 1 - fr) * grow          # owned rows of frame fr: the band grown by this
+            ry0, ry1 = max(0, y0 - g_rect), min(Hf, y0 + rows + g_rect)
+            vy0, vy1 = max(0, ry0 - grow), min(Hf, ry1 + grow)
+            view, rect = oracle.Rect(0, vy0, Wf, vy1 - vy0), oracle.Rect(0, ry0, Wf, ry1 - ry0)
+            want, res, _ = oracle.render_frame(osc, cam, f, Wf, Hf, SEED, fr, prev=prev, view=view, rect=rect,
+                                               threads=16)
+            top = Hf - ry1                             # RGB row 0 = top of the image
+            assert_bits(rgbs[fr][top:top + (ry1 - ry0)], want, f"C3 frame {fr} rows {ry0}..{ry1 - 1}")
+            # the next frame's view is this frame's owned rows: its predecessor grid is those rows of `res`
+            a, b = res
+            sl = slice((ry0 - vy0) * Wf, (ry1 - vy0) * Wf)
+            prev = (np.ascontiguousarray(a[:, sl]), np.ascontiguousarray(b[:, sl]))
+        a, b = prev                                    # frame 3's grid on its owned band (= the checked rows)
+        a = a.reshape(1, -1, Wf, 4)
+        b = b.reshape(1, -1, Wf, 4)
+        gs = slice(y0, y0 + rows)
+        assert_bits(pos[:, gs], np.ascontiguousarray(a[..., :3]), f"C3 grid position rows {y0}..")
+        assert_bits(w[:, gs], np.ascontiguousarray(a[..., 3]), f"C3 grid W rows {y0}..")
+        assert_bits(col[:, gs], np.ascontiguousarray(b[..., :3]), f"C3 grid colour rows {y0}..")
+        assert np.array_equal(m[:, gs], np.ascontiguousarray(b[..., 3]).view(np.uint32)), f"C3 grid M rows {y0}.."

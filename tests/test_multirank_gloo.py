@@ -167,3 +167,51 @@ def test_halo_exchange_with_temporal_matches_single_frames(tmp_path, world, tile
     mp.spawn(_halo_worker, args=(world, _free_port(), tiles, passes, 3, result, name), nprocs=world, join=True)
     with open(result) as fh:
         assert fh.read() == "ok"
+
+
+# ---- bench.py's N > 1 halo self-check (romis_amd.distributed.tile_mismatches / exchange_probe) -----------------
+def _selfcheck_worker(rank, world, port, tiles, result_path):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from oracle import pyoracle
+    from romis_amd import _abi, distributed, restir, scene
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=2, temporal_reuse=0)
+    R, P = f.spatial_resample_radius, f.spatial_resampling_passes
+    name = "nightclub_128pt"
+    osc = pyoracle.OracleScene(scene.bench_scene(name))
+    cam = scene.camera_for(name, W, H)
+    # the two decompositions bench.py compares, here on the oracle: ghost zone (tile + P * r) and the tile owned
+    # with an r-ring that an exchange fills (the halo protocol itself is pinned by the halo tests above; its
+    # frame on the owned tile equals the full frame's, so the ghost tile's)
+    tg = restir.tile_plan(W, H, tiles[0], tiles[1], rank, P * R)
+    ghost, _, _ = pyoracle.render_frame(osc, cam, f, W, H, view=pyoracle.Rect(tg.gx0, tg.gy0, tg.gwidth, tg.gheight),
+                                        rect=pyoracle.Rect(tg.x0, tg.y0, tg.width, tg.height), threads=1)
+    full, _, _ = pyoracle.render_frame(osc, cam, f, W, H, threads=1)
+    r0 = H - (tg.y0 + tg.height)
+    owned = np.ascontiguousarray(full[r0:r0 + tg.height, tg.x0:tg.x0 + tg.width])
+    same = distributed.tile_mismatches(owned, ghost)
+    flipped = ghost.copy()
+    if rank == world - 1:               # one flipped bit on the last rank must reach every rank's count
+        flipped.view(np.uint32)[0, 0, 0] ^= 1
+    diff = distributed.tile_mismatches(owned, flipped)
+    shape = distributed.tile_mismatches(owned, ghost[:-1] if rank == 0 else ghost)
+    send, recv = restir.halo_plan(W, H, tiles[0], tiles[1], rank, R, 1)
+    us = distributed.exchange_probe(send, recv, iters=3)
+    with open(f"{result_path}.{rank}", "w") as fh:
+        fh.write(f"{same} {diff} {int(shape >= ghost.size // 3)} {int(us > 0)}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,tiles", [(2, (2, 1)), (8, (4, 2))])
+def test_bench_halo_self_check_over_gloo(tmp_path, world, tiles, abi_lib, oracle):
+    """bench.py --gpus N's self-check: equal tiles count 0 mismatches on every rank, a single flipped bit on one
+    rank is seen by all, a shape mismatch counts the whole tile; the exchange probe moves the plan's segments."""
+    result = str(tmp_path / "r")
+    mp.spawn(_selfcheck_worker, args=(world, _free_port(), tiles, result), nprocs=world, join=True)
+    for rank in range(world):
+        with open(f"{result}.{rank}") as fh:
+            assert fh.read().split() == ["0", "1", "1", "1"], rank

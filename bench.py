@@ -122,9 +122,13 @@ def committed_traffic(cfg):
         with open(path) as fh:
             rec = json.load(fh)
         keys = ("scene", "tile", "M", "N", "k", "r", "passes")
-        rc = rec.get("config") or {}
-        if rec.get("source_hash") == build.source_hash() and all(rc.get(k) == cfg.get(k) for k in keys):
-            return rec["traffic_bytes_per_launch"], rec.get("profile")
+        if rec.get("source_hash") != build.source_hash():
+            return None, None
+        # entries: per config and XCD tile order (scripts/traffic_json.py); the default order is "chunks"
+        for e in rec.get("entries") or [rec]:
+            rc = e.get("config") or {}
+            if e.get("xcd_order", "chunks") == "chunks" and all(rc.get(k) == cfg.get(k) for k in keys):
+                return e["traffic_bytes_per_launch"], rec.get("profile")
     except (OSError, ValueError, KeyError):
         pass
     return None, None
@@ -243,14 +247,21 @@ def halo_check(torch, r, rank, world, local, cf, f, cam, GW, GH, tx, ty, passes,
     fc = _abi.Features.from_buffer_copy(f)
     fc.temporal_reuse = 0
     rec = {"transport": transport}
+    rgb_halo = None
     try:
         hfc = distributed.HaloFrames(r, GW, GH, (tx, ty), rank, fc, transport=transport)
+        r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
+        rgb_halo, _ = hfc.render(None, cam, want_rgb=True, want_grid=False)
     except _abi.RestirError as e:    # RCCL unavailable: the torch transport carries the same protocol
         rec["native_error"] = str(e)[:200]
+    failed = torch.tensor([1 if rgb_halo is None else 0], dtype=torch.int32,
+                          device=torch.device("cuda", local) if args.dist_backend == "nccl" else "cpu")
+    torch.distributed.all_reduce(failed, op=torch.distributed.ReduceOp.MAX)
+    if int(failed.item()):           # every rank falls back together
         rec["transport"] = transport = "torch"
         hfc = distributed.HaloFrames(r, GW, GH, (tx, ty), rank, fc, transport=transport)
-    r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
-    rgb_halo, _ = hfc.render(None, cam, want_rgb=True, want_grid=False)
+        r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
+        rgb_halo, _ = hfc.render(None, cam, want_rgb=True, want_grid=False)
     r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
     ghost_tile = restir.tile_plan(GW, GH, tx, ty, rank, passes * args.r)
     rgb_ghost, _ = r.render_restir(None, cam, GW, GH, fc, tile=ghost_tile, want_grid=False)
@@ -421,6 +432,21 @@ def main():
                         "achieved": round(tf, 2), "peak": FP32_VECTOR_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": round(tf / FP32_VECTOR_PEAK_TFS, 4), "flop_per_candidate": RIS_FLOP_PER_CANDIDATE,
                         "candidates_per_launch": cand, "avg_launch_us": round(avg_s * 1e6, 2)}
+    # visibility reuse (c5): the spatial pass is ray-bound, so its rate is reported as shadow-ray slots per second --
+    # (k + 1) N per pixel, an upper bound on the rays cast (a ray is skipped where p-hat = 0 and the whole Z loop
+    # where W = 0) -- next to the final pass's one ray per pixel per sub-reservoir
+    roofline_rays = None
+    sms, sn = kt_all.get("spatial", (0.0, 0))
+    fms, fn = kt_all.get("final", (0.0, 0))
+    if cf["vis"] and sn and fn:
+        px = tile.width * tile.height
+        slots = px * (args.k + 1) * args.N
+        roofline_rays = {"kernel": "k_spatial (unbiased + visibility)", "bound": "rays",
+                         "ray_slots_per_launch": slots, "avg_launch_us": round(sms / sn * 1e3, 2),
+                         "grays_per_s": round(slots / (sms / sn * 1e-3) / 1e9, 2),
+                         "final_grays_per_s": round(px * args.N / (fms / fn * 1e-3) / 1e9, 2),
+                         "note": "ray slots = (k+1) N per pixel, an upper bound on the shadow rays cast; final = 1 per "
+                                 "pixel and sub-reservoir (also an upper bound: no ray where the shaded value is 0)"}
     kernels["note"] = "separate run after the timed region, every kernel's dispatch recording HIP events"
     if rank == 0:
         out = {
@@ -439,6 +465,7 @@ def main():
             "config": cfg,
             "roofline": roofline,
             "roofline_ris": roofline_ris,
+            "roofline_rays": roofline_rays,
             "cpu_baseline": cpu,
             "kernels": kernels,
         }

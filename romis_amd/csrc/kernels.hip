@@ -1394,6 +1394,29 @@ ROMIS_SPATIAL1_LDS_KERNEL(true, false, 3, k_spatial1_ldsr_dbg)
 // no ds_write pass), issued together with the pixel's own records; the powf tables are staged in the same phase,
 // so the block passes one barrier (81.3-82.5 -> 81.3 us in kbench, profiles/r2/glds).  The accepted neighbours' reservoirs stay global gathers, one neighbour ahead of the consume sequence (as in
 // spatial1_pixel).  Same arithmetic, RNG slots and update order as spatial1_pixel; R <= kLdsSpatialR.
+// The n_t window of an ntl spatial block: the tile grown by R, clipped, AW entries per row, copied to LDS by
+// LDS-DMA.  Each wave's 64 consecutive window entries l_nt[256k + 64w + lane] are written straight from global
+// memory (global_load_lds_dwordx4, lane l at the wave-uniform base + 16 l), no VGPR round trip; the caller waits
+// for them (explicit s_waitcnt vmcnt(0)) before its barrier, so after it every wave may read every entry.
+__device__ __forceinline__ void ntl_stage_window(const Region& rg, const float4* __restrict__ n_t, float4* l_nt, int ax0,
+                                                 int ay0, uint32_t AW, uint32_t n_apron) {
+    constexpr uint32_t kPer = (kApronMax + 255u) / 256u;
+    const uint32_t magic = 0xFFFFFFFFu / AW + 1u;
+    const uint32_t w64 = (threadIdx.x >> 6) << 6;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+        const uint32_t i = threadIdx.x + 256u * k;
+        if (i < n_apron) {
+            uint32_t r = __umulhi(i, magic);   // i / AW for i < 2^16
+            if (r * AW > i) r--;
+            const uint32_t c = i - r * AW;
+            const float4* src = n_t + (((uint32_t)(ay0 - (int)rg.vy0) + r) * rg.vw + (uint32_t)(ax0 - (int)rg.vx0) + c);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(l_nt + 256u * k + w64), 16, 0, 0);
+        }
+    }
+}
+
 template <bool DBG>
 __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
                                                   v3 origin, const float4* __restrict__ n_t,
@@ -1427,27 +1450,7 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
         cb = ld_at(ib, pofs);
         if (rp_in) pd_cached = ld_at(rp_in, pofs >> 2);
     }
-    {
-        // LDS-DMA: each wave's 64 consecutive window entries l_nt[256k + 64w + lane] are written straight from
-        // global memory (global_load_lds_dwordx4, lane l at the wave-uniform base + 16 l), no VGPR round trip;
-        // every wave waits for its own copies (explicit s_waitcnt vmcnt(0), below) before the barrier, so after
-        // it every wave may read every entry
-        constexpr uint32_t kPer = (kApronMax + 255u) / 256u;
-        const uint32_t magic = 0xFFFFFFFFu / AW + 1u;
-        const uint32_t w64 = (threadIdx.x >> 6) << 6;
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; k++) {
-            const uint32_t i = threadIdx.x + 256u * k;
-            if (i < n_apron) {
-                uint32_t r = __umulhi(i, magic);   // i / AW for i < 2^16
-                if (r * AW > i) r--;
-                const uint32_t c = i - r * AW;
-                const float4* src = n_t + (((uint32_t)(ay0 - (int)rg.vy0) + r) * rg.vw + (uint32_t)(ax0 - (int)rg.vx0) + c);
-                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                                 (__attribute__((address_space(3))) void*)(l_nt + 256u * k + w64), 16, 0, 0);
-            }
-        }
-    }
+    ntl_stage_window(rg, n_t, l_nt, ax0, ay0, AW, n_apron);
     // neighbour draws while the loads are in flight
     const uint32_t K = f.K;   // <= kLeanK (host check)
     const uint32_t ps = pix_state(key, (uint32_t)y * rg.W + (uint32_t)x);
@@ -1538,6 +1541,179 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     }
 ROMIS_SPATIAL1_NTL_KERNEL(false, k_spatial1_ntl)
 ROMIS_SPATIAL1_NTL_KERNEL(true, k_spatial1_ntl_dbg)
+
+// k_spatial2_ntl: the biased pass for N = 2 sub-reservoirs (the reference's default, common.h:105), laid out like
+// k_spatial1_ntl (32x8 tiles in the XCD chunk order, the n_t window in LDS by LDS-DMA, one shared depth
+// reciprocal).  Each accepted neighbour contributes its N sub-reservoirs in order, then the pixel's own (render_utils
+// .cpp:108-124); every input goes to the output sub-reservoir with the smallest wSum (strict <, first index:
+// Reservoir::update, reservoir.cpp:10-32) and adds its M to that one's routed sum (combineBiased, reservoir.cpp:40-
+// 66).  Same arithmetic, RNG slots (2K + input index) and order as spatial_pixel<N, false>; R <= kLdsSpatialR.
+template <int NT>
+struct CombN {
+    v3 pos[NT], col[NT];
+    float wsum[NT], chosen[NT], pd[NT];
+    uint32_t macc[NT];
+    bool has_pd[NT];
+    uint32_t h;   // ps + slot * 0x9E3779B9 of the next accept draw
+    __device__ __forceinline__ void init(uint32_t h0) {
+#pragma unroll
+        for (int j = 0; j < NT; j++) {
+            pos[j] = mk(0.0f, 0.0f, 0.0f); col[j] = mk(0.0f, 0.0f, 0.0f);
+            wsum[j] = ROMIS_FLT_MIN; chosen[j] = 0.0f; pd[j] = 0.0f; macc[j] = 0u; has_pd[j] = false;
+        }
+        h = h0;
+    }
+    __device__ __forceinline__ void take(float pd_in, float W, uint32_t M, v3 p, v3 c) {
+        const float w = (pd_in * W) * (float)M;          // reservoir.cpp:50
+        uint32_t k = 0;                                    // argmin wSum from FLT_MAX, strict <, first index
+        float best = ROMIS_FLT_MAX;                        // (reservoir.cpp:12-19; a NaN wSum is never taken)
+#pragma unroll
+        for (int j = 0; j < NT; j++)
+            if (wsum[j] < best) { k = (uint32_t)j; best = wsum[j]; }
+        const float u = rand01(mix32(h));
+        h += 0x9E3779B9u;
+#pragma unroll
+        for (int j = 0; j < NT; j++) {
+            if ((uint32_t)j == k) {
+                macc[j] += M;
+                wsum[j] += w;
+                if (u < (w / wsum[j])) { pos[j] = p; col[j] = c; chosen[j] = w; pd[j] = pd_in; has_pd[j] = true; }
+            }
+        }
+    }
+};
+
+template <bool DBG, int NT>
+__device__ __forceinline__ void spatialn_ntl_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
+                                                  v3 origin, const float4* __restrict__ n_t,
+                                                  const float4* __restrict__ p_mat, const float4* __restrict__ ia,
+                                                  const float4* __restrict__ ib, float4* __restrict__ oa,
+                                                  float4* __restrict__ ob, float2* __restrict__ odbg) {
+    const GlTabs tb = gl_stage_tables<false>();   // made visible by the window's barrier below
+    float4* const l_nt = g_lds;
+    uint32_t tile;
+    if (!xcd_tile(rg, num_tiles(rg), blockIdx.x, tile)) return;   // block-uniform
+    const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
+    const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTileH);
+    const int xlo = max(0, (int)rg.vx0), xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1;
+    const int ylo = max(0, (int)rg.vy0), yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1;
+    const int R = (int)f.R;
+    const int ax0 = max(tx0 - R, xlo), ax1 = min(tx0 + (int)kTileW - 1 + R, xhi);
+    const int ay0 = max(ty0 - R, ylo), ay1 = min(ty0 + (int)kTileH - 1 + R, yhi);
+    const uint32_t AW = (uint32_t)(ax1 - ax0 + 1), n_apron = AW * (uint32_t)(ay1 - ay0 + 1);
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    const int x = tx0 + (int)(w * 8u + (l & 7u)), y = ty0 + (int)(l >> 3);
+    const bool live = x < (int)(rg.rx0 + rg.rw) && y < (int)(rg.ry0 + rg.rh);
+    const uint32_t pofs = ((uint32_t)(y - (int)rg.vy0) * rg.vw + (uint32_t)(x - (int)rg.vx0)) << 4;
+    const uint32_t jofs = rg.js << 4;   // bytes between sub-reservoir planes (host check: fits 32 bits)
+    float4 cpm = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ca[NT], cb[NT];
+#pragma unroll
+    for (int j = 0; j < NT; j++) { ca[j] = cpm; cb[j] = cpm; }
+    if (live) {
+        cpm = ld_at(p_mat, pofs);
+#pragma unroll
+        for (int j = 0; j < NT; j++) { ca[j] = ld_at(ia, pofs + (uint32_t)j * jofs); cb[j] = ld_at(ib, pofs + (uint32_t)j * jofs); }
+    }
+    ntl_stage_window(rg, n_t, l_nt, ax0, ay0, AW, n_apron);
+    const uint32_t K = f.K;   // <= kLeanK (host check)
+    const uint32_t ps = pix_state(key, (uint32_t)y * rg.W + (uint32_t)x);
+    const uint32_t span = 2u * f.R + 1u;
+    uint32_t qi[kLeanK], qo[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        qi[n] = 0u;
+        qo[n] = pofs;
+        if (n < K) {
+            const int nx = min(max(x - R + (int)__umulhi(draw(ps, 2u * n), span), xlo), xhi);
+            const int ny = min(max(y - R + (int)__umulhi(draw(ps, 2u * n + 1u), span), ylo), yhi);
+            qi[n] = (uint32_t)(ny - ay0) * AW + (uint32_t)(nx - ax0);
+            qo[n] = ((uint32_t)(ny - (int)rg.vy0) * rg.vw + (uint32_t)(nx - (int)rg.vx0)) << 4;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's window copies, before the barrier
+    __syncthreads();
+    if (!live) return;   // no barrier follows
+    const float4 cn = l_nt[(uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0)];
+    const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
+    // primary-ray miss (see spatial1_pixel): every neighbour is rejected and every own input weighs (0 W) M = +-0,
+    // so both go to sub-reservoir 0 (equal wSums FLT_MIN), nothing is accepted: M_0 = sum of the own Ms, W = 0
+    bool miss = cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z);
+#pragma unroll
+    for (int j = 0; j < NT; j++) miss = miss && __builtin_isfinite(ca[j].w) && __builtin_isfinite(cb[j].x + cb[j].y + cb[j].z);
+    if (miss) {
+        uint32_t m = 0u;
+#pragma unroll
+        for (int j = 0; j < NT; j++) m += __float_as_uint(cb[j].w);
+#pragma unroll
+        for (int j = 0; j < NT; j++) {
+            st_at(oa, pofs + (uint32_t)j * jofs, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+            st_at(ob, pofs + (uint32_t)j * jofs, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(j == 0 ? m : 0u)));
+            if (DBG) st_at(odbg, (pofs + (uint32_t)j * jofs) >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
+        }
+        return;
+    }
+    // depth / normal heuristic (render_utils.cpp:114-118), as in spatial1_ntl_body
+    const double rt = rcp_d(cur.t);
+    const bool rt_all = __all(div_fast_ok(cur.t));
+    bool ok[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        ok[n] = false;
+        if (n < K) {
+            const float4 g = l_nt[qi[n]];
+            const float nd = vdot(xyz(g), cur.N);
+            float q = div_by_rcp_d(g.w, rt);
+            if (__builtin_expect(!rt_all, 0)) {
+                if (!div_fast_ok(cur.t)) q = g.w / cur.t;
+            }
+            ok[n] = !(nd < 0.90630778703f) && !(fabsf(1.0f - q) > 0.1f);
+        }
+    }
+    CombN<NT> cmb;
+    cmb.init(ps + 2u * K * 0x9E3779B9u);
+    float4 na[NT], nb[NT];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        if (ok[n]) {
+#pragma unroll
+            for (int j = 0; j < NT; j++) { na[j] = ld_at(ia, qo[n] + (uint32_t)j * jofs); nb[j] = ld_at(ib, qo[n] + (uint32_t)j * jofs); }
+#pragma unroll
+            for (int j = 0; j < NT; j++) {
+                const v3 p = xyz(na[j]), c = xyz(nb[j]);
+                cmb.take(target_pdf(s, f, cur, p, c, tb), na[j].w, __float_as_uint(nb[j].w), p, c);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+        const v3 p = xyz(ca[j]), c = xyz(cb[j]);
+        cmb.take(target_pdf(s, f, cur, p, c, tb), ca[j].w, __float_as_uint(cb[j].w), p, c);
+    }
+    // finish_biased: M = routed sum, W from the held sample's target pdf (light.cpp:90-93 / reservoir.cpp:61-64);
+    // nothing accepted: the initial (0, 0) sample, whose shaded value is +-0 at a non-NaN position (W = 0)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+        float p = cmb.pd[j];
+        if (!cmb.has_pd[j])
+            p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, cmb.pos[j], cmb.col[j], tb);
+        const float W = contribution_weight(p, cmb.macc[j], cmb.wsum[j]);
+        st_at(oa, pofs + (uint32_t)j * jofs, make_float4(cmb.pos[j].x, cmb.pos[j].y, cmb.pos[j].z, W));
+        st_at(ob, pofs + (uint32_t)j * jofs, make_float4(cmb.col[j].x, cmb.col[j].y, cmb.col[j].z, __uint_as_float(cmb.macc[j])));
+        if (DBG) st_at(odbg, (pofs + (uint32_t)j * jofs) >> 1, make_float2(cmb.wsum[j], cmb.chosen[j]));
+    }
+}
+
+#ifndef ROMIS_SPATIAL2_NTL_WPE
+#define ROMIS_SPATIAL2_NTL_WPE 4
+#endif
+#define ROMIS_SPATIALN_NTL_KERNEL(DBG, NT, NAME)                                                                      \
+    extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL2_NTL_WPE))) void     \
+    NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
+         const float4* p_mat, const float4* ia, const float4* ib, float4* oa, float4* ob, float2* odbg) {             \
+        spatialn_ntl_body<DBG, NT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg);                   \
+    }
+ROMIS_SPATIALN_NTL_KERNEL(false, 2, k_spatial2_ntl)
+ROMIS_SPATIALN_NTL_KERNEL(true, 2, k_spatial2_ntl_dbg)
 
 #define ROMIS_SPATIAL1_KERNEL(DBG, NAME)                                                                              \
     extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL1_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f,     \
@@ -1722,15 +1898,17 @@ __device__ __forceinline__ uint32_t target_bin(const Bvh& b, v3 y) {
            ((qz & 1u) << 2) | ((qx & 1u) << 1) | (qy & 1u);
 }
 
-template <bool LDS_BVH>
+template <bool LDS_BVH, int NT>
 __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, v3 origin,
                                                   const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                                   const float4* __restrict__ ra, const float4* __restrict__ rb,
                                                   float* __restrict__ rgb) {
+    // NT shadow rays per pixel (one per sub-reservoir): ray j * 256 + t is pixel t's sub-reservoir j
+    constexpr uint32_t kRays = 256u * NT;
     __shared__ uint32_t s_hist[256];
     __shared__ uint32_t s_wsum[4];
-    __shared__ float4 s_from[256], s_to[256];
-    __shared__ uint32_t s_vis[256];
+    __shared__ float4 s_from[kRays], s_to[kRays];
+    __shared__ uint32_t s_vis[kRays];
     const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
     const GlTabs tb = gl_stage_tables();
     const float g = 1.0f / f.gamma;
@@ -1739,19 +1917,28 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
     size_t p;
     const bool valid = work_pixel(rg, blockIdx.x, x, y, p);
     Px px;
-    Sub r;
-    v3 sc = mk(0.0f, 0.0f, 0.0f);
-    bool need = false;
+    Sub r[NT];
+    v3 sc[NT];
+    bool need[NT];
+#pragma unroll
+    for (int j = 0; j < NT; j++) { sc[j] = mk(0.0f, 0.0f, 0.0f); need[j] = false; }
     if (valid) {
         px = load_px(s, rg, n_t, p_mat, p, origin);
-        sub_load(r, ra, rb, ridx(rg, 0, p));
-        sc = shade(s, f, px, r.pos, r.col, tb);
-        need = sc.x != 0.0f || sc.y != 0.0f || sc.z != 0.0f;   // see final_body: no ray when sc == 0
+#pragma unroll
+        for (int j = 0; j < NT; j++) {
+            sub_load(r[j], ra, rb, ridx(rg, (uint32_t)j, p));
+            sc[j] = shade(s, f, px, r[j].pos, r[j].col, tb);
+            need[j] = sc[j].x != 0.0f || sc[j].y != 0.0f || sc[j].z != 0.0f;   // see final_body: no ray when sc == 0
+        }
     }
     s_hist[t] = 0u;
     __syncthreads();
-    const uint32_t bin = need ? target_bin(bvh, r.pos) : 0u;
-    const uint32_t rank = need ? atomicAdd(&s_hist[bin], 1u) : 0u;
+    uint32_t bin[NT], rank[NT];
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+        bin[j] = need[j] ? target_bin(bvh, r[j].pos) : 0u;
+        rank[j] = need[j] ? atomicAdd(&s_hist[bin[j]], 1u) : 0u;
+    }
     __syncthreads();
     // exclusive scan of the 256 bin counts: wave scan + wave totals
     const uint32_t cnt = s_hist[t];
@@ -1769,21 +1956,34 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
     __syncthreads();
     s_hist[t] = excl;
     __syncthreads();
-    if (need) {
-        const uint32_t slot = s_hist[bin] + rank;
-        s_from[slot] = make_float4(px.P.x, px.P.y, px.P.z, __uint_as_float(t));
-        s_to[slot] = make_float4(r.pos.x, r.pos.y, r.pos.z, 0.0f);
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+        if (need[j]) {
+            const uint32_t slot = s_hist[bin[j]] + rank[j];
+            s_from[slot] = make_float4(px.P.x, px.P.y, px.P.z, __uint_as_float((uint32_t)j * 256u + t));
+            s_to[slot] = make_float4(r[j].pos.x, r[j].pos.y, r[j].pos.z, 0.0f);
+        }
     }
     __syncthreads();
-    if (t < total) {
-        const float4 a = s_from[t], b = s_to[t];
-        s_vis[__float_as_uint(a.w)] = visible(bvh, xyz(a), xyz(b)) ? 1u : 0u;
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+        const uint32_t i = (uint32_t)j * 256u + t;
+        if (i < total) {
+            const float4 a = s_from[i], b = s_to[i];
+            s_vis[__float_as_uint(a.w)] = visible(bvh, xyz(a), xyz(b)) ? 1u : 0u;
+        }
     }
     __syncthreads();
     if (!valid) return;
-    if (need && !s_vis[t]) sc = mk(0.0f, 0.0f, 0.0f);
-    v3 color = vadd(mk(0.0f, 0.0f, 0.0f), vscale(sc, r.W));   // final_body's accumulation from 0 (-0 -> +0)
-    color = vdivs(color, 1.0f);
+    // finalShading's sum in sub-reservoir order from 0 (final_body: -0 -> +0), then / N
+    v3 color = mk(0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+        v3 c = sc[j];
+        if (need[j] && !s_vis[(uint32_t)j * 256u + t]) c = mk(0.0f, 0.0f, 0.0f);
+        color = vadd(color, vscale(c, r[j].W));
+    }
+    color = vdivs(color, (float)NT);
     if (f.tone_map) {
         v3 e = vscale(mk(-color.x, -color.y, -color.z), f.exposure);
         v3 mapped = mk(1.0f - gl_expf(tb, e.x), 1.0f - gl_expf(tb, e.y), 1.0f - gl_expf(tb, e.z));
@@ -1797,7 +1997,12 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
 extern "C" __global__ __launch_bounds__(256) void k_final_n1_sorted(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,
                                                                    float oz, const float4* n_t, const float4* p_mat,
                                                                    const float4* ra, const float4* rb, float* rgb) {
-    final_sorted_body<true>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb);
+    final_sorted_body<true, 1>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb);
+}
+extern "C" __global__ __launch_bounds__(256) void k_final_n2_sorted(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,
+                                                                   float oz, const float4* n_t, const float4* p_mat,
+                                                                   const float4* ra, const float4* rb, float* rgb) {
+    final_sorted_body<true, 2>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb);
 }
 
 #define ROMIS_FINAL_KERNEL(NT, LDS, NAME)                                                                              \
@@ -2639,6 +2844,9 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
     const size_t bvh_bytes = bvh_lds_bytes(s);
     const bool lean = tu.spatial_lean && f.N == 1 && f.K <= kLeanK && rg.ps == 1u && rg.map2d == 2u &&
                       (size_t)rg.vw * rg.vh * 16u <= 0xFFFFFFFFull;
+    // N = 2 planes: byte offsets of both sub-reservoir planes within 32 bits
+    const bool lean2 = tu.spatial_lean && f.N == 2 && f.K <= kLeanK && rg.ps == 1u && rg.map2d == 2u &&
+                       (size_t)rg.js * 16u + (size_t)rg.vw * rg.vh * 16u <= 0xFFFFFFFFull;
     if (lean && f.unbiased && (!f.spatial_vis || bvh_bytes <= kLdsBudget)) {
         // combineUnbiased, N = 1: one block per tile in the XCD order of the biased pass (xcd_tile)
         const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
@@ -2649,6 +2857,16 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         ROMIS_LAUNCH(k, dim3(grid), dim3(kBlock), f.spatial_vis ? bvh_bytes : 0, stream, s, rg, f, key, o[0], o[1], o[2],
                      n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
         if (rp_written) *rp_written = rp_out != nullptr;
+        return hipGetLastError();
+    }
+    if (lean2 && !f.unbiased && f.R <= kLdsSpatialR) {
+        // N = 2 biased: one block per tile in the XCD chunk order (xcd_tile)
+        const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
+        rg.xcd_rows = tu.spatial_xcd_rows == kXcdRowsAuto ? std::max(1u, std::min(8u, 8192u / std::max(rg.rw, 1u)))
+                                                          : tu.spatial_xcd_rows;
+        if (rg.xcd_rows) grid = 8u * ((((nty + rg.xcd_rows - 1) / rg.xcd_rows) + 7u) / 8u) * rg.xcd_rows * ntx;
+        ROMIS_LAUNCH(odbg ? k_spatial2_ntl_dbg : k_spatial2_ntl, dim3(grid), dim3(kBlock), kApronMax * 16u, stream, s, rg, f,
+                     key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg);
         return hipGetLastError();
     }
     if (lean && !f.unbiased) {
@@ -2716,9 +2934,9 @@ hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev&
     const bool use_lds = tu.final_lds && lds <= kLdsBudget;
     auto k = use_lds ? (f.N == 1 ? k_final_n1_lds : (f.N == 2 ? k_final_n2_lds : k_final_n0_lds))
                      : (f.N == 1 ? k_final_n1 : (f.N == 2 ? k_final_n2 : k_final_n0));
-    if (tu.final_sort && use_lds && f.N == 1 && rg.map2d) {   // one tile per block
-        ROMIS_LAUNCH(k_final_n1_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, s, rg, f, o[0], o[1], o[2],
-                           n_t, p_mat, ra, rb, rgb);
+    if (tu.final_sort && use_lds && (f.N == 1 || f.N == 2) && rg.map2d) {   // one tile per block
+        ROMIS_LAUNCH(f.N == 1 ? k_final_n1_sorted : k_final_n2_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, s,
+                     rg, f, o[0], o[1], o[2], n_t, p_mat, ra, rb, rgb);
         return hipGetLastError();
     }
     ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.final_blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,

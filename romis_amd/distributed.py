@@ -44,14 +44,33 @@ class HaloFrames:
         if self.transport not in ("torch", "native"):
             raise ValueError(f"HaloFrames: unknown transport {self.transport!r}")
         if self.transport == "native":
-            # one rank draws the communicator id, every rank receives it over the torch group
-            idt = torch.zeros(restir._abi.RESTIR_RCCL_ID_BYTES, dtype=torch.uint8)
+            # one rank draws the communicator id, every rank receives it over the torch group; its last byte says
+            # whether rank 0 could draw one, so that every rank fails together (never some ranks waiting inside a
+            # collective the others left)
+            n_id = restir._abi.RESTIR_RCCL_ID_BYTES
+            idt = torch.zeros(n_id + 1, dtype=torch.uint8)
             if dist.get_rank(group) == 0:
-                idt[:] = torch.frombuffer(bytearray(restir.rccl_unique_id()), dtype=torch.uint8)
-            if self.on_device:
-                idt = idt.to(torch.device("cuda", torch.cuda.current_device()))
+                try:
+                    idt[:n_id] = torch.frombuffer(bytearray(restir.rccl_unique_id()), dtype=torch.uint8)
+                    idt[n_id] = 1
+                except restir._abi.RestirError:
+                    pass
+            dev = torch.device("cuda", torch.cuda.current_device()) if self.on_device else torch.device("cpu")
+            idt = idt.to(dev)
             dist.broadcast(idt, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-            self.r.halo_attach_rccl(bytes(idt.cpu().numpy().tobytes()), dist.get_world_size(group), dist.get_rank(group))
+            host = idt.cpu()
+            if int(host[n_id]) != 1:
+                raise restir._abi.RestirError("HaloFrames: RCCL unavailable on rank 0 (native transport)")
+            err = None
+            try:   # ncclCommInitRank: every rank joins the same communicator
+                self.r.halo_attach_rccl(bytes(host[:n_id].numpy().tobytes()), dist.get_world_size(group),
+                                        dist.get_rank(group))
+            except restir._abi.RestirError as e:
+                err = e
+            ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+            if int(ok.item()) != 1:
+                raise err or restir._abi.RestirError("HaloFrames: the RCCL communicator failed on another rank")
             return
         dev = torch.device("cuda", torch.cuda.current_device()) if self.on_device else torch.device("cpu")
         sb = sum(s.bytes for s in self.send)

@@ -31,6 +31,12 @@ VARIANTS = {
     # the neighbour offset draws (2 mix32 + umulhi + clamp each) -> a multiply-add of the pixel state
     "no_rng": [(r"__umulhi\(draw\(ps, 2u \* n\), span\)", "((ps + 2u * n) % span)"),
                (r"__umulhi\(draw\(ps, 2u \* n \+ 1u\), span\)", "((ps >> 8) + n) % span")],
+    # the accepted neighbours' reservoir gathers read the pixel's own records instead (same instructions, coalesced
+    # addresses): what the scattered addresses cost in the memory pipeline
+    "coalesced": [(r"ld_at\(ia, qo\[(n \+ 1|0)\]\)", "ld_at(ia, pofs)"), (r"ld_at\(ib, qo\[(n \+ 1|0)\]\)", "ld_at(ib, pofs)")],
+    # no neighbour reservoir loads at all (the pixel's own records stand in): gather latency and traffic removed
+    "no_gather": [(r"na\[(n \+ 1|0)\] = ld_at\(ia, qo\[(n \+ 1|0)\]\);", r"na[\1] = ca;"),
+                  (r"nb\[(n \+ 1|0)\] = ld_at\(ib, qo\[(n \+ 1|0)\]\);", r"nb[\1] = cb;")],
     # the whole combine (takes) -> sums
     "no_take": [(r"cmb\.take\(target_pdf\(s, f, cur, p, c, tb\), na\[n\]\.w, __float_as_uint\(nb\[n\]\.w\), p, c\);",
                  "cmb.wsum += target_pdf(s, f, cur, p, c, tb) * na[n].w; cmb.macc += __float_as_uint(nb[n].w);")],
@@ -40,7 +46,10 @@ VARIANTS = {
 def main():
     src = open(SRC).read()
     a, b = body_span(src)
+    only = set(sys.argv[1:])
     for name, subs in VARIANTS.items():
+        if only and name not in only:
+            continue
         body = src[a:b]
         for pat, rep in subs:
             body, n = re.subn(pat, rep, body)

@@ -277,12 +277,13 @@ def test_final_shading(gpu, oracle, N, tonemap):
 
 @pytest.mark.parametrize("name", ["nightclub_128pt", "cornell_1024"])
 @pytest.mark.parametrize("binned", [1, 0])
-def test_final_shading_binned_rays(gpu, oracle, name, binned):
-    """final.sort (N = 1, the default): rays traced in target-bin order by other lanes -- the image must not
+@pytest.mark.parametrize("N", [1, 2])
+def test_final_shading_binned_rays(gpu, oracle, name, binned, N):
+    """final.sort (N = 1 and 2, the default): rays traced in target-bin order by other lanes -- the image must not
     change; final.sort 0: the unbinned kernel."""
-    _, osc, cam = setup(gpu, oracle, name, 1)
+    _, osc, cam = setup(gpu, oracle, name, N)
     n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
-    f = _abi.default_features(num_samples_in_reservoir=1)
+    f = _abi.default_features(num_samples_in_reservoir=N)
     a, b, _ = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
     for which, arr in [(_abi.BUF_GBUF_N_T, n_t), (_abi.BUF_GBUF_P_MAT, p_mat), (_abi.BUF_RES_A, a), (_abi.BUF_RES_B, b)]:
         gpu.upload(which, arr)

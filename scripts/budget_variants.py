@@ -18,9 +18,15 @@ from romis_amd import build  # noqa: E402
 SRC = os.path.join(build.CSRC, "kernels.hip")
 
 
-def body_span(src):
-    a = src.index("__device__ __forceinline__ void spatial1_ntl_body(")
-    b = src.index("#ifndef ROMIS_SPATIAL1_NTL_WPE")
+SPANS = {   # the function each variant patches: (first line, the text that follows the function)
+    "spatial": ("__device__ __forceinline__ void spatial1_ntl_body(", "#ifndef ROMIS_SPATIAL1_NTL_WPE"),
+    "ris": ("__device__ __forceinline__ void ris_pixel(", "// k_ris: genCanonicalSamples per pixel."),
+}
+
+
+def body_span(src, which):
+    a = src.index(SPANS[which][0])
+    b = src.index(SPANS[which][1], a)
     return a, b
 
 
@@ -37,6 +43,12 @@ VARIANTS = {
     # no neighbour reservoir loads at all (the pixel's own records stand in): gather latency and traffic removed
     "no_gather": [(r"na\[(n \+ 1|0)\] = ld_at\(ia, qo\[(n \+ 1|0)\]\);", r"na[\1] = ca;"),
                   (r"nb\[(n \+ 1|0)\] = ld_at\(ib, qo\[(n \+ 1|0)\]\);", r"nb[\1] = cb;")],
+    # RIS (ris_pixel): the candidates' target pdfs, light-index draws + accept draws, reservoir updates
+    "ris_no_phat": [(r"target_pdf\(s, f, px, pos, col, tb\);", "fabsf(pos.x + col.y);")],
+    "ris_no_rng": [(r"uniform_index\(draw\(ps, 4u \* c\), L\)", "min(c, L - 1u)"),
+                   (r"rand01\(draw\(ps, 4u \* c \+ 3u\)\)", "0.5f")],
+    "ris_no_update": [(r"res_update<NT>\(r, N, pos, col, weight\(pd\), rand01\(draw\(ps, 4u \* c \+ 3u\)\), pd\);",
+                       "r[0].wsum += weight(pd); r[0].pos = vadd(r[0].pos, pos);")],
     # the whole combine (takes) -> sums
     "no_take": [(r"cmb\.take\(target_pdf\(s, f, cur, p, c, tb\), na\[n\]\.w, __float_as_uint\(nb\[n\]\.w\), p, c\);",
                  "cmb.wsum += target_pdf(s, f, cur, p, c, tb) * na[n].w; cmb.macc += __float_as_uint(nb[n].w);")],
@@ -45,11 +57,11 @@ VARIANTS = {
 
 def main():
     src = open(SRC).read()
-    a, b = body_span(src)
     only = set(sys.argv[1:])
     for name, subs in VARIANTS.items():
         if only and name not in only:
             continue
+        a, b = body_span(src, "ris" if name.startswith("ris_") else "spatial")
         body = src[a:b]
         for pat, rep in subs:
             body, n = re.subn(pat, rep, body)

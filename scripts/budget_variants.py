@@ -43,6 +43,15 @@ VARIANTS = {
     # no neighbour reservoir loads at all (the pixel's own records stand in): gather latency and traffic removed
     "no_gather": [(r"na\[(n \+ 1|0)\] = ld_at\(ia, qo\[(n \+ 1|0)\]\);", r"na[\1] = ca;"),
                   (r"nb\[(n \+ 1|0)\] = ld_at\(ib, qo\[(n \+ 1|0)\]\);", r"nb[\1] = cb;")],
+    # everything after the window barrier replaced by a copy of the pixel's own records (the skeleton: own loads,
+    # window DMA, barrier, stores), and the same without the window DMA
+    "skeleton": [(r"    const float4 cn = l_nt\[\(uint32_t\)\(y - ay0\) \* AW \+ \(uint32_t\)\(x - ax0\)\];",
+                  "    st_at(oa, pofs, ca); st_at(ob, pofs, make_float4(cb.x, cb.y, cb.z, __uint_as_float(qi[0] + qo[1]))); return;\n"
+                  "    const float4 cn = l_nt[(uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0)];")],
+    "skeleton_nodma": [(r"    const float4 cn = l_nt\[\(uint32_t\)\(y - ay0\) \* AW \+ \(uint32_t\)\(x - ax0\)\];",
+                        "    st_at(oa, pofs, ca); st_at(ob, pofs, make_float4(cb.x, cb.y, cb.z, __uint_as_float(qi[0] + qo[1]))); return;\n"
+                        "    const float4 cn = l_nt[(uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0)];"),
+                       (r"    ntl_stage_window\(rg, n_t, l_nt, ax0, ay0, AW, n_apron\);", "")],
     # RIS (ris_pixel): the candidates' target pdfs, light-index draws + accept draws, reservoir updates
     "ris_no_phat": [(r"target_pdf\(s, f, px, pos, col, tb\);", "fabsf(pos.x + col.y);")],
     "ris_no_rng": [(r"uniform_index\(draw\(ps, 4u \* c\), L\)", "min(c, L - 1u)"),

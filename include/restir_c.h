@@ -159,7 +159,9 @@ typedef struct restir_features {
     /* R-MIS / R-OMIS parameters and the neighbour-selection heuristic (common.h:110-121) -- ABI v2 */
     uint8_t  neighbour_same_geometry;                   /* true */
     uint8_t  use_progressive_romis;                     /* false */
-    uint8_t  save_alphas_visualisation;                 /* accepted; the per-distribution BMPs are not written */
+    uint8_t  save_alphas_visualisation;                 /* true; R-OMIS writes the per-distribution bitmaps
+                                                           when the context has a renders dir
+                                                           (restir_set_renders_dir) */
     uint8_t  reserved0;
     float    neighbour_max_depth_difference_fraction;   /* 0.10 */
     float    neighbour_max_normal_angle_difference_radians; /* 0.436332, compared with the normals' dot product
@@ -222,6 +224,15 @@ restir_status restir_device_count(int* out);
 restir_status restir_create(int device, restir_ctx** out);
 void          restir_destroy(restir_ctx* ctx);
 restir_status restir_set_seed(restir_ctx* ctx, uint32_t seed, uint32_t frame_index);
+/* The reference's RENDERS_DIR (a build-time constant there) for this context's file side outputs; NULL or "" =
+ * none (the default).  With a dir, an R-OMIS render with features->save_alphas_visualisation writes
+ * visualiseAlphas' bitmaps after every iteration (render.cpp:227-229, render_utils.cpp:189-243):
+ * <dir>/<"%d-%m-%Y %H-%M-%S" local time>/Distribution <i> - <Red|Green|Blue>.bmp for technique i of the k + 1,
+ * each pixel mix(black, (1, .5, 0), alpha) for alpha > 0 and mix(black, (0, .5, 1), -alpha) otherwise, the
+ * alphas solved from the technique matrix and contribution vectors so far -- byte for byte the reference's images
+ * (iterations within one second share the folder and overwrite, as there).  The dirs are created as needed;
+ * a file that cannot be written fails the render (RESTIR_ERR_INVALID). */
+restir_status restir_set_renders_dir(restir_ctx* ctx, const char* dir);
 
 /* Uploads the scene: materials, light SoA table, and the flattened BVH built on the host (replaces
  * EmbreeInterface(scene), embree_interface.cpp:14-51). */

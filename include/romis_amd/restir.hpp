@@ -202,6 +202,10 @@ public:
               "restir_set_scene");
     }
     void setSeed(uint32_t seed, uint32_t frameIndex = 0) { check(restir_set_seed(ctx_, seed, frameIndex), "restir_set_seed"); }
+    // RENDERS_DIR for the file side outputs the library writes itself (R-OMIS alpha visualisation); empty = none
+    void setRendersDir(const std::filesystem::path& dir) {
+        check(restir_set_renders_dir(ctx_, dir.empty() ? nullptr : dir.c_str()), "restir_set_renders_dir");
+    }
     restir_ctx* handle() const { return ctx_; }
 
 private:
@@ -260,13 +264,15 @@ inline void renderMIS(Renderer& r, const Camera& camera, Screen& screen, const F
 
 // renderRayTraced (render.cpp:268-290): the grid for temporal reuse in ReSTIR mode, nullptr (std::nullopt) for
 // R-MIS / R-OMIS.  Like the reference, every render then saves its configuration record to
-// <rendersDir>/<currentTime()>.json (render.cpp:281-287, saveFeaturesRecord); the reference's RENDERS_DIR is a
-// build-time constant, here the caller passes it -- an empty path skips the record.
+// <rendersDir>/<currentTime()>.json (render.cpp:281-287, saveFeaturesRecord), and R-OMIS with
+// saveAlphasVisualisation writes its alpha bitmaps to <rendersDir>/<currentTime()>/ after every iteration; the
+// reference's RENDERS_DIR is a build-time constant, here the caller passes it -- an empty path skips both.
 inline std::shared_ptr<ReservoirGrid> renderRayTraced(Renderer& r, const std::shared_ptr<ReservoirGrid>& prev,
                                                       const Camera& camera, Screen& screen, const Features& features,
                                                       const std::filesystem::path& rendersDir = {},
                                                       const restir_features_record_extra* extra = nullptr) {
     std::shared_ptr<ReservoirGrid> next;
+    r.setRendersDir(rendersDir);   // R-OMIS's per-iteration alpha visualisation (render.cpp:227-229)
     switch (features.ray_trace_mode) {
         case RESTIR_MODE_RESTIR: next = renderReSTIR(r, prev, camera, screen, features); break;
         case RESTIR_MODE_RMIS:

@@ -142,6 +142,7 @@ SIGNATURES = {
     "restir_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "restir_destroy": (None, [_P]),
     "restir_set_seed": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
+    "restir_set_renders_dir": (C.c_int, [_P, C.c_char_p]),
     "restir_set_scene": (C.c_int, [_P, C.POINTER(Mesh), C.c_uint32, C.POINTER(Light), C.c_uint32]),
     "restir_set_scene_textured": (C.c_int, [_P, C.POINTER(Mesh), C.c_uint32, C.POINTER(Light), C.c_uint32,
                                             C.POINTER(Texture), C.c_uint32]),

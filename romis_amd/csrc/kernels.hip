@@ -2631,6 +2631,42 @@ __device__ __forceinline__ void romis_alphas_body(uint32_t W, uint32_t H, float*
     }
 }
 
+// saveAlphasVisualisation (render.cpp:227-229, visualiseAlphas render_utils.cpp:189-243): after an iteration, each
+// colour's alpha vector solved from the sums so far (the sums themselves untouched; progressive alphas live in their
+// own rows).  Technique i, colour ch -> image 3 i + ch; a pixel is glm::mix(0, (1, .5, 0), a) for a > 0 and
+// glm::mix(0, (0, .5, 1), -a) otherwise (x (1 - a) + y a, unfused), stored as Screen::writeBitmapToFile's 8-bit word
+// (clamp to [0, 1], x255, truncate; bytes B, G, R, A = 255).  A bitmap's rows run bottom-up, and Screen::setPixel
+// flips y, so image pixel order = this grid's order (y = 0 bottom): out[(3 i + ch) npx + p].
+__device__ __forceinline__ uint32_t vis_u8(float v) {
+    const float m = (v < 0.0f) ? 0.0f : v;   // glm::clamp: a NaN passes through ...
+    const float c = (1.0f < m) ? 1.0f : m;
+    if (c != c) return 0u;                   // ... and truncates to 0 (screen.cpp's to_u8)
+    return (uint32_t)(int)__fmul_rn(c, 255.0f);
+}
+__device__ __forceinline__ float vis_mix(float y, float a) {
+    return __fadd_rn(__fmul_rn(0.0f, __fsub_rn(1.0f, a)), __fmul_rn(y, a));
+}
+template <int T>
+__device__ __forceinline__ void romis_vis_body(uint32_t W, uint32_t H, const float* __restrict__ acc,
+                                               uint32_t* __restrict__ out) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= W * H) return;
+    const size_t npx = (size_t)W * H;
+    float A[T * T], bv[T], xv[T];
+    for (int e = 0; e < T * T; e++) A[e] = acc[(size_t)e * npx + p];
+    for (int ch = 0; ch < 3; ch++) {
+        for (int i = 0; i < T; i++) bv[i] = acc[(size_t)(T * T + ch * T + i) * npx + p];
+        cod_solve_dev<T>(A, bv, xv);
+        for (int i = 0; i < T; i++) {
+            const float a = xv[i];
+            const bool pos = a > 0.0f;
+            const float m = pos ? a : -a;
+            const float r = vis_mix(pos ? 1.0f : 0.0f, m), g = vis_mix(0.5f, m), b = vis_mix(pos ? 0.0f : 1.0f, m);
+            out[(size_t)(3 * i + ch) * npx + p] = vis_u8(b) | (vis_u8(g) << 8) | (vis_u8(r) << 16) | 0xFF000000u;
+        }
+    }
+}
+
 #define ROMIS_ROMIS_SAMPLES(T, LDS, NAME)                                                                           \
     extern "C" __global__ __launch_bounds__(256) void NAME(SceneDev s, uint32_t W, uint32_t H, FeaturesDev f, float ox,  \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,  \
@@ -2650,6 +2686,10 @@ __device__ __forceinline__ void romis_alphas_body(uint32_t W, uint32_t H, float*
     ROMIS_ROMIS_ACCUM(T, true, k_romis_accum_prog_t##T)                                                               \
     extern "C" __global__ __launch_bounds__(256) void k_romis_alphas_t##T(uint32_t W, uint32_t H, float* acc) {         \
         romis_alphas_body<T>(W, H, acc);                                                                              \
+    }                                                                                                                 \
+    extern "C" __global__ __launch_bounds__(256) void k_romis_vis_t##T(uint32_t W, uint32_t H, const float* acc,        \
+                                                                      uint32_t* out) {                                \
+        romis_vis_body<T>(W, H, acc, out);                                                                            \
     }                                                                                                                 \
     extern "C" __global__ __launch_bounds__(256) void k_romis_solve_t##T(uint32_t W, uint32_t H, FeaturesDev f,         \
                                                                         const float* acc, float* rgb) {               \
@@ -2978,6 +3018,7 @@ typedef void (*RomisSamplesFn)(SceneDev, uint32_t, uint32_t, FeaturesDev, float,
 typedef void (*RomisAccumFn)(uint32_t, uint32_t, FeaturesDev, uint32_t, uint32_t, const float*, float*);
 typedef void (*RomisAlphasFn)(uint32_t, uint32_t, float*);
 typedef void (*RomisSolveFn)(uint32_t, uint32_t, FeaturesDev, const float*, float*);
+typedef void (*RomisVisFn)(uint32_t, uint32_t, const float*, uint32_t*);
 typedef void (*DebugCodFn)(const float*, const float*, float*, uint32_t);
 #define ROMIS_T_TABLE(PFX) {PFX##1, PFX##2, PFX##3, PFX##4, PFX##5, PFX##6, PFX##7, PFX##8}
 const RomisSamplesFn kRomisSamples[8] = ROMIS_T_TABLE(k_romis_samples_t);
@@ -2986,6 +3027,7 @@ const RomisAccumFn kRomisAccum[8] = ROMIS_T_TABLE(k_romis_accum_t);
 const RomisAccumFn kRomisAccumProg[8] = ROMIS_T_TABLE(k_romis_accum_prog_t);
 const RomisAlphasFn kRomisAlphas[8] = ROMIS_T_TABLE(k_romis_alphas_t);
 const RomisSolveFn kRomisSolve[8] = ROMIS_T_TABLE(k_romis_solve_t);
+const RomisVisFn kRomisVis[8] = ROMIS_T_TABLE(k_romis_vis_t);
 const DebugCodFn kDebugCod[8] = ROMIS_T_TABLE(k_debug_cod_t);
 inline dim3 px_grid(size_t npx) { return dim3((uint32_t)((npx + kBlock - 1) / kBlock)); }
 }  // namespace
@@ -3037,6 +3079,12 @@ hipError_t launch_mis_finish(uint32_t W, uint32_t H, const FeaturesDev& f, const
         const float* col = f.mode == RESTIR_MODE_ROMIS ? acc + (size_t)(T * T + 6u * T) * W * H : acc;
         ROMIS_LAUNCH(k_mis_combine, grid, dim3(kBlock), 0, stream, W, H, f, col, rgb);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_romis_vis(uint32_t W, uint32_t H, uint32_t T, const float* acc, uint32_t* out, hipStream_t stream) {
+    if (T < 1u || T > 8u) return hipErrorInvalidValue;
+    ROMIS_LAUNCH(kRomisVis[T - 1], px_grid((size_t)W * H), dim3(kBlock), 0, stream, W, H, acc, out);
     return hipGetLastError();
 }
 

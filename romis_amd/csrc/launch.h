@@ -47,6 +47,8 @@ hipError_t launch_mis_accumulate(const SceneDev& s, uint32_t W, uint32_t H, cons
                                  const float4* rb, const float2* rdbg, uint32_t iteration, float* acc, float* smp,
                                  uint32_t smp_samples, const Tuning& tu, hipStream_t stream);
 hipError_t launch_mis_finish(uint32_t W, uint32_t H, const FeaturesDev& f, const float* acc, float* rgb, hipStream_t stream);
+// R-OMIS alpha visualisation words: [3T images][W*H] (k_romis_vis_t{T})
+hipError_t launch_romis_vis(uint32_t W, uint32_t H, uint32_t T, const float* acc, uint32_t* out, hipStream_t stream);
 hipError_t launch_debug_cod(uint32_t n, const float* A, const float* b, float* x, uint32_t count, hipStream_t stream);
 hipError_t launch_debug_math(const float* x, const float* y, float* pw, float* ex, uint32_t n, hipStream_t stream);
 

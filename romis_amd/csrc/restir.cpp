@@ -16,11 +16,13 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <ctime>
 #include <dlfcn.h>
+#include <filesystem>
 #include <memory>
 #include <mutex>
-#include <vector>
 #include <string>
+#include <system_error>
 #include <vector>
 
 #include "bvh.h"
@@ -28,6 +30,9 @@
 #include "launch.h"
 #include "restir_types.h"
 
+namespace romis {
+bool write_bmp_words(const char* path, uint32_t width, uint32_t height, const uint32_t* words);   // screen.cpp
+}
 using namespace romis;
 
 // ---------------------------------------------------------------------------------------------------------
@@ -259,6 +264,10 @@ struct restir_ctx {
     // R-MIS / R-OMIS: neighbourhoods [1 + cap][pixels] and accumulators [rows][pixels] (RESTIR_BUF_MIS_*)
     DevBuf mis_nbr, mis_acc, mis_smp;
     uint32_t mis_cap = 0, mis_rows = 0, mis_smp_samples = 0;
+    // file side outputs (restir_set_renders_dir): R-OMIS alpha visualisation words [3T][pixels]
+    std::string renders_dir;
+    DevBuf mis_vis;
+    std::vector<uint32_t> mis_vis_host;
 
     // timing
     bool timing = false;
@@ -740,6 +749,13 @@ restir_status restir_set_seed(restir_ctx* c, uint32_t seed, uint32_t frame_index
     return RESTIR_OK;
 }
 
+restir_status restir_set_renders_dir(restir_ctx* c, const char* dir) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->renders_dir = dir ? dir : "";
+    return RESTIR_OK;
+}
+
 restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_t num_meshes, const restir_light* lights,
                                uint32_t num_lights) {
     return restir_set_scene_textured(c, meshes, num_meshes, lights, num_lights, nullptr, 0);
@@ -945,6 +961,35 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     return RESTIR_OK;
 }
 
+// visualiseAlphas (render_utils.cpp:189-243) of the accumulators so far: k_romis_vis_t{T} solves and colours the
+// 3T images on the device, the host writes them to <renders dir>/<currentTime()>/ (utils.cpp:16-22's format).
+static restir_status save_alphas_visualisation(restir_ctx* c, uint32_t W, uint32_t H, uint32_t T) {
+    const size_t npx = (size_t)W * H, words = (size_t)3 * T * npx;
+    ST_TRY(c->mis_vis.ensure(words * 4));
+    HIP_TRY(launch_romis_vis(W, H, T, c->mis_acc.as<float>(), c->mis_vis.as<uint32_t>(), c->stream));
+    c->mis_vis_host.resize(words);
+    HIP_TRY(hipMemcpyAsync(c->mis_vis_host.data(), c->mis_vis.p, words * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const std::time_t now = std::time(nullptr);
+    std::tm tm_local{};
+    localtime_r(&now, &tm_local);
+    char stamp[64];
+    std::strftime(stamp, sizeof(stamp), "%d-%m-%Y %H-%M-%S", &tm_local);
+    const std::filesystem::path dir = std::filesystem::path(c->renders_dir) / stamp;
+    std::error_code ec;
+    std::filesystem::create_directories(dir, ec);
+    if (ec) return fail(RESTIR_ERR_INVALID, "alpha visualisation: cannot create %s: %s", dir.c_str(), ec.message().c_str());
+    static const char* const kColour[3] = {"Red", "Green", "Blue"};   // enum Color (render_utils.cpp:238)
+    for (uint32_t i = 0; i < T; i++)
+        for (uint32_t ch = 0; ch < 3; ch++) {
+            const std::filesystem::path file =
+                dir / ("Distribution " + std::to_string(i) + " - " + kColour[ch] + ".bmp");
+            if (!write_bmp_words(file.c_str(), W, H, c->mis_vis_host.data() + (size_t)(3 * i + ch) * npx))
+                return fail(RESTIR_ERR_INVALID, "alpha visualisation: cannot write %s", file.c_str());
+        }
+    return RESTIR_OK;
+}
+
 // renderRMIS / renderROMIS (render.cpp:64-265) over the whole image; the caller holds c->mu.
 static restir_status render_mis(restir_ctx* c, const restir_camera* cam, const restir_features* features, uint32_t W,
                                 uint32_t H, float* out_rgb) {
@@ -976,6 +1021,8 @@ static restir_status render_mis(restir_ctx* c, const restir_camera* cam, const r
                                                      c->ra[0].as<float4>(), c->rb[0].as<float4>(), c->dbg[0].as<float2>(), it,
                                                      c->mis_acc.as<float>(), c->mis_smp.as<float>(), c->mis_smp_samples,
                                                      c->tuning, c->stream));
+        if (f.mode == RESTIR_MODE_ROMIS && features->save_alphas_visualisation && !c->renders_dir.empty())
+            ST_TRY(save_alphas_visualisation(c, W, H, f.K + 1u));   // render.cpp:227-229
     }
     TIMED(c, RESTIR_K_MIS, launch_mis_finish(W, H, f, c->mis_acc.as<float>(), c->rgb.as<float>(), c->stream));
     if (out_rgb) {

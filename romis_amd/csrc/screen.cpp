@@ -159,7 +159,36 @@ bool json_double(double d, std::string& out) {
     return true;
 }
 
+// stbi_write_bmp's header with 4 components: BITMAPFILEHEADER + BITMAPV4HEADER (BI_BITFIELDS, 32 bpp, alpha mask)
+void bmp_header(std::vector<uint8_t>& o, uint32_t width, uint32_t height) {
+    const size_t bytes = 14 + 108 + (size_t)width * height * 4;
+    o.push_back('B'); o.push_back('M');
+    put32(o, (uint32_t)bytes); put16(o, 0); put16(o, 0); put32(o, 14 + 108);
+    put32(o, 108); put32(o, width); put32(o, height); put16(o, 1); put16(o, 32);
+    put32(o, 3); put32(o, 0); put32(o, 0); put32(o, 0); put32(o, 0); put32(o, 0);
+    put32(o, 0xff0000u); put32(o, 0xff00u); put32(o, 0xffu); put32(o, 0xff000000u);
+    put32(o, 0);
+    for (int i = 0; i < 12; i++) put32(o, 0);   // CIEXYZ endpoints (9) + gamma (3)
+}
+
 }  // namespace
+
+namespace romis {
+// A bitmap whose pixels are already stb's 32-bit words (bytes B, G, R, A) in file order, rows bottom-up
+// (the R-OMIS alpha visualisation, k_romis_vis_t{T}).
+bool write_bmp_words(const char* path, uint32_t width, uint32_t height, const uint32_t* words) {
+    const size_t px = (size_t)width * height;
+    if (!path || (!words && px) || 14 + 108 + px * 4 > 0xFFFFFFFFull) return false;
+    std::vector<uint8_t> o;
+    o.reserve(14 + 108);
+    bmp_header(o, width, height);
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return false;
+    bool ok = std::fwrite(o.data(), 1, o.size(), f) == o.size();
+    if (px) ok = std::fwrite(words, 4, px, f) == px && ok;   // little-endian words = the B, G, R, A bytes
+    return std::fclose(f) == 0 && ok;
+}
+}  // namespace romis
 
 extern "C" {
 
@@ -185,13 +214,7 @@ restir_status restir_encode_bmp(const float* rgb, uint32_t width, uint32_t heigh
     // pixels B, G, R, A (stb_image_write.h stbi_write_bmp_core / stbiw__write_pixels)
     std::vector<uint8_t> o;
     o.reserve(bytes);
-    o.push_back('B'); o.push_back('M');
-    put32(o, (uint32_t)bytes); put16(o, 0); put16(o, 0); put32(o, 14 + 108);
-    put32(o, 108); put32(o, width); put32(o, height); put16(o, 1); put16(o, 32);
-    put32(o, 3); put32(o, 0); put32(o, 0); put32(o, 0); put32(o, 0); put32(o, 0);
-    put32(o, 0xff0000u); put32(o, 0xff00u); put32(o, 0xffu); put32(o, 0xff000000u);
-    put32(o, 0);
-    for (int i = 0; i < 12; i++) put32(o, 0);   // CIEXYZ endpoints (9) + gamma (3)
+    bmp_header(o, width, height);
     for (uint32_t j = height; j-- > 0;) {
         const uint8_t* row = rgba.data() + (size_t)j * width * 4;
         for (uint32_t i = 0; i < width; i++) {

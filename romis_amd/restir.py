@@ -10,6 +10,7 @@ libromis_amd.so on the GPU; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -78,6 +79,12 @@ class Renderer:
 
     def set_seed(self, seed: int = _abi.RESTIR_DEFAULT_SEED, frame: int = 0) -> None:
         check(self.lib, self.lib.restir_set_seed(self.ctx, seed, frame), "restir_set_seed")
+
+    def set_renders_dir(self, path) -> None:
+        """The reference's RENDERS_DIR for file side outputs (None = none): R-OMIS renders with
+        save_alphas_visualisation write visualiseAlphas' bitmaps there after every iteration."""
+        d = None if path is None else os.fsencode(path)
+        check(self.lib, self.lib.restir_set_renders_dir(self.ctx, d), "restir_set_renders_dir")
 
     # ---- frame ----------------------------------------------------------------------------------------
     def render_restir(self, prev: ReservoirGrid | None, camera, width: int, height: int, features,

@@ -162,6 +162,77 @@ def test_render_mis_matches_oracle(gpu, oracle, name, case):
     assert np.isfinite(got).all() and got.max() > 0.0
 
 
+def expected_alpha_bitmaps(abi_lib, oracle, f, acc):
+    """visualiseAlphas (render_utils.cpp:189-243) of one iteration's accumulators: {file name: bytes}.  The alphas
+    are the oracle's solves (pinned to the reference's Eigen), the colours glm::mix in float32 (x (1 - a) + y a),
+    the bytes restir_encode_bmp's (pinned to the reference's stb in test_screen_output.py)."""
+    import ctypes as C
+    T = f.num_neighbours_to_sample + 1
+    npx = W * H
+    A = acc[:T * T]
+    alphas = np.zeros((3, T, npx), np.float32)
+    for p in range(npx):
+        Ap = A[:, p].reshape(T, T)   # symmetric (sums of v v^T)
+        for ch in range(3):
+            alphas[ch, :, p] = oracle.cod_solve(Ap, acc[T * T + ch * T:T * T + (ch + 1) * T, p])
+    one, zero = np.float32(1.0), np.float32(0.0)
+    out = {}
+    for i in range(T):
+        for ch, name in enumerate(("Red", "Green", "Blue")):
+            a = alphas[ch, i]
+            pos = a > zero
+            m = np.where(pos, a, -a).astype(np.float32)
+            mix = lambda y: (zero * (one - m)) + (np.asarray(y, np.float32) * m)   # noqa: E731
+            rgb = np.stack([mix(np.where(pos, one, zero)), mix(np.full(npx, 0.5, np.float32)),
+                            mix(np.where(pos, zero, one))], axis=-1).astype(np.float32)
+            img = np.ascontiguousarray(rgb.reshape(H, W, 3)[::-1])   # Screen::setPixel's y flip: row 0 = top
+            n = C.c_size_t()
+            abi_lib.restir_encode_bmp(img.ctypes.data, W, H, None, 0, C.byref(n))
+            buf = (C.c_uint8 * n.value)()
+            assert abi_lib.restir_encode_bmp(img.ctypes.data, W, H, buf, n.value, C.byref(n)) == 0
+            out[f"Distribution {i} - {name}.bmp"] = bytes(buf)
+    return out
+
+
+@pytest.mark.parametrize("case", ["romis_direct", "romis_progressive"])
+def test_romis_alpha_visualisation_matches_oracle(gpu, oracle, abi_lib, tmp_path, case):
+    """saveAlphasVisualisation (render.cpp:227-229): after every iteration the render writes the 3 (k + 1) alpha
+    bitmaps to <renders dir>/<currentTime()>/; each folder's files are byte-equal to one iteration's expected
+    images (iterations within a second share a folder and overwrite, as in the reference), the newest folder
+    holds the last iteration's, and the rendered screen is unchanged by the side output."""
+    f = _abi.default_features(**MIS_CASES[case])
+    f.max_iterations_mis = 2
+    f.save_alphas_visualisation = 1
+    osc, cam, n_t, p_mat, origin = setup(gpu, oracle, "nightclub_128pt", f)
+    nbr = oracle.neighbours(osc, f, key(oracle, 4, 0), key(oracle, 4, 1), W, H, n_t, p_mat)
+    acc = np.zeros((oracle.mis_acc_rows(f), W * H), np.float32)
+    want = []
+    for it in range(f.max_iterations_mis):
+        a, b, d = oracle.ris(osc, f, key(oracle, _abi.RESTIR_STAGE_RIS, it), origin, W, H, n_t, p_mat)
+        oracle.romis_accumulate(osc, f, origin, W, H, n_t, p_mat, nbr, a, b, d, it, acc)
+        want.append(expected_alpha_bitmaps(abi_lib, oracle, f, acc))
+    gpu.set_seed(SEED, 0)
+    gpu.set_renders_dir(tmp_path)
+    try:
+        got_rgb = gpu.render_mis(cam, W, H, f)
+    finally:
+        gpu.set_renders_dir(None)
+    bits_equal(got_rgb, oracle.render_mis(osc, cam, f, W, H, SEED, 0), f"{case}: screen with the visualisation on")
+    folders = sorted((d for d in tmp_path.iterdir() if d.is_dir()), key=lambda d: d.stat().st_mtime_ns)
+    assert 1 <= len(folders) <= f.max_iterations_mis, [d.name for d in folders]
+    for d in folders:
+        files = {p.name: p.read_bytes() for p in d.iterdir()}
+        assert sorted(files) == sorted(want[0]), d.name
+        assert any(files == w for w in want), f"{d.name}: images match no iteration's alphas"
+    newest = {p.name: p.read_bytes() for p in folders[-1].iterdir()}
+    for name, data in want[-1].items():
+        assert newest[name] == data, f"{folders[-1].name}/{name}: not the last iteration's image"
+    assert len({v for w in want for v in w.values()}) > 1   # the images carry information
+    gpu.set_seed(SEED, 0)
+    gpu.render_mis(cam, W, H, f)   # no renders dir: nothing more written
+    assert sorted(d.name for d in tmp_path.iterdir()) == sorted(d.name for d in folders)
+
+
 def test_mis_errors(gpu, oracle):
     sc = scene.bench_scene("nightclub_128pt")
     gpu.set_scene(sc)

@@ -85,7 +85,19 @@ def main():
                    "profile": os.path.relpath(dst, ROOT),
                    "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; bytes = "
                              "FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read correction) + WRITE_SIZE KiB x 1024"}
-            with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as fh:
+            # the per-config / per-order attribution study (scripts/traffic_json.py) stays, under its own hash
+            tpath = os.path.join(ROOT, "profiles", "traffic.json")
+            try:
+                with open(tpath) as fh:
+                    old = json.load(fh)
+            except (OSError, ValueError):
+                old = {}
+            if old.get("entries"):
+                rec["attribution"] = {"source_hash": old.get("source_hash"), "profile": old.get("profile"),
+                                      "method": old.get("method"), "entries": old["entries"]}
+            elif old.get("attribution"):
+                rec["attribution"] = old["attribution"]
+            with open(tpath, "w") as fh:
                 json.dump(rec, fh, indent=1)
     bj = os.path.join(src, "bench.json")
     if os.path.exists(bj):

@@ -756,7 +756,8 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
 }
 
 // RIS: capped at 96 VGPRs = 5 waves per SIMD (uncapped the allocator takes 100 = 4 waves; 5 waves run the
-// latency-bound candidate loop 9 % faster, 6 waves spill -- scripts/ablate.py, profiles/r1)
+// latency-bound candidate loop 9 % faster, 6 waves spill -- scripts/ablate.py, profiles/r1).  N = 2 the same:
+// k_primary_ris_n2_lds 407 -> 381 us at C2 N = 2 (profiles/r3/r3_configs/n2_*_c2.json).
 #ifndef ROMIS_RIS_WPE
 #define ROMIS_RIS_WPE 5
 #endif
@@ -768,10 +769,10 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         ris_body<NT, LDS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg, rp, wq);                             \
     }
 ROMIS_RIS_KERNEL(1, false, k_ris_n1, ROMIS_RIS_ATTR)
-ROMIS_RIS_KERNEL(2, false, k_ris_n2, )
+ROMIS_RIS_KERNEL(2, false, k_ris_n2, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL(0, false, k_ris_n0, )
 ROMIS_RIS_KERNEL(1, true, k_ris_n1_lds, ROMIS_RIS_ATTR)
-ROMIS_RIS_KERNEL(2, true, k_ris_n2_lds, )
+ROMIS_RIS_KERNEL(2, true, k_ris_n2_lds, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL(0, true, k_ris_n0_lds, )
 
 #define ROMIS_PRIMARY_RIS_KERNEL(NT, LDS, NAME, ATTR)                                                                  \
@@ -782,8 +783,8 @@ ROMIS_RIS_KERNEL(0, true, k_ris_n0_lds, )
     }
 ROMIS_PRIMARY_RIS_KERNEL(1, true, k_primary_ris_n1_lds, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(1, false, k_primary_ris_n1, ROMIS_RIS_ATTR)
-ROMIS_PRIMARY_RIS_KERNEL(2, true, k_primary_ris_n2_lds, )
-ROMIS_PRIMARY_RIS_KERNEL(2, false, k_primary_ris_n2, )
+ROMIS_PRIMARY_RIS_KERNEL(2, true, k_primary_ris_n2_lds, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL(2, false, k_primary_ris_n2, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(0, true, k_primary_ris_n0_lds, )
 ROMIS_PRIMARY_RIS_KERNEL(0, false, k_primary_ris_n0, )
 
@@ -1398,26 +1399,29 @@ ROMIS_SPATIAL1_LDS_KERNEL(true, false, 3, k_spatial1_ldsr_dbg)
 // LDS-DMA.  Each wave's 64 consecutive window entries l_nt[256k + 64w + lane] are written straight from global
 // memory (global_load_lds_dwordx4, lane l at the wave-uniform base + 16 l), no VGPR round trip; the caller waits
 // for them (explicit s_waitcnt vmcnt(0)) before its barrier, so after it every wave may read every entry.
+// TH: tile height in 8-row units (blocks of 256 TH threads, a (32 + 2R) x (8 TH + 2R) window).
+constexpr uint32_t apron_max(uint32_t TH) { return (kTileW + 2u * kLdsSpatialR) * (kTileH * TH + 2u * kLdsSpatialR); }
+template <uint32_t TH = 1>
 __device__ __forceinline__ void ntl_stage_window(const Region& rg, const float4* __restrict__ n_t, float4* l_nt, int ax0,
                                                  int ay0, uint32_t AW, uint32_t n_apron) {
-    constexpr uint32_t kPer = (kApronMax + 255u) / 256u;
+    constexpr uint32_t kThreads = 256u * TH, kPer = (apron_max(TH) + kThreads - 1u) / kThreads;
     const uint32_t magic = 0xFFFFFFFFu / AW + 1u;
     const uint32_t w64 = (threadIdx.x >> 6) << 6;
 #pragma unroll
     for (uint32_t k = 0; k < kPer; k++) {
-        const uint32_t i = threadIdx.x + 256u * k;
+        const uint32_t i = threadIdx.x + kThreads * k;
         if (i < n_apron) {
             uint32_t r = __umulhi(i, magic);   // i / AW for i < 2^16
             if (r * AW > i) r--;
             const uint32_t c = i - r * AW;
             const float4* src = n_t + (((uint32_t)(ay0 - (int)rg.vy0) + r) * rg.vw + (uint32_t)(ax0 - (int)rg.vx0) + c);
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                             (__attribute__((address_space(3))) void*)(l_nt + 256u * k + w64), 16, 0, 0);
+                                             (__attribute__((address_space(3))) void*)(l_nt + kThreads * k + w64), 16, 0, 0);
         }
     }
 }
 
-template <bool DBG>
+template <bool DBG, uint32_t TH = 1>
 __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
                                                   v3 origin, const float4* __restrict__ n_t,
                                                   const float4* __restrict__ p_mat, const float4* __restrict__ ia,
@@ -1427,18 +1431,19 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     const GlTabs tb = gl_stage_tables<false>();   // made visible by the window's barrier below
     float4* const l_nt = g_lds;
     uint32_t tile;
-    if (!xcd_tile(rg, num_tiles(rg), blockIdx.x, tile)) return;   // block-uniform
+    constexpr uint32_t kTH = kTileH * TH;   // tile rows
     const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
-    const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTileH);
+    if (!xcd_tile(rg, ntx * ((rg.rh + kTH - 1) / kTH), blockIdx.x, tile)) return;   // block-uniform
+    const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTH);
     // neighbour clamp bounds (render_utils.cpp:109-110: the image; here also the stored view), global coords
     const int xlo = max(0, (int)rg.vx0), xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1;
     const int ylo = max(0, (int)rg.vy0), yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1;
     const int R = (int)f.R;
     const int ax0 = max(tx0 - R, xlo), ax1 = min(tx0 + (int)kTileW - 1 + R, xhi);
-    const int ay0 = max(ty0 - R, ylo), ay1 = min(ty0 + (int)kTileH - 1 + R, yhi);
+    const int ay0 = max(ty0 - R, ylo), ay1 = min(ty0 + (int)kTH - 1 + R, yhi);
     const uint32_t AW = (uint32_t)(ax1 - ax0 + 1), n_apron = AW * (uint32_t)(ay1 - ay0 + 1);
-    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
-    const int x = tx0 + (int)(w * 8u + (l & 7u)), y = ty0 + (int)(l >> 3);
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;   // wave w: the 8x8 block (w % 4, w / 4)
+    const int x = tx0 + (int)((w & 3u) * 8u + (l & 7u)), y = ty0 + (int)((w >> 2) * 8u + (l >> 3));
     const bool live = x < (int)(rg.rx0 + rg.rw) && y < (int)(rg.ry0 + rg.rh);
     const uint32_t pofs = ((uint32_t)(y - (int)rg.vy0) * rg.vw + (uint32_t)(x - (int)rg.vx0)) << 4;
     // the pixel's own records (coalesced), issued first
@@ -1450,7 +1455,7 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
         cb = ld_at(ib, pofs);
         if (rp_in) pd_cached = ld_at(rp_in, pofs >> 2);
     }
-    ntl_stage_window(rg, n_t, l_nt, ax0, ay0, AW, n_apron);
+    ntl_stage_window<TH>(rg, n_t, l_nt, ax0, ay0, AW, n_apron);
     // neighbour draws while the loads are in flight
     const uint32_t K = f.K;   // <= kLeanK (host check)
     const uint32_t ps = pix_state(key, (uint32_t)y * rg.W + (uint32_t)x);
@@ -1541,6 +1546,22 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     }
 ROMIS_SPATIAL1_NTL_KERNEL(false, k_spatial1_ntl)
 ROMIS_SPATIAL1_NTL_KERNEL(true, k_spatial1_ntl_dbg)
+
+// k_spatial1_ntl_t2: the same pass on 32x16 tiles, 512-thread blocks (8 waves of 8x8): the window's apron rows are
+// shared by twice the pixels (30 KB per 8 waves instead of 23 KB per 4), so LDS allows 8 waves per SIMD when the
+// registers do (ROMIS_SPATIAL1_T2_WPE caps them: 8 -> 64 VGPRs).
+#ifndef ROMIS_SPATIAL1_T2_WPE
+#define ROMIS_SPATIAL1_T2_WPE 6
+#endif
+#define ROMIS_SPATIAL1_T2_KERNEL(DBG, NAME)                                                                           \
+    extern "C" __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL1_T2_WPE))) void     \
+    NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
+         const float4* p_mat, const float4* ia, const float4* ib, float4* oa, float4* ob, float2* odbg,               \
+         const float* rp_in, float* rp_out) {                                                                         \
+        spatial1_ntl_body<DBG, 2>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);    \
+    }
+ROMIS_SPATIAL1_T2_KERNEL(false, k_spatial1_ntl_t2)
+ROMIS_SPATIAL1_T2_KERNEL(true, k_spatial1_ntl_t2_dbg)
 
 // k_spatial2_ntl: the biased pass for N = 2 sub-reservoirs (the reference's default, common.h:105), laid out like
 // k_spatial1_ntl (32x8 tiles in the XCD chunk order, the n_t window in LDS by LDS-DMA, one shared depth
@@ -2923,7 +2944,22 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
             const uint32_t chunks = (nty + rg.xcd_rows - 1) / rg.xcd_rows;
             grid = 8u * ((chunks + 7u) / 8u) * rg.xcd_rows * ntx;
         }
-        if (tu.spatial_lds == 3u && f.R <= kLdsSpatialR) {
+        // 32x16 tiles (k_spatial1_ntl_t2) where the auto XCD chunk is at most 2 tile rows (wide images): C4 222 ->
+        // 203 us, C2 76.8 -> 79.0 (cfg_kbench, profiles/r3/r3k); spatial.th = 1 / 2 forces either
+        const uint32_t th = tu.spatial_th ? tu.spatial_th : (8192u / std::max(rg.rw, 1u) <= 2u ? 2u : 1u);
+        if (tu.spatial_lds == 3u && f.R <= kLdsSpatialR && th == 2u) {
+            // 32x16 tiles: the chunks hold half as many (twice as tall) tile rows
+            const uint32_t nty2 = (rg.rh + 2u * kTileH - 1) / (2u * kTileH);
+            if (rg.xcd_rows) {
+                rg.xcd_rows = std::max(1u, rg.xcd_rows / 2u);
+                grid = 8u * ((((nty2 + rg.xcd_rows - 1) / rg.xcd_rows) + 7u) / 8u) * rg.xcd_rows * ntx;
+            } else {
+                grid = ntx * nty2;
+            }
+            ROMIS_LAUNCH(odbg ? k_spatial1_ntl_t2_dbg : k_spatial1_ntl_t2, dim3(grid), dim3(2u * kBlock),
+                         apron_max(2) * 16u, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg,
+                         rp_in, rp_out);
+        } else if (tu.spatial_lds == 3u && f.R <= kLdsSpatialR) {
             ROMIS_LAUNCH(odbg ? k_spatial1_ntl_dbg : k_spatial1_ntl, dim3(grid), dim3(kBlock), kApronMax * 16u, stream,
                          s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
         } else if (tu.spatial_lds == 2u && f.R <= kLdsSpatialR) {

@@ -199,15 +199,17 @@ def test_temporal_bit_exact(gpu, oracle, N, clamp):
 
 # spatial kernels of an N = 1 biased pass: k_spatial1 (gathers; XCD order in 4-row chunks or one band),
 # k_spatial1_lds (n_t + reservoirs staged in LDS), k_spatial1_ldsr (reservoirs staged), k_spatial1_ntl (n_t
-# staged, the default), the general kernel
+# staged, the default; _t2: 32x16 tiles), the general kernel
 SPATIAL_VARIANTS = {"gather": {"spatial.lean": 1, "spatial.lds": 0},
                     "gather_band": {"spatial.lean": 1, "spatial.lds": 0, "spatial.xcd_rows": 0},
                     "lds": {"spatial.lean": 1, "spatial.lds": 1},
                     "ldsr": {"spatial.lean": 1, "spatial.lds": 2},
-                    "ntl": {"spatial.lean": 1, "spatial.lds": 3},
+                    "ntl": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 1},
                     "ntl_rows2": {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 2},
+                    "ntl_t2": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 2},
+                    "ntl_t2_band": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 2, "spatial.xcd_rows": 0},
                     "general": {"spatial.lean": 0}}
-SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 255}
+SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 255, "spatial.th": 0}
 
 
 # every (scene, N, combine mode) through the default knobs ("gather" selects the lean gather kernel for N = 1 biased

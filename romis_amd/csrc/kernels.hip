@@ -2960,7 +2960,11 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
                          apron_max(2) * 16u, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg,
                          rp_in, rp_out);
         } else if (tu.spatial_lds == 3u && f.R <= kLdsSpatialR) {
-            ROMIS_LAUNCH(odbg ? k_spatial1_ntl_dbg : k_spatial1_ntl, dim3(grid), dim3(kBlock), kApronMax * 16u, stream,
+#ifndef ROMIS_NTL_EXTRA_LDS
+#define ROMIS_NTL_EXTRA_LDS 0   // occupancy experiments (build variants): extra dynamic LDS per block
+#endif
+            ROMIS_LAUNCH(odbg ? k_spatial1_ntl_dbg : k_spatial1_ntl, dim3(grid), dim3(kBlock),
+                         kApronMax * 16u + ROMIS_NTL_EXTRA_LDS, stream,
                          s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
         } else if (tu.spatial_lds == 2u && f.R <= kLdsSpatialR) {
             ROMIS_LAUNCH(odbg ? k_spatial1_ldsr_dbg : k_spatial1_ldsr, dim3(grid), dim3(kBlock), 2u * kApronMax * 16u, stream,

@@ -58,6 +58,15 @@ VARIANTS = {
                    (r"rand01\(draw\(ps, 4u \* c \+ 3u\)\)", "0.5f")],
     "ris_no_update": [(r"res_update<NT>\(r, N, pos, col, weight\(pd\), rand01\(draw\(ps, 4u \* c \+ 3u\)\), pd\);",
                        "r[0].wsum += weight(pd); r[0].pos = vadd(r[0].pos, pos);")],
+    # pieces of the target pdf itself (shared device functions: every kernel changes, RIS is the one timed)
+    "risg_no_pow": [(r"return pow_pre\(x, px, pw, job\) \? pw : pow_core\(tb, job, px\.kd_sh\.w\);",
+                     "return x * px.kd_sh.w;")],
+    "risg_no_div": [(r"return vdivs\(vadd\(diffuse, specular\), d \* d\);", "return vscale(vadd(diffuse, specular), d * d);")],
+    "risg_no_norm": [(r"v3 L = vnormalize_len\(vsub\(lpos, px\.P\), r\.d\);", "v3 L = vsub(lpos, px.P); r.d = L.x + L.y;"),
+                     (r"v3 R = vnormalize\(vsub\(vscale\(px\.N, 2\.0f \* r\.dotNL\), L\)\);",
+                      "v3 R = vsub(vscale(px.N, 2.0f * r.dotNL), L);")],
+    "risg_no_len": [(r"return vlength\(shade_ref\(s, f, px, lpos, lcol, tb\)\);",
+                     "const v3 sh_ = shade_ref(s, f, px, lpos, lcol, tb); return sh_.x + sh_.y + sh_.z;")],
     # the whole combine (takes) -> sums
     "no_take": [(r"cmb\.take\(target_pdf\(s, f, cur, p, c, tb\), na\[n\]\.w, __float_as_uint\(nb\[n\]\.w\), p, c\);",
                  "cmb.wsum += target_pdf(s, f, cur, p, c, tb) * na[n].w; cmb.macc += __float_as_uint(nb[n].w);")],
@@ -70,7 +79,10 @@ def main():
     for name, subs in VARIANTS.items():
         if only and name not in only:
             continue
-        a, b = body_span(src, "ris" if name.startswith("ris_") else "spatial")
+        if name.startswith("risg_"):
+            a, b = 0, len(src)
+        else:
+            a, b = body_span(src, "ris" if name.startswith("ris_") else "spatial")
         body = src[a:b]
         for pat, rep in subs:
             body, n = re.subn(pat, rep, body)

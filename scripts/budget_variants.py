@@ -33,7 +33,7 @@ def body_span(src, which):
 # name -> list of (regex, replacement) applied inside spatial1_ntl_body only
 VARIANTS = {
     # the K neighbour target pdfs (the combine's p-hat chains) -> a 2-op stand-in on the same inputs
-    "no_phat": [(r"target_pdf\(s, f, cur, p, c, tb\)", "fabsf(p.x + c.y)")],
+    "no_phat": [(r"target_pdf(?:_lean)?\(s, f, cur, p, c, tb\)", "fabsf(p.x + c.y)")],
     # the neighbour offset draws (2 mix32 + umulhi + clamp each) -> a multiply-add of the pixel state
     "no_rng": [(r"__umulhi\(draw\(ps, 2u \* n\), span\)", "((ps + 2u * n) % span)"),
                (r"__umulhi\(draw\(ps, 2u \* n \+ 1u\), span\)", "((ps >> 8) + n) % span")],
@@ -53,7 +53,7 @@ VARIANTS = {
                         "    const float4 cn = l_nt[(uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0)];"),
                        (r"    ntl_stage_window\(rg, n_t, l_nt, ax0, ay0, AW, n_apron\);", "")],
     # RIS (ris_pixel): the candidates' target pdfs, light-index draws + accept draws, reservoir updates
-    "ris_no_phat": [(r"target_pdf\(s, f, px, pos, col, tb\);", "fabsf(pos.x + col.y);")],
+    "ris_no_phat": [(r"target_pdf(?:_lean)?\(s, f, px, pos, col, tb\);", "fabsf(pos.x + col.y);")],
     "ris_no_rng": [(r"uniform_index\(draw\(ps, 4u \* c\), L\)", "min(c, L - 1u)"),
                    (r"rand01\(draw\(ps, 4u \* c \+ 3u\)\)", "0.5f")],
     "ris_no_update": [(r"res_update<NT>\(r, N, pos, col, weight\(pd\), rand01\(draw\(ps, 4u \* c \+ 3u\)\), pd\);",
@@ -68,7 +68,7 @@ VARIANTS = {
     "risg_no_len": [(r"return vlength\(shade_ref\(s, f, px, lpos, lcol, tb\)\);",
                      "const v3 sh_ = shade_ref(s, f, px, lpos, lcol, tb); return sh_.x + sh_.y + sh_.z;")],
     # the whole combine (takes) -> sums
-    "no_take": [(r"cmb\.take\(target_pdf\(s, f, cur, p, c, tb\), na\[n\]\.w, __float_as_uint\(nb\[n\]\.w\), p, c\);",
+    "no_take": [(r"cmb\.take\(target_pdf(?:_lean)?\(s, f, cur, p, c, tb\), na\[n\]\.w, __float_as_uint\(nb\[n\]\.w\), p, c\);",
                  "cmb.wsum += target_pdf(s, f, cur, p, c, tb) * na[n].w; cmb.macc += __float_as_uint(nb[n].w);")],
 }
 

@@ -39,7 +39,8 @@ def main():
         W, H = cf.get("tile") or cf["image"]
         px = W * H
         times = json.load(open(os.path.join(src, f"{cfgname}_times.json")))["us_per_launch"]
-        for order, rows in (("chunks", 255), ("bands", 0)):
+        orders = [("chunks", 255), ("bands", 0)] + ([("chunks_th1", 255)] if cfgname == "c4" else [])
+        for order, rows in orders:
             f = os.path.join(src, f"{cfgname}_{order}_FETCH_SIZE", "run_counter_collection.csv")
             w = os.path.join(src, f"{cfgname}_{order}_WRITE_SIZE", "run_counter_collection.csv")
             for p, tag in ((f, "fetch"), (w, "write")):
@@ -49,8 +50,9 @@ def main():
             alg = px * 96
             cfg = {"config": cfgname, "scene": cf["scene"], "tile": [W, H], "M": cf["M"], "N": 1, "k": 5, "r": 10,
                    "passes": cf["passes"]}
+            kernels = sorted({r["Kernel_Name"] for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith("k_spatial")})
             entries.append({
-                "config": cfg, "xcd_order": order, "spatial.xcd_rows": rows,
+                "config": cfg, "xcd_order": order, "spatial.xcd_rows": rows, "kernel": ",".join(kernels),
                 "traffic_bytes_per_launch": int(fetch + write), "fetch_bytes": int(fetch), "write_bytes": int(write),
                 "algorithmic_bytes": alg, "ratio": round((fetch + write) / alg, 3),
                 "fetch_B_per_px": round(fetch / px, 1), "write_B_per_px": round(write / px, 1),

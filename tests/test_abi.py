@@ -84,6 +84,7 @@ def test_features_default_matches_reference_struct(abi_lib):
 
 def test_context_calls_fail_cleanly_on_null(abi_lib):
     assert abi_lib.restir_set_seed(None, 1, 2) == 1
+    assert abi_lib.restir_set_renders_dir(None, b"/tmp") == 1
     assert abi_lib.restir_synchronize(None) == 1
     assert abi_lib.restir_render(None, None, None, 1, 1, None, None, None, None) == 1
 

@@ -38,8 +38,8 @@ TILE_W, TILE_H = 1920, 1080
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)   # ~0.1 s timed at C2: past the first frames after the idle sync (slower clocks; 50 steps read 2 % low, profiles/r3/r3q)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
                     help="BASELINE.json config (c2 = configs[1], the headline)")
     ap.add_argument("--scene", default=None, help="override the config's scene")

@@ -1966,6 +1966,17 @@ restir_status restir_enable_timing(restir_ctx* c, int enable) {
     if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
     std::lock_guard<std::mutex> lk(c->mu);
     c->timing = enable != 0;
+    if (c->timing) {
+        // the events the timed launches take, created here rather than by the launches themselves: a
+        // hipEventCreate costs microseconds of host time inside whatever region is being timed
+        HIP_TRY(hipSetDevice(c->device));
+        const size_t want = 2048;
+        while (c->free_events.size() + c->pending.size() * 2 < want) {
+            hipEvent_t e = nullptr;
+            HIP_TRY(hipEventCreate(&e));
+            c->free_events.push_back(e);
+        }
+    }
     return RESTIR_OK;
 }
 

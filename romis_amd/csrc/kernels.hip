@@ -426,13 +426,27 @@ __device__ __forceinline__ uint32_t res_update(Sub* r, uint32_t N, v3 pos, v3 co
     float best = ROMIS_FLT_MAX;
     const uint32_t n = NT > 0 ? (uint32_t)NT : N;
     if (NT > 0) {
-        // compile-time N: predicated updates, no dynamic register indexing
+        // compile-time N: every sub-reservoir updated by selects, no dynamic register indexing (predicated
+        // sub_take calls were merged back into one r[k] store by the compiler, which put r[] in scratch memory)
 #pragma unroll
         for (uint32_t j = 0; j < (uint32_t)(NT > 0 ? NT : 1); j++)
             if (r[j].wsum < best) { k = j; best = r[j].wsum; }
+        float ws = r[0].wsum;
 #pragma unroll
-        for (uint32_t j = 0; j < (uint32_t)(NT > 0 ? NT : 1); j++)
-            if (j == k) sub_take(r[j], pos, col, w, u, pd);
+        for (uint32_t j = 1; j < (uint32_t)(NT > 0 ? NT : 1); j++) ws = (j == k) ? r[j].wsum : ws;
+        ws += w;                            // sub_take's wsum += w on the routed one
+        const bool acc = u < (w / ws);      // ... and its acceptance test
+#pragma unroll
+        for (uint32_t j = 0; j < (uint32_t)(NT > 0 ? NT : 1); j++) {
+            const bool sel = j == k, take = sel && acc;
+            r[j].M += sel ? 1u : 0u;
+            r[j].wsum = sel ? ws : r[j].wsum;
+            r[j].pos = mk(take ? pos.x : r[j].pos.x, take ? pos.y : r[j].pos.y, take ? pos.z : r[j].pos.z);
+            r[j].col = mk(take ? col.x : r[j].col.x, take ? col.y : r[j].col.y, take ? col.z : r[j].col.z);
+            r[j].chosen = take ? w : r[j].chosen;
+            r[j].pd = take ? pd : r[j].pd;
+            r[j].has_pd = take || r[j].has_pd;
+        }
     } else {
         for (uint32_t j = 0; j < n; j++)
             if (r[j].wsum < best) { k = j; best = r[j].wsum; }
@@ -863,8 +877,14 @@ __device__ __forceinline__ void temporal_body(const SceneDev& s, const Region& r
     if (NT == 1 && rp_out) rp_out[p] = pd_out[0];
 }
 
+// register cap of the temporal kernels (build variants; unset = the compiler's choice)
+#ifdef ROMIS_TEMPORAL_WPE
+#define ROMIS_TEMPORAL_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_TEMPORAL_WPE)))
+#else
+#define ROMIS_TEMPORAL_ATTR
+#endif
 #define ROMIS_TEMPORAL_KERNEL(NT)                                                                                      \
-    extern "C" __global__ __launch_bounds__(256) void k_temporal_n##NT(                                               \
+    extern "C" __global__ __launch_bounds__(256) ROMIS_TEMPORAL_ATTR void k_temporal_n##NT(                           \
         SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,          \
         const float4* p_mat, const float4* ca, const float4* cb, const float4* pa, const float4* pb, float4* oa,      \
         float4* ob, float2* odbg, const float* rp_in, float* rp_out) {                                                \

@@ -690,20 +690,22 @@ def test_full_size_c1_frame_matches_oracle(gpu, oracle):
     assert rgb.mean() > 0.01
 
 
-def test_full_size_c3_sequence_band_parity(gpu, oracle):
+@pytest.mark.parametrize("N", [1, 2])
+def test_full_size_c3_sequence_band_parity(gpu, oracle, N):
     """C3 at its full size: 1080p nightclub, 128 point lights, M = 32, two spatial passes, temporal reuse over 4
     frames threaded through the frame pool (each predecessor released as the sequence goes, and an unrelated frame
     rendered between frames 1 and 2 so recycled records are reused).  Checked on sampled row bands: frame f's rows
     depend on frame f - 1's grid within passes * r = 20 rows (temporal reuse is same-pixel, render_utils.cpp:155;
     spatial reuse reads +-r per pass, :91), so the oracle renders frame 0 on the band grown by 4 * 20 = 80 rows,
     frame 1 on the band grown by 60, ... each frame's view being the previous frame's owned rows.  Every frame's
-    RGB and the last frame's grid are compared on the band, bit for bit."""
+    RGB and the last frame's grid are compared on the band, bit for bit.  N = 2 is the reference's default
+    (common.h:105): k_temporal_n2, k_spatial2_ntl and k_final_n2_sorted at full size."""
     name, Wf, Hf, P, R, frames = "nightclub_128pt", 1920, 1080, 2, 10, 4
     s = get_scene(name)
     gpu.set_scene(s)
     osc = oracle.OracleScene(s)
     cam = scene.camera_for(name, Wf, Hf)
-    f = _abi.default_features(initial_light_samples=32, num_samples_in_reservoir=1, spatial_resampling_passes=P,
+    f = _abi.default_features(initial_light_samples=32, num_samples_in_reservoir=N, spatial_resampling_passes=P,
                               spatial_resample_radius=R, temporal_reuse=1)
     gpu.set_seed(SEED, 0)
     rgbs, grid = [], None
@@ -733,8 +735,8 @@ def test_full_size_c3_sequence_band_parity(gpu, oracle):
             sl = slice((ry0 - vy0) * Wf, (ry1 - vy0) * Wf)
             prev = (np.ascontiguousarray(a[:, sl]), np.ascontiguousarray(b[:, sl]))
         a, b = prev                                    # frame 3's grid on its owned band (= the checked rows)
-        a = a.reshape(1, -1, Wf, 4)
-        b = b.reshape(1, -1, Wf, 4)
+        a = a.reshape(N, -1, Wf, 4)
+        b = b.reshape(N, -1, Wf, 4)
         gs = slice(y0, y0 + rows)
         assert_bits(pos[:, gs], np.ascontiguousarray(a[..., :3]), f"C3 grid position rows {y0}..")
         assert_bits(w[:, gs], np.ascontiguousarray(a[..., 3]), f"C3 grid W rows {y0}..")

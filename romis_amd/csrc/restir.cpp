@@ -1970,7 +1970,7 @@ restir_status restir_enable_timing(restir_ctx* c, int enable) {
         // the events the timed launches take, created here rather than by the launches themselves: a
         // hipEventCreate costs microseconds of host time inside whatever region is being timed
         HIP_TRY(hipSetDevice(c->device));
-        const size_t want = 2048;
+        const size_t want = 512;   // bench.py's default timed region (200 frames x 2) without growing; more on demand
         while (c->free_events.size() + c->pending.size() * 2 < want) {
             hipEvent_t e = nullptr;
             HIP_TRY(hipEventCreate(&e));

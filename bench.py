@@ -122,13 +122,21 @@ def committed_traffic(cfg):
         with open(path) as fh:
             rec = json.load(fh)
         keys = ("scene", "tile", "M", "N", "k", "r", "passes")
-        if rec.get("source_hash") != build.source_hash():
-            return None, None
-        # entries: per config and XCD tile order (scripts/traffic_json.py); the default order is "chunks"
-        for e in rec.get("entries") or [rec]:
-            rc = e.get("config") or {}
-            if e.get("xcd_order", "chunks") == "chunks" and all(rc.get(k) == cfg.get(k) for k in keys):
-                return e["traffic_bytes_per_launch"], rec.get("profile")
+        here = build.source_hash()
+        # the top-level record (scripts/collect_profiles.py: the headline's --pmc passes), then the per-config
+        # entries of the attribution study (scripts/traffic_json.py), each only at these exact kernel sources;
+        # the default XCD tile order is "chunks"
+        groups = []
+        if rec.get("source_hash") == here:
+            groups.append((rec.get("entries") or [rec], rec.get("profile")))
+        att = rec.get("attribution") or {}
+        if att.get("source_hash") == here:
+            groups.append((att.get("entries") or [], att.get("profile")))
+        for entries, profile in groups:
+            for e in entries:
+                rc = e.get("config") or {}
+                if e.get("xcd_order", "chunks") == "chunks" and all(rc.get(k) == cfg.get(k) for k in keys):
+                    return e["traffic_bytes_per_launch"], profile
     except (OSError, ValueError, KeyError):
         pass
     return None, None

@@ -642,7 +642,18 @@ extern "C" __global__ __launch_bounds__(256) void k_primary_lds(SceneDev s, Regi
 // ---------------------------------------------------------------------------------------------------------
 // genCanonicalSamples for one pixel whose G-buffer records are (nt, pm); lights = the light table (global or
 // the block's LDS copy), bvh = the traversal arrays for the initial visibility rays.
-template <int NT>
+// LT: the light table's form (host-detected scene properties; genCanonicalSamples' switch, light.cpp:55-78, reduces
+// to one case, so the candidate loop carries no lane-divergent light-type branch):
+//   kLtGeneral  7 float4 per light (SceneDev::lights);
+//   kLtPoint    every light a point light (light_types == 1): the compact table SceneDev::light_c2, 2 float4 per
+//               light (rows 0 and 3 of its record: position, colour);
+//   kLtGrid     every light a parallelogram with light 0's edges and one colour at all four of its corners
+//               (SceneDev::lights_grid: the reference's regularLightGrid, scene.cpp:5-28): light_c2 holds its
+//               corner v0 and colour; the shared edges are read from light 0's record, and the two identical
+//               inner mixes of the colour interpolation are evaluated once.  The same operations on the same
+//               values as the general case.
+constexpr int kLtGeneral = 0, kLtPoint = 1, kLtGrid = 2;
+template <int NT, int LT = kLtGeneral>
 __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                           const float4* lights, const Bvh& bvh, float4 nt, float4 pm, uint32_t x,
                                           uint32_t y, size_t p, float4* __restrict__ ra, float4* __restrict__ rb,
@@ -685,11 +696,29 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 }
             };
             auto record = [&](uint32_t c) {
-                return lights + 7u * uniform_index(draw(ps, 4u * c), L);
+                return lights + (LT == kLtGeneral ? 7u : 2u) * uniform_index(draw(ps, 4u * c), L);
+            };
+            // kLtGrid: the shared edges, light 0's rows 1 and 2, read per candidate through the scalar cache (an
+            // opaque pointer keeps the compiler from hoisting them into loop-long VGPRs, which spill)
+            auto shared_row = [&](uint32_t r) {
+                const float4* sh = s.lights;
+                asm volatile("" : "+s"(sh));
+                return xyz(sh[r]);
             };
             auto sample = [&](uint32_t c, v3& pos, v3& col) {
                 const float4* lt = record(c);
-                sample_rec(c, lt, lt[0], lt[3], pos, col);
+                if (LT == kLtPoint) {
+                    pos = xyz(lt[0]); col = xyz(lt[1]);
+                } else if (LT == kLtGrid) {   // sampleParallelogramLight, as sample_rec's type-2 case
+                    float a = rand01(draw(ps, 4u * c + 1u));
+                    float b = rand01(draw(ps, 4u * c + 2u));
+                    pos = vadd(vadd(xyz(lt[0]), vscale(shared_row(1), a)), vscale(shared_row(2), b));
+                    const v3 gc = xyz(lt[1]);
+                    const v3 m = vmix(gc, gc, a);   // = vmix(c0, c1, a) = vmix(c2, c3, a): all four corners are gc
+                    col = vmix(m, m, b);
+                } else {
+                    sample_rec(c, lt, lt[0], lt[3], pos, col);
+                }
             };
             auto weight = [&](float pd) { return s.light_scale != 0.0f ? pd * s.light_scale : pd / invL; };  // light.cpp:80
             uint32_t c = 0;
@@ -716,14 +745,25 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
 // k_ris: genCanonicalSamples per pixel.  Lane-serial candidate loop (M iterations) -- VALU bound.  The light
 // table is staged into LDS once per persistent block when it fits (LDS_LIGHTS), so the per-candidate random
 // light fetch is an LDS read instead of a dependent global load.
-template <int NT, bool LDS_LIGHTS>
+// The light table of form LT: the 7-float4 records or the compact (row 0, row 3) table.
+template <int LT>
+__device__ __forceinline__ const float4* global_lights(const SceneDev& s) { return LT == kLtGeneral ? s.lights : s.light_c2; }
+// Stage it into LDS at dst.  No barrier.
+template <int LT>
+__device__ __forceinline__ void stage_lights(const SceneDev& s, float4* dst) {
+    const float4* src = global_lights<LT>(s);
+    const uint32_t n = (LT == kLtGeneral ? 7u : 2u) * s.num_lights;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
+template <int NT, bool LDS_LIGHTS, int LT = kLtGeneral>
 __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                          const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                          float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
                                          float* __restrict__ rp, WorkQueue wq) {
-    const float4* lights = s.lights;
+    const float4* lights = global_lights<LT>(s);
     if (LDS_LIGHTS) {
-        for (uint32_t i = threadIdx.x; i < 7u * s.num_lights; i += blockDim.x) g_lds[i] = s.lights[i];
+        stage_lights<LT>(s, g_lds);
         __syncthreads();
         lights = g_lds;
     }
@@ -735,7 +775,7 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
         uint32_t x, y;
         size_t p;
         if (!work_pixel(rg, item, x, y, p)) continue;
-        ris_pixel<NT>(s, rg, f, key, origin, lights, bvh, n_t[gidx(rg, p)], p_mat[p], x, y, p, ra, rb, rdbg, rp, tb);
+        ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, n_t[gidx(rg, p)], p_mat[p], x, y, p, ra, rb, rdbg, rp, tb);
     }
 }
 
@@ -743,16 +783,16 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
 // the G-buffer records go to memory for the later passes and straight into the pixel's RIS, and the primary
 // ray's latency-bound BVH traversal runs beside other waves' VALU-bound candidate loops.  The block stages the
 // BVH and, when it fits beside it, the light table in LDS.
-template <int NT, bool LDS_LIGHTS>
+template <int NT, bool LDS_LIGHTS, int LT = kLtGeneral>
 __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region& rg, const CameraDev& cam,
                                                  const FeaturesDev& f, uint32_t key, float4* __restrict__ n_t,
                                                  float4* __restrict__ p_mat, float4* __restrict__ n_t2,
                                                  float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
                                                  float* __restrict__ rp) {
     const uint32_t bvh_f4 = 2u * s.num_nodes + 3u * s.num_tris;
-    const float4* lights = s.lights;
+    const float4* lights = global_lights<LT>(s);
     if (LDS_LIGHTS) {
-        for (uint32_t i = threadIdx.x; i < 7u * s.num_lights; i += blockDim.x) g_lds[bvh_f4 + i] = s.lights[i];
+        stage_lights<LT>(s, g_lds + bvh_f4);
         lights = g_lds + bvh_f4;
     }
     const Bvh bvh = stage_bvh(s, g_lds);   // ends with the barrier that also covers the light copy
@@ -765,7 +805,7 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         if (!work_pixel(rg, item, x, y, p)) continue;
         float4 nt, pm;
         primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, nt, pm);
-        ris_pixel<NT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb);
+        ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb);
     }
 }
 
@@ -776,31 +816,49 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
 #define ROMIS_RIS_WPE 5
 #endif
 #define ROMIS_RIS_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_RIS_WPE)))
-#define ROMIS_RIS_KERNEL(NT, LDS, NAME, ATTR)                                                                         \
+#define ROMIS_RIS_KERNEL_LT(NT, LDS, LT, NAME, ATTR)                                                                  \
     extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,   \
                                                           float4* ra, float4* rb, float2* rdbg, float* rp, WorkQueue wq) { \
-        ris_body<NT, LDS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg, rp, wq);                             \
+        ris_body<NT, LDS, LT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg, rp, wq);                         \
     }
+#define ROMIS_RIS_KERNEL(NT, LDS, NAME, ATTR) ROMIS_RIS_KERNEL_LT(NT, LDS, kLtGeneral, NAME, ATTR)
 ROMIS_RIS_KERNEL(1, false, k_ris_n1, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL(2, false, k_ris_n2, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL(0, false, k_ris_n0, )
 ROMIS_RIS_KERNEL(1, true, k_ris_n1_lds, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL(2, true, k_ris_n2_lds, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL(0, true, k_ris_n0_lds, )
+ROMIS_RIS_KERNEL_LT(1, true, kLtPoint, k_ris_n1_lds_pt, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(2, true, kLtPoint, k_ris_n2_lds_pt, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(1, false, kLtPoint, k_ris_n1_pt, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(2, false, kLtPoint, k_ris_n2_pt, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(1, true, kLtGrid, k_ris_n1_lds_grid, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(2, true, kLtGrid, k_ris_n2_lds_grid, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(1, false, kLtGrid, k_ris_n1_grid, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(2, false, kLtGrid, k_ris_n2_grid, ROMIS_RIS_ATTR)
 
-#define ROMIS_PRIMARY_RIS_KERNEL(NT, LDS, NAME, ATTR)                                                                  \
+#define ROMIS_PRIMARY_RIS_KERNEL_LT(NT, LDS, LT, NAME, ATTR)                                                           \
     extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, CameraDev cam, FeaturesDev f,   \
                                                           uint32_t key, float4* n_t, float4* p_mat, float4* n_t2,      \
                                                           float4* ra, float4* rb, float2* rdbg, float* rp) {           \
-        primary_ris_body<NT, LDS>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp);                              \
+        primary_ris_body<NT, LDS, LT>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp);                          \
     }
+#define ROMIS_PRIMARY_RIS_KERNEL(NT, LDS, NAME, ATTR) ROMIS_PRIMARY_RIS_KERNEL_LT(NT, LDS, kLtGeneral, NAME, ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(1, true, k_primary_ris_n1_lds, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(1, false, k_primary_ris_n1, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(2, true, k_primary_ris_n2_lds, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(2, false, k_primary_ris_n2, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(0, true, k_primary_ris_n0_lds, )
 ROMIS_PRIMARY_RIS_KERNEL(0, false, k_primary_ris_n0, )
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtPoint, k_primary_ris_n1_lds_pt, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(2, true, kLtPoint, k_primary_ris_n2_lds_pt, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtPoint, k_primary_ris_n1_pt, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(2, false, kLtPoint, k_primary_ris_n2_pt, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtGrid, k_primary_ris_n1_lds_grid, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(2, true, kLtGrid, k_primary_ris_n2_lds_grid, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtGrid, k_primary_ris_n1_grid, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(2, false, kLtGrid, k_primary_ris_n2_grid, ROMIS_RIS_ATTR)
 
 // ---------------------------------------------------------------------------------------------------------
 // Combine state shared by temporal and spatial: out[] (Reservoir(N) of the current pixel) + routed M sums.
@@ -2846,6 +2904,15 @@ inline uint32_t items_of(const Region& rg) {
 inline dim3 grid_capped(uint32_t items, uint32_t cap) { return dim3(cap && items > cap ? cap : items); }
 inline size_t bvh_lds_bytes(const SceneDev& s) { return ((size_t)2 * s.num_nodes + (size_t)3 * s.num_tris) * 16; }
 inline size_t lights_lds_bytes(const SceneDev& s) { return (size_t)7 * s.num_lights * 16; }
+// The RIS light-table form (ris_pixel's LT) for this scene and N: the compact tables of the _pt / _grid kernels
+// (N = 1, 2) when the scene's lights allow them and ris.compact is on, else the general records.
+inline int ris_light_form(const SceneDev& s, const FeaturesDev& f, const Tuning& tu) {
+    if (!tu.ris_compact || s.num_lights == 0 || (f.N != 1 && f.N != 2)) return kLtGeneral;
+    if (s.light_types == 1u) return kLtPoint;
+    if (s.lights_grid) return kLtGrid;
+    return kLtGeneral;
+}
+inline size_t ris_lights_lds_bytes(const SceneDev& s, int lt) { return (size_t)(lt == kLtGeneral ? 7 : 2) * s.num_lights * 16; }
 inline Region with_map(Region rg, uint32_t map2d) { rg.map2d = map2d; return rg; }
 }  // namespace
 
@@ -2874,11 +2941,16 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f
         wq = WorkQueue{qs.ctr, qs.base};
         qs.base += items_of(rg) + grid.x;
     }
-    const size_t lds = lights_lds_bytes(s);
-    const bool use_lds = tu.ris_lds && s.num_lights > 0 && lds <= kLdsBudget;
-    auto k = use_lds ? (f.N == 1 ? k_ris_n1_lds : (f.N == 2 ? k_ris_n2_lds : k_ris_n0_lds))
-                     : (f.N == 1 ? k_ris_n1 : (f.N == 2 ? k_ris_n2 : k_ris_n0));
-    ROMIS_LAUNCH(k, grid, dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ra,
+    const int lt = ris_light_form(s, f, tu);
+    const size_t lds = ris_lights_lds_bytes(s, lt);
+    const bool staged = tu.ris_lds && s.num_lights > 0 && lds <= kLdsBudget;
+    auto k = lt == kLtPoint ? (staged ? (f.N == 1 ? k_ris_n1_lds_pt : k_ris_n2_lds_pt) : (f.N == 1 ? k_ris_n1_pt : k_ris_n2_pt))
+           : lt == kLtGrid ? (staged ? (f.N == 1 ? k_ris_n1_lds_grid : k_ris_n2_lds_grid)
+                                     : (f.N == 1 ? k_ris_n1_grid : k_ris_n2_grid))
+           : staged ? (f.N == 1 ? k_ris_n1_lds : (f.N == 2 ? k_ris_n2_lds : k_ris_n0_lds))
+                    : (f.N == 1 ? k_ris_n1 : (f.N == 2 ? k_ris_n2 : k_ris_n0));
+    const size_t lds_used = lds;
+    ROMIS_LAUNCH(k, grid, dim3(kBlock), staged ? lds_used : 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ra,
                        rb, rdbg, f.N == 1 ? rp : nullptr, wq);
     return hipGetLastError();
 }
@@ -2888,10 +2960,16 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
                               float* rp, const Tuning& tu, hipStream_t stream) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, tu.primary_2d);
-    const size_t bvh = bvh_lds_bytes(s), lights = lights_lds_bytes(s);
+    const size_t bvh = bvh_lds_bytes(s);
     if (bvh > kLdsBudget) return hipErrorInvalidValue;   // caller checks primary_ris_fits()
+    const int lt = ris_light_form(s, f, tu);
+    const size_t lights = ris_lights_lds_bytes(s, lt);
     const bool use_lights = tu.ris_lds && s.num_lights > 0 && bvh + lights <= kLdsBudget;
-    auto k = use_lights ? (f.N == 1 ? k_primary_ris_n1_lds : (f.N == 2 ? k_primary_ris_n2_lds : k_primary_ris_n0_lds))
+    auto k = lt == kLtPoint ? (use_lights ? (f.N == 1 ? k_primary_ris_n1_lds_pt : k_primary_ris_n2_lds_pt)
+                                          : (f.N == 1 ? k_primary_ris_n1_pt : k_primary_ris_n2_pt))
+           : lt == kLtGrid ? (use_lights ? (f.N == 1 ? k_primary_ris_n1_lds_grid : k_primary_ris_n2_lds_grid)
+                                         : (f.N == 1 ? k_primary_ris_n1_grid : k_primary_ris_n2_grid))
+           : use_lights ? (f.N == 1 ? k_primary_ris_n1_lds : (f.N == 2 ? k_primary_ris_n2_lds : k_primary_ris_n0_lds))
                         : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
     ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.ris_blocks), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
                  cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr);

@@ -206,7 +206,7 @@ struct restir_ctx {
     std::mutex mu;
 
     // scene
-    DevBuf nodes, tri_v0, tri_e1, tri_e2, tri_n0, tri_n1, tri_n2, materials, lights, tex_texels, tex_dims, tri_uv;
+    DevBuf nodes, tri_v0, tri_e1, tri_e2, tri_n0, tri_n1, tri_n2, materials, lights, light_c2, tex_texels, tex_dims, tri_uv;
     SceneDev sdev{};
     bool has_scene = false;
 
@@ -878,6 +878,21 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     ST_TRY(c->tri_n2.upload(n2.data(), n2.size() * 4, c->stream));
     ST_TRY(c->materials.upload(mats.data(), mats.size() * 4, c->stream));
     ST_TRY(c->lights.upload(lt.data(), lt.size() * 4, c->stream));
+    // the compact light table of the RIS kernels' point and grid forms (kernels.hip kLtPoint / kLtGrid): rows 0 and 3
+    // of every record.  A light grid (the reference's regularLightGrid, scene.cpp:5-28): every light a parallelogram
+    // with light 0's edges and one colour at all four of its corners, bit for bit.
+    bool grid = num_lights > 0 && types == (1u << RESTIR_LIGHT_PARALLELOGRAM);
+    for (uint32_t i = 0; grid && i < num_lights; i++) {
+        const float* o = &lt[28 * i];
+        grid = std::memcmp(o + 4, &lt[4], 8 * sizeof(float)) == 0 && std::memcmp(o + 16, o + 12, 3 * sizeof(float)) == 0 &&
+               std::memcmp(o + 20, o + 12, 3 * sizeof(float)) == 0 && std::memcmp(o + 24, o + 12, 3 * sizeof(float)) == 0;
+    }
+    std::vector<float> lc2(8 * std::max<uint32_t>(num_lights, 1), 0.0f);
+    for (uint32_t i = 0; i < num_lights; i++) {
+        std::memcpy(&lc2[8 * i], &lt[28 * i], 16);
+        std::memcpy(&lc2[8 * i + 4], &lt[28 * i + 12], 16);
+    }
+    ST_TRY(c->light_c2.upload(lc2.data(), lc2.size() * 4, c->stream));
     // textures: texels as float4, images back to back; (width, height, first texel, 0) per image
     std::vector<float> texels;
     std::vector<uint32_t> dims;
@@ -926,6 +941,8 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     s.lights = c->lights.as<float4>();
     s.num_lights = num_lights;
     s.light_types = types;
+    s.light_c2 = c->light_c2.as<float4>();
+    s.lights_grid = grid ? 1u : 0u;
     // w = p / (1/L) (light.cpp:80) equals p * L exactly when 1/L is a power of two
     s.light_scale = (num_lights && (num_lights & (num_lights - 1)) == 0) ? (float)num_lights : 0.0f;
     s.lights_finite = 1u;
@@ -2012,6 +2029,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "fuse.primary_ris")) t.fuse_primary_ris = v;
     else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;
     else if (!std::strcmp(key, "ris.queue")) t.ris_queue = v;
+    else if (!std::strcmp(key, "ris.compact")) t.ris_compact = v;
     else if (!std::strcmp(key, "bvh.max_leaf")) t.bvh_max_leaf = v;
     else if (!std::strcmp(key, "final.sort")) t.final_sort = v;
     else if (!std::strcmp(key, "mis.chunk")) t.mis_chunk = v;   // applies from the next ensure_mis

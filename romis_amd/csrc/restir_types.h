@@ -52,6 +52,8 @@ struct SceneDev {
     uint32_t num_lights;
     uint32_t light_types;      // bit t set <=> a light of type t is present
     float light_scale;         // L when 1/L is a power of two (then p / (1/L) == p * L exactly), else 0
+    const float4* light_c2;    // compact table: rows 0 and 3 of every light's record (p0 / position, first colour)
+    uint32_t lights_grid;      // every light a parallelogram with light 0's edges (rows 1, 2) and c0 = c1 = c2 = c3
     uint32_t lights_finite;    // every light coordinate / colour is finite
     uint32_t shade_finite;     // every light colour x material kd / ks product is finite (shade()'s NaN tests)
     uint32_t normals_bounded;  // every vertex normal component finite with |n| <= 2^125: interpolated normals are
@@ -93,6 +95,8 @@ struct Tuning {
     uint32_t ris_blocks = 0;
     uint32_t ris_lds = 1;          // stage the light table in LDS when it fits
     uint32_t ris_queue = 0;        // persistent blocks (this many) pulling tiles from a WorkQueue; 0 = off
+    uint32_t ris_compact = 1;      // N <= 2: compact light tables for point-light-only scenes and light grids (_pt /
+                                   // _grid RIS kernels, kernels.hip ris_light_form)
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
     uint32_t spatial_lds = 3;      // k_spatial1: stage the tile's neighbourhood in LDS (R <= 10): 3 n_t only (default,
                                    // k_spatial1_ntl), 1 n_t + reservoirs, 2 reservoirs only, 0 none (all gathers)

@@ -298,6 +298,44 @@ def test_final_shading_binned_rays(gpu, oracle, name, binned, N):
     assert_bits(gpu.download(_abi.BUF_RGB), want, "rgb")
 
 
+@pytest.mark.parametrize("name,N,compact,lds", [
+    ("nightclub_128pt", 1, 1, 1), ("nightclub_128pt", 2, 1, 1), ("nightclub_128pt", 1, 1, 0), ("nightclub_128pt", 1, 0, 1),
+    ("cornell_1024", 1, 1, 1), ("cornell_1024", 2, 1, 1), ("cornell_1024", 1, 1, 0), ("cornell_1024", 2, 0, 1)])
+def test_ris_compact_light_tables(gpu, oracle, name, N, compact, lds):
+    """ris.compact (default 1): point-light-only scenes (C2) and light grids (C4 / C5: parallelograms sharing their
+    edges, one colour per light) run the _pt / _grid RIS kernels over the compact (row 0, row 3) light table, staged
+    in LDS (ris.lds 1) or read from global memory (0); ris.compact 0: the general kernels on the same scene.  Each
+    bit-exact vs the oracle, through the unfused k_ris (stage_ris) and the fused k_primary_ris of a whole frame."""
+    s = get_scene(name)
+    if name == "cornell_1024":   # the scene must qualify as a light grid, or this would test the general form
+        e = np.array([[*l.p1, *l.p2] for l in s.lights], np.float32)
+        c = np.array([[*l.c0, *l.c1, *l.c2, *l.c3] for l in s.lights], np.float32).reshape(-1, 4, 3)
+        assert (e.view(np.uint32) == e[0].view(np.uint32)).all() and (c.view(np.uint32) == c[:, :1].view(np.uint32)).all()
+    _, osc, cam = setup(gpu, oracle, name, N)
+    n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
+    gpu.upload(_abi.BUF_GBUF_N_T, n_t)
+    gpu.upload(_abi.BUF_GBUF_P_MAT, p_mat)
+    f = _abi.default_features(num_samples_in_reservoir=N)
+    gpu.set_tuning("ris.compact", compact)
+    gpu.set_tuning("ris.lds", lds)
+    try:
+        gpu.stage_ris(cam, f, key(_abi.RESTIR_STAGE_RIS))
+        a, b, d = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
+        assert_bits(gpu.download(_abi.BUF_RES_A), a, "res_a")
+        assert_bits(gpu.download(_abi.BUF_RES_B), b, "res_b")
+        assert_bits(gpu.download(_abi.BUF_RES_DBG), d, "wSum/chosen")
+        fr = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=1, spatial_reuse=1,
+                                   temporal_reuse=0)
+        gpu.set_seed(SEED, 0)
+        rgb, grid = gpu.render_restir(None, cam, W, H, fr)
+        want, res, _ = oracle.render_frame(osc, cam, fr, W, H, SEED, 0)
+        assert_bits(rgb, want, "frame rgb")
+        assert_grid(grid, res, "frame")
+    finally:
+        gpu.set_tuning("ris.compact", 1)
+        gpu.set_tuning("ris.lds", 1)
+
+
 def test_device_math_matches_oracle(gpu, oracle):
     """gl_powf / gl_expf on the GPU == the oracle's glibc restatement (== this image's libm, bit for bit:
     tests/test_oracle_pinning.py) -- the scenes' exponents over 2^20 random bit patterns each, random exponents,

@@ -439,7 +439,11 @@ def main():
         roofline_ris = {"kernel": "k_primary_ris" if rk == "primary_ris" else "k_ris", "bound": "valu",
                         "achieved": round(tf, 2), "peak": FP32_VECTOR_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": round(tf / FP32_VECTOR_PEAK_TFS, 4), "flop_per_candidate": RIS_FLOP_PER_CANDIDATE,
-                        "candidates_per_launch": cand, "avg_launch_us": round(avg_s * 1e6, 2)}
+                        "candidates_per_launch": cand, "avg_launch_us": round(avg_s * 1e6, 2),
+                        "flop_model": "the reference's operations per candidate (SURVEY.md §8d), powf included; the "
+                                      "kernel skips powf exactly where a material has ks = 0 (7 of the 8 Cornell "
+                                      "materials: c1, c4, c5), so there achieved is an algorithmic rate that can "
+                                      "exceed the FP32 peak, not the SIMDs' FLOP rate"}
     # visibility reuse (c5): the spatial pass is ray-bound, so its rate is reported as shadow-ray slots per second --
     # (k + 1) N per pixel, an upper bound on the rays cast (a ray is skipped where p-hat = 0 and the whole Z loop
     # where W = 0) -- next to the final pass's one ray per pixel per sub-reservoir

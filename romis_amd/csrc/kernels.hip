@@ -652,7 +652,12 @@ extern "C" __global__ __launch_bounds__(256) void k_primary_lds(SceneDev s, Regi
 //               corner v0 and colour; the shared edges are read from light 0's record, and the two identical
 //               inner mixes of the colour interpolation are evaluated once.  The same operations on the same
 //               values as the general case.
-constexpr int kLtGeneral = 0, kLtPoint = 1, kLtGrid = 2;
+//   kLtPgram    every light a parallelogram with one colour at all four of its corners, edges free (the reference's
+//               default nightclub set, scene.cpp:30-66: two wall grids): SceneDev::light_c4, rows 0..3 of each record
+//               (v0, edge01, edge02, colour), 4 float4 per light instead of 7.
+constexpr int kLtGeneral = 0, kLtPoint = 1, kLtGrid = 2, kLtPgram = 3;
+// float4s per light of the table form LT
+__host__ __device__ constexpr uint32_t lt_stride(int lt) { return lt == kLtGeneral ? 7u : lt == kLtPgram ? 4u : 2u; }
 template <int NT, int LT = kLtGeneral>
 __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                           const float4* lights, const Bvh& bvh, float4 nt, float4 pm, uint32_t x,
@@ -696,7 +701,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 }
             };
             auto record = [&](uint32_t c) {
-                return lights + (LT == kLtGeneral ? 7u : 2u) * uniform_index(draw(ps, 4u * c), L);
+                return lights + lt_stride(LT) * uniform_index(draw(ps, 4u * c), L);
             };
             // kLtGrid: the shared edges, light 0's rows 1 and 2, read per candidate through the scalar cache (an
             // opaque pointer keeps the compiler from hoisting them into loop-long VGPRs, which spill)
@@ -715,6 +720,13 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                     pos = vadd(vadd(xyz(lt[0]), vscale(shared_row(1), a)), vscale(shared_row(2), b));
                     const v3 gc = xyz(lt[1]);
                     const v3 m = vmix(gc, gc, a);   // = vmix(c0, c1, a) = vmix(c2, c3, a): all four corners are gc
+                    col = vmix(m, m, b);
+                } else if (LT == kLtPgram) {
+                    float a = rand01(draw(ps, 4u * c + 1u));
+                    float b = rand01(draw(ps, 4u * c + 2u));
+                    pos = vadd(vadd(xyz(lt[0]), vscale(xyz(lt[1]), a)), vscale(xyz(lt[2]), b));
+                    const v3 gc = xyz(lt[3]);
+                    const v3 m = vmix(gc, gc, a);
                     col = vmix(m, m, b);
                 } else {
                     sample_rec(c, lt, lt[0], lt[3], pos, col);
@@ -747,12 +759,14 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
 // light fetch is an LDS read instead of a dependent global load.
 // The light table of form LT: the 7-float4 records or the compact (row 0, row 3) table.
 template <int LT>
-__device__ __forceinline__ const float4* global_lights(const SceneDev& s) { return LT == kLtGeneral ? s.lights : s.light_c2; }
+__device__ __forceinline__ const float4* global_lights(const SceneDev& s) {
+    return LT == kLtGeneral ? s.lights : LT == kLtPgram ? s.light_c4 : s.light_c2;
+}
 // Stage it into LDS at dst.  No barrier.
 template <int LT>
 __device__ __forceinline__ void stage_lights(const SceneDev& s, float4* dst) {
     const float4* src = global_lights<LT>(s);
-    const uint32_t n = (LT == kLtGeneral ? 7u : 2u) * s.num_lights;
+    const uint32_t n = lt_stride(LT) * s.num_lights;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
@@ -837,6 +851,10 @@ ROMIS_RIS_KERNEL_LT(1, true, kLtGrid, k_ris_n1_lds_grid, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(2, true, kLtGrid, k_ris_n2_lds_grid, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(1, false, kLtGrid, k_ris_n1_grid, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(2, false, kLtGrid, k_ris_n2_grid, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(1, true, kLtPgram, k_ris_n1_lds_pg, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(2, true, kLtPgram, k_ris_n2_lds_pg, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(1, false, kLtPgram, k_ris_n1_pg, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(2, false, kLtPgram, k_ris_n2_pg, ROMIS_RIS_ATTR)
 
 #define ROMIS_PRIMARY_RIS_KERNEL_LT(NT, LDS, LT, NAME, ATTR)                                                           \
     extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, CameraDev cam, FeaturesDev f,   \
@@ -859,6 +877,10 @@ ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtGrid, k_primary_ris_n1_lds_grid, ROMIS_R
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, true, kLtGrid, k_primary_ris_n2_lds_grid, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtGrid, k_primary_ris_n1_grid, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, false, kLtGrid, k_primary_ris_n2_grid, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtPgram, k_primary_ris_n1_lds_pg, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(2, true, kLtPgram, k_primary_ris_n2_lds_pg, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtPgram, k_primary_ris_n1_pg, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(2, false, kLtPgram, k_primary_ris_n2_pg, ROMIS_RIS_ATTR)
 
 // ---------------------------------------------------------------------------------------------------------
 // Combine state shared by temporal and spatial: out[] (Reservoir(N) of the current pixel) + routed M sums.
@@ -2910,9 +2932,10 @@ inline int ris_light_form(const SceneDev& s, const FeaturesDev& f, const Tuning&
     if (!tu.ris_compact || s.num_lights == 0 || (f.N != 1 && f.N != 2)) return kLtGeneral;
     if (s.light_types == 1u) return kLtPoint;
     if (s.lights_grid) return kLtGrid;
+    if (s.lights_pgram) return kLtPgram;
     return kLtGeneral;
 }
-inline size_t ris_lights_lds_bytes(const SceneDev& s, int lt) { return (size_t)(lt == kLtGeneral ? 7 : 2) * s.num_lights * 16; }
+inline size_t ris_lights_lds_bytes(const SceneDev& s, int lt) { return (size_t)lt_stride(lt) * s.num_lights * 16; }
 inline Region with_map(Region rg, uint32_t map2d) { rg.map2d = map2d; return rg; }
 }  // namespace
 
@@ -2947,6 +2970,7 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f
     auto k = lt == kLtPoint ? (staged ? (f.N == 1 ? k_ris_n1_lds_pt : k_ris_n2_lds_pt) : (f.N == 1 ? k_ris_n1_pt : k_ris_n2_pt))
            : lt == kLtGrid ? (staged ? (f.N == 1 ? k_ris_n1_lds_grid : k_ris_n2_lds_grid)
                                      : (f.N == 1 ? k_ris_n1_grid : k_ris_n2_grid))
+           : lt == kLtPgram ? (staged ? (f.N == 1 ? k_ris_n1_lds_pg : k_ris_n2_lds_pg) : (f.N == 1 ? k_ris_n1_pg : k_ris_n2_pg))
            : staged ? (f.N == 1 ? k_ris_n1_lds : (f.N == 2 ? k_ris_n2_lds : k_ris_n0_lds))
                     : (f.N == 1 ? k_ris_n1 : (f.N == 2 ? k_ris_n2 : k_ris_n0));
     const size_t lds_used = lds;
@@ -2969,6 +2993,8 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
                                           : (f.N == 1 ? k_primary_ris_n1_pt : k_primary_ris_n2_pt))
            : lt == kLtGrid ? (use_lights ? (f.N == 1 ? k_primary_ris_n1_lds_grid : k_primary_ris_n2_lds_grid)
                                          : (f.N == 1 ? k_primary_ris_n1_grid : k_primary_ris_n2_grid))
+           : lt == kLtPgram ? (use_lights ? (f.N == 1 ? k_primary_ris_n1_lds_pg : k_primary_ris_n2_lds_pg)
+                                          : (f.N == 1 ? k_primary_ris_n1_pg : k_primary_ris_n2_pg))
            : use_lights ? (f.N == 1 ? k_primary_ris_n1_lds : (f.N == 2 ? k_primary_ris_n2_lds : k_primary_ris_n0_lds))
                         : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
     ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.ris_blocks), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,

@@ -206,7 +206,7 @@ struct restir_ctx {
     std::mutex mu;
 
     // scene
-    DevBuf nodes, tri_v0, tri_e1, tri_e2, tri_n0, tri_n1, tri_n2, materials, lights, light_c2, tex_texels, tex_dims, tri_uv;
+    DevBuf nodes, tri_v0, tri_e1, tri_e2, tri_n0, tri_n1, tri_n2, materials, lights, light_c2, light_c4, tex_texels, tex_dims, tri_uv;
     SceneDev sdev{};
     bool has_scene = false;
 
@@ -881,12 +881,19 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     // the compact light table of the RIS kernels' point and grid forms (kernels.hip kLtPoint / kLtGrid): rows 0 and 3
     // of every record.  A light grid (the reference's regularLightGrid, scene.cpp:5-28): every light a parallelogram
     // with light 0's edges and one colour at all four of its corners, bit for bit.
-    bool grid = num_lights > 0 && types == (1u << RESTIR_LIGHT_PARALLELOGRAM);
-    for (uint32_t i = 0; grid && i < num_lights; i++) {
+    // Parallelograms with one colour at all four corners (kLtPgram: rows 0..3 of every record) are the
+    // reference's default nightclub set (scene.cpp:30-66); a grid also shares light 0's edges.
+    bool pgram = num_lights > 0 && types == (1u << RESTIR_LIGHT_PARALLELOGRAM);
+    for (uint32_t i = 0; pgram && i < num_lights; i++) {
         const float* o = &lt[28 * i];
-        grid = std::memcmp(o + 4, &lt[4], 8 * sizeof(float)) == 0 && std::memcmp(o + 16, o + 12, 3 * sizeof(float)) == 0 &&
-               std::memcmp(o + 20, o + 12, 3 * sizeof(float)) == 0 && std::memcmp(o + 24, o + 12, 3 * sizeof(float)) == 0;
+        pgram = std::memcmp(o + 16, o + 12, 3 * sizeof(float)) == 0 && std::memcmp(o + 20, o + 12, 3 * sizeof(float)) == 0 &&
+                std::memcmp(o + 24, o + 12, 3 * sizeof(float)) == 0;
     }
+    bool grid = pgram;
+    for (uint32_t i = 0; grid && i < num_lights; i++) grid = std::memcmp(&lt[28 * i + 4], &lt[4], 8 * sizeof(float)) == 0;
+    std::vector<float> lc4(16 * std::max<uint32_t>(pgram ? num_lights : 1u, 1u), 0.0f);
+    for (uint32_t i = 0; pgram && i < num_lights; i++) std::memcpy(&lc4[16 * i], &lt[28 * i], 64);
+    ST_TRY(c->light_c4.upload(lc4.data(), lc4.size() * 4, c->stream));
     std::vector<float> lc2(8 * std::max<uint32_t>(num_lights, 1), 0.0f);
     for (uint32_t i = 0; i < num_lights; i++) {
         std::memcpy(&lc2[8 * i], &lt[28 * i], 16);
@@ -943,6 +950,8 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     s.light_types = types;
     s.light_c2 = c->light_c2.as<float4>();
     s.lights_grid = grid ? 1u : 0u;
+    s.light_c4 = c->light_c4.as<float4>();
+    s.lights_pgram = pgram ? 1u : 0u;
     // w = p / (1/L) (light.cpp:80) equals p * L exactly when 1/L is a power of two
     s.light_scale = (num_lights && (num_lights & (num_lights - 1)) == 0) ? (float)num_lights : 0.0f;
     s.lights_finite = 1u;

@@ -54,6 +54,8 @@ struct SceneDev {
     float light_scale;         // L when 1/L is a power of two (then p / (1/L) == p * L exactly), else 0
     const float4* light_c2;    // compact table: rows 0 and 3 of every light's record (p0 / position, first colour)
     uint32_t lights_grid;      // every light a parallelogram with light 0's edges (rows 1, 2) and c0 = c1 = c2 = c3
+    const float4* light_c4;    // rows 0..3 of every light's record (v0, edge01, edge02, c0): the kLtPgram table
+    uint32_t lights_pgram;     // every light a parallelogram with c0 = c1 = c2 = c3
     uint32_t lights_finite;    // every light coordinate / colour is finite
     uint32_t shade_finite;     // every light colour x material kd / ks product is finite (shade()'s NaN tests)
     uint32_t normals_bounded;  // every vertex normal component finite with |n| <= 2^125: interpolated normals are

@@ -26,11 +26,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2", choices=list(bench.CONFIGS))
     ap.add_argument("--N", type=int, default=1)
+    ap.add_argument("--scene", default=None, help="another bench scene under the config's settings")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--frames", type=int, default=5)
     ap.add_argument("--variants", nargs="+", default=["default:"])
     args = ap.parse_args()
-    cf = bench.CONFIGS[args.config]
+    cf = dict(bench.CONFIGS[args.config])
+    if args.scene:
+        cf["scene"] = args.scene
     W, H = cf.get("image") or cf["tile"]
     passes = cf["passes"]
     f = _abi.default_features(initial_light_samples=cf["M"], num_samples_in_reservoir=args.N, spatial_resampling_passes=passes,
@@ -66,7 +69,7 @@ def main():
                 if n:
                     samples[name].setdefault(k, []).append(ms / n * 1e3)
     out = {name: {k: round(statistics.median(v), 2) for k, v in ks.items()} for name, ks in samples.items()}
-    print(json.dumps({"config": args.config, "N": args.N, "us_per_launch": out}))
+    print(json.dumps({"config": args.config, "scene": cf["scene"], "N": args.N, "us_per_launch": out}))
     r.close()
 
 

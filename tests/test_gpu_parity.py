@@ -300,10 +300,12 @@ def test_final_shading_binned_rays(gpu, oracle, name, binned, N):
 
 @pytest.mark.parametrize("name,N,compact,lds", [
     ("nightclub_128pt", 1, 1, 1), ("nightclub_128pt", 2, 1, 1), ("nightclub_128pt", 1, 1, 0), ("nightclub_128pt", 1, 0, 1),
-    ("cornell_1024", 1, 1, 1), ("cornell_1024", 2, 1, 1), ("cornell_1024", 1, 1, 0), ("cornell_1024", 2, 0, 1)])
+    ("cornell_1024", 1, 1, 1), ("cornell_1024", 2, 1, 1), ("cornell_1024", 1, 1, 0), ("cornell_1024", 2, 0, 1),
+    ("nightclub_512", 1, 1, 1), ("nightclub_512", 2, 1, 1), ("nightclub_512", 2, 1, 0), ("nightclub_512", 2, 0, 1)])
 def test_ris_compact_light_tables(gpu, oracle, name, N, compact, lds):
-    """ris.compact (default 1): point-light-only scenes (C2) and light grids (C4 / C5: parallelograms sharing their
-    edges, one colour per light) run the _pt / _grid RIS kernels over the compact (row 0, row 3) light table, staged
+    """ris.compact (default 1): point-light-only scenes (C2), light grids (C4 / C5: parallelograms sharing their
+    edges, one colour per light) and one-colour parallelograms (the reference's 512-light nightclub) run the _pt /
+    _grid / _pg RIS kernels over the compact light tables, staged
     in LDS (ris.lds 1) or read from global memory (0); ris.compact 0: the general kernels on the same scene.  Each
     bit-exact vs the oracle, through the unfused k_ris (stage_ris) and the fused k_primary_ris of a whole frame."""
     s = get_scene(name)
@@ -311,6 +313,10 @@ def test_ris_compact_light_tables(gpu, oracle, name, N, compact, lds):
         e = np.array([[*l.p1, *l.p2] for l in s.lights], np.float32)
         c = np.array([[*l.c0, *l.c1, *l.c2, *l.c3] for l in s.lights], np.float32).reshape(-1, 4, 3)
         assert (e.view(np.uint32) == e[0].view(np.uint32)).all() and (c.view(np.uint32) == c[:, :1].view(np.uint32)).all()
+    if name == "nightclub_512":   # one colour per light, edges not shared: the kLtPgram form
+        e = np.array([[*l.p1, *l.p2] for l in s.lights], np.float32)
+        c = np.array([[*l.c0, *l.c1, *l.c2, *l.c3] for l in s.lights], np.float32).reshape(-1, 4, 3)
+        assert (c.view(np.uint32) == c[:, :1].view(np.uint32)).all() and not (e.view(np.uint32) == e[0].view(np.uint32)).all()
     _, osc, cam = setup(gpu, oracle, name, N)
     n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
     gpu.upload(_abi.BUF_GBUF_N_T, n_t)

@@ -446,7 +446,9 @@ restir_status restir_enable_timing(restir_ctx* ctx, int enable);
  * "final.blocks|lds|2d", "fuse.primary_ris" (restir_render runs primary rays + RIS as one kernel, default 1).  *.blocks = persistent grid cap (0 = one block per work item).  "timing.mask": the
  * kernels (bit 1 << RESTIR_K_*) restir_enable_timing brackets with HIP events (default all).  "bvh.max_leaf":
  * triangles per BVH leaf for the next restir_set_scene (default 2).  "layout.records": restir_render's buffers as
- * per-pixel records [n_t, res_a, res_b] (1) or SoA planes (0, default). */
+ * per-pixel records [n_t, res_a, res_b] (1) or SoA planes (0, default).  "ris.compact": initial RIS (N = 1, 2) reads
+ * a compact light table when the scene allows one -- point lights only, a light grid, one-colour parallelograms --
+ * instead of the 7-float4 records (default 1; restir_set_scene detects the form bit for bit). */
 restir_status restir_set_tuning(restir_ctx* ctx, const char* key, int value);
 restir_status restir_timings(restir_ctx* ctx, double* ms /*[RESTIR_K_COUNT]*/, uint64_t* launches /*[RESTIR_K_COUNT]*/);
 restir_status restir_reset_timings(restir_ctx* ctx);

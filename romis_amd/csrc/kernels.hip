@@ -327,12 +327,18 @@ __device__ __forceinline__ float material_pow(const GlTabs& tb, float x, const P
 struct ShadePre {
     float d, dotNL, cosTheta;
 };
+#ifndef ROMIS_SKIP_COS
+#define ROMIS_SKIP_COS 1
+#endif
 __device__ __forceinline__ ShadePre shade_pre(const Px& px, v3 lpos) {
     ShadePre r;
     v3 L = vnormalize_len(vsub(lpos, px.P), r.d);   // d = glm::distance(hitPos, lightPos), the length normalize() takes
     r.dotNL = vdot(px.N, L);
     r.cosTheta = 0.0f;
     if (r.dotNL < 0.0f) return r;
+    // ks = 0 (ROMIS_POW_SKIP): the power, and so R and cosTheta, never reach the result (pow_pre returns 1 for any
+    // argument) -- skipped, ROMIS_SKIP_COS (7 of the 8 Cornell materials)
+    if (ROMIS_SKIP_COS && __float_as_uint(px.ks_pm.w) == ROMIS_POW_SKIP) return r;
     v3 R = vnormalize(vsub(vscale(px.N, 2.0f * r.dotNL), L));
     r.cosTheta = vdot(R, px.V);
     return r;

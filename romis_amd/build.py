@@ -42,11 +42,12 @@ HEADERS = ["device_math.h", "restir_types.h", "launch.h", "bvh.h", "pow10_table.
 
 
 def source_hash() -> str:
-    """sha256 over the device sources and flags: identifies the kernels a profile was measured on (bench.py
-    reports a committed PMC traffic figure only when it matches)."""
+    """sha256 over the device sources, the launcher (restir.cpp decides which buffers a pass reads and writes) and
+    the flags: identifies the kernels a profile was measured on (bench.py reports a committed PMC traffic figure
+    only when it matches)."""
     import hashlib
     h = hashlib.sha256()
-    for f in [SOURCES[0][0]] + HEADERS:
+    for f in [SOURCES[0][0], SOURCES[1][0]] + HEADERS:
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(f.encode() + b"\0" + fh.read())
     h.update(" ".join([c for c in COMMON + DEVICE + KERNEL_FLAGS if not c.startswith("-I")]).encode())   # flags, not paths

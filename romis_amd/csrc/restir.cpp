@@ -1157,7 +1157,9 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
         TIMED(c, RESTIR_K_SPATIAL,
               launch_spatial(s, pr, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_SPATIAL, pass), camd.origin, fb.nt(cur), pm,
                              fb.ra(cur), fb.rb(cur), fb.ra(nxt), fb.rb(nxt), nullptr, rp_ok ? fb.rp(cur) : nullptr,
-                             fb.rp(nxt), &rp_ok, c->tuning, c->stream));
+                             // the last pass's pdf cache has no reader (final shading re-shades; the next frame's
+                             // temporal pass evaluates its own): not written
+                             pass + 1 < passes ? fb.rp(nxt) : nullptr, &rp_ok, c->tuning, c->stream));
         cur = nxt;
     }
     TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), c->rgb.as<float>(),

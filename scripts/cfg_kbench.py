@@ -53,6 +53,8 @@ def main():
         for name, knobs in variants.items():
             for k in keys:   # every knob any variant sets: this variant's value or the default
                 r.set_tuning(k, knobs.get(k, DEFAULTS[k]))
+            if any(k.startswith("bvh.") for k in keys):   # BVH knobs apply at the next set_scene
+                r.set_scene(scene.bench_scene(cf["scene"]))
             r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
             rgb, _ = r.render_restir(None, cam, W, H, f, want_grid=False)
             if ref is None:

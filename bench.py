@@ -142,6 +142,25 @@ def committed_traffic(cfg):
     return None, None
 
 
+def committed_valu(cfg_name, n_sub, kernel):
+    """VALU wave-instructions per candidate of the RIS kernel from profiles/valu.json (scripts/valu_json.py: an SQ
+    counter pass over this bench), only when it was measured on these exact sources and this config."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "valu.json")
+    try:
+        from romis_amd import build
+        with open(path) as fh:
+            rec = json.load(fh)
+        if rec.get("source_hash") != build.source_hash() or rec.get("config") != cfg_name or rec.get("N") != n_sub:
+            return None
+        for k, e in rec.get("kernels", {}).items():
+            if k.startswith(kernel) and "valu_instr_per_candidate" in e:
+                return {"valu_instr_per_candidate": e["valu_instr_per_candidate"], "sq_insts_valu_per_launch": e["sq_insts_valu"],
+                        "kernel_variant": k, "source": rec.get("profile")}
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
 def pmc_traffic(path, kernel_prefix="k_spatial"):
     """Per-launch HBM bytes of the spatial kernel from a rocprofv3 --pmc CSV (counter_collection.csv).
     FETCH_SIZE / WRITE_SIZE are KB; FETCH_SIZE is doubled for wide coalesced streams on gfx950
@@ -444,6 +463,9 @@ def main():
                                       "kernel skips powf exactly where a material has ks = 0 (7 of the 8 Cornell "
                                       "materials: c1, c4, c5), so there achieved is an algorithmic rate that can "
                                       "exceed the FP32 peak, not the SIMDs' FLOP rate"}
+        valu = committed_valu(args.config, cfg["N"], roofline_ris["kernel"])
+        if valu:   # measured issue: VALU wave-instructions per candidate (SQ_INSTS_VALU / (pixels x M / 64))
+            roofline_ris.update(valu)
     # visibility reuse (c5): the spatial pass is ray-bound, so its rate is reported as shadow-ray slots per second --
     # (k + 1) N per pixel, an upper bound on the rays cast (a ray is skipped where p-hat = 0 and the whole Z loop
     # where W = 0) -- next to the final pass's one ray per pixel per sub-reservoir

@@ -373,24 +373,8 @@ __device__ __forceinline__ v3 shade(const SceneDev& s, const FeaturesDev& f, con
 }
 
 // target pdf = glm::length(computeShading(...)) (light.cpp:84, reservoir.cpp:49)
-// ks = 0 (ROMIS_POW_SKIP): after the reference's NaN clean-up the specular term is a +-0 vector whatever pow
-// returns, so diffuse + specular differs from diffuse at most in the sign of a zero component, which the length
-// squares away -- the target pdf is the diffuse term's length alone (ROMIS_PDF_DIFFUSE_ONLY; shade() keeps the sum:
-// final shading's colour carries those signs).
-#ifndef ROMIS_PDF_DIFFUSE_ONLY
-#define ROMIS_PDF_DIFFUSE_ONLY 1
-#endif
 __device__ __forceinline__ float target_pdf(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,
                                             const GlTabs& tb = gl_global_tabs()) {
-    if (ROMIS_PDF_DIFFUSE_ONLY && f.shading && __float_as_uint(px.ks_pm.w) == ROMIS_POW_SKIP) {
-        const ShadePre sp = shade_pre(px, lpos);   // returns before R / cosTheta for this mode
-        if (sp.dotNL < 0.0f) return 0.0f;          // length(vec3(0))
-        v3 diffuse = vscale(vmul(lcol, xyz(px.kd_sh)), sp.dotNL);
-        if (!(s.shade_finite && __builtin_isfinite(sp.dotNL)) && vany_nan(diffuse)) diffuse = mk(0.0f, 0.0f, 0.0f);
-        float d = sp.d;
-        if (fabsf(d) < 1e-5f) d = 1.0f;
-        return vlength(vdivs(diffuse, d * d));
-    }
     return vlength(shade_ref(s, f, px, lpos, lcol, tb));
 }
 

@@ -46,10 +46,12 @@
 extern "C" {
 #endif
 
-#define RESTIR_ABI_VERSION 4   /* 2: restir_features gained the R-MIS / R-OMIS fields;
+#define RESTIR_ABI_VERSION 5   /* 2: restir_features gained the R-MIS / R-OMIS fields;
                                   3: textures (restir_texture, restir_material.kd_texture, restir_mesh.texcoords);
                                   4: halo passes split into interior / border, native RCCL halo transport,
-                                     frame output (8-bit BMP, Features JSON record) */
+                                     frame output (8-bit BMP, Features JSON record);
+                                  5: the native transport's operation list (restir_halo_ops) and its record-only
+                                     mode (restir_halo_record / restir_halo_log) */
 
 #define RESTIR_STAGE_RIS      1u
 #define RESTIR_STAGE_TEMPORAL 2u
@@ -400,6 +402,47 @@ restir_status restir_rccl_unique_id(void* out, size_t bytes);
 restir_status restir_halo_attach_rccl(restir_ctx* ctx, const void* unique_id, uint32_t nranks, uint32_t rank);
 restir_status restir_halo_attach_comm(restir_ctx* ctx, void* nccl_comm);
 restir_status restir_halo_pass(restir_ctx* ctx);
+
+/* The point-to-point operations restir_halo_pass posts for every spatial pass, in posting order: one ncclSend
+ * then one ncclRecv per restir_halo_plan segment, all inside one ncclGroupStart / ncclGroupEnd on the
+ * communication stream.  Each: kind, peer (tile rank), byte offset into the pass's device send / receive buffer,
+ * bytes, and the global pixel rectangle the bytes hold ([sub-reservoir][pixel row-major][res_a, res_b]).  Pure
+ * host: restir_halo_begin builds the list restir_halo_pass posts from with this same function.  *count: in =
+ * capacity (2 per segment; 16 suffices), out = operations. */
+#define RESTIR_HALO_OP_SEND 0u
+#define RESTIR_HALO_OP_RECV 1u
+typedef struct restir_halo_op {
+    uint32_t kind, peer;
+    uint64_t offset, bytes;
+    uint32_t x0, y0, width, height;          /* global pixel rectangle */
+} restir_halo_op;
+restir_status restir_halo_ops(uint32_t global_width, uint32_t global_height, uint32_t tiles_x, uint32_t tiles_y,
+                              uint32_t rank, uint32_t radius, uint32_t N, restir_halo_op* ops, uint32_t* count);
+
+/* Record-only mode of restir_halo_pass: the native transport's plumbing checked without a second GPU.  With
+ * restir_halo_record(ctx, 1) a pass needs no communicator and posts no RCCL operation; it appends every step it
+ * issues to the context's log instead -- on the context stream (0) the pack launch and the `packed` event, on the
+ * communication stream (1) the wait for it, the group with each send / receive (peer, offset, bytes), the `moved`
+ * event, then on the context stream the interior launch, the wait for `moved`, the unpack and the border launches
+ * -- and otherwise runs the pass with a zeroed receive buffer (the border strips then read zero reservoirs: not a
+ * valid image).  restir_halo_log copies the log out in issue order and clears it; *count: in = capacity, out =
+ * entries (RESTIR_ERR_INVALID, nothing cleared, when the capacity is short: *count = entries needed). */
+#define RESTIR_HALO_EV_PACK         0u
+#define RESTIR_HALO_EV_RECORD       1u   /* peer: 0 = `packed`, 1 = `moved` */
+#define RESTIR_HALO_EV_WAIT         2u   /* peer: the event waited for, as above */
+#define RESTIR_HALO_EV_GROUP_START  3u
+#define RESTIR_HALO_EV_SEND         4u
+#define RESTIR_HALO_EV_RECV         5u
+#define RESTIR_HALO_EV_GROUP_END    6u
+#define RESTIR_HALO_EV_INTERIOR     7u
+#define RESTIR_HALO_EV_UNPACK       8u
+#define RESTIR_HALO_EV_BORDER       9u
+typedef struct restir_halo_event {
+    uint32_t what, stream, peer, pass;
+    uint64_t offset, bytes;
+} restir_halo_event;
+restir_status restir_halo_record(restir_ctx* ctx, int on);
+restir_status restir_halo_log(restir_ctx* ctx, restir_halo_event* out, uint32_t* count);
 
 /* ---- frame output (pure host, no device needed) --------------------------------------------------------
  * restir_rgb_to_rgba8: Screen::writeBitmapToFile's conversion (screen.cpp:45-51): glm::clamp(c, 0, 1), then

@@ -205,11 +205,14 @@ public:
     // RENDERS_DIR for the file side outputs the library writes itself (R-OMIS alpha visualisation); empty = none
     void setRendersDir(const std::filesystem::path& dir) {
         check(restir_set_renders_dir(ctx_, dir.empty() ? nullptr : dir.c_str()), "restir_set_renders_dir");
+        rendersDir_ = dir;
     }
+    const std::filesystem::path& rendersDir() const { return rendersDir_; }
     restir_ctx* handle() const { return ctx_; }
 
 private:
     restir_ctx* ctx_ = nullptr;
+    std::filesystem::path rendersDir_;
 };
 
 // Contexts for callers that render concurrently: the reference's CLI renders one std::thread per camera through
@@ -266,13 +269,27 @@ inline void renderMIS(Renderer& r, const Camera& camera, Screen& screen, const F
 // R-MIS / R-OMIS.  Like the reference, every render then saves its configuration record to
 // <rendersDir>/<currentTime()>.json (render.cpp:281-287, saveFeaturesRecord), and R-OMIS with
 // saveAlphasVisualisation writes its alpha bitmaps to <rendersDir>/<currentTime()>/ after every iteration; the
-// reference's RENDERS_DIR is a build-time constant, here the caller passes it -- an empty path skips both.
+// reference's RENDERS_DIR is a build-time constant, here the caller passes it.  A non-empty rendersDir applies to
+// this render only (the Renderer's own setRendersDir is restored afterwards); an empty one writes no record and
+// leaves the alpha bitmaps to whatever the Renderer was given with setRendersDir.
 inline std::shared_ptr<ReservoirGrid> renderRayTraced(Renderer& r, const std::shared_ptr<ReservoirGrid>& prev,
                                                       const Camera& camera, Screen& screen, const Features& features,
                                                       const std::filesystem::path& rendersDir = {},
                                                       const restir_features_record_extra* extra = nullptr) {
     std::shared_ptr<ReservoirGrid> next;
-    r.setRendersDir(rendersDir);   // R-OMIS's per-iteration alpha visualisation (render.cpp:227-229)
+    // R-OMIS's per-iteration alpha visualisation (render.cpp:227-229) goes to rendersDir for this call
+    struct DirScope {
+        Renderer& r;
+        std::filesystem::path saved;
+        bool set;
+        DirScope(Renderer& rr, const std::filesystem::path& d) : r(rr), saved(rr.rendersDir()), set(!d.empty()) {
+            if (set) r.setRendersDir(d);
+        }
+        ~DirScope() {
+            if (!set) return;
+            try { r.setRendersDir(saved); } catch (...) {}   // never throws from a destructor
+        }
+    } scope(r, rendersDir);
     switch (features.ray_trace_mode) {
         case RESTIR_MODE_RESTIR: next = renderReSTIR(r, prev, camera, screen, features); break;
         case RESTIR_MODE_RMIS:

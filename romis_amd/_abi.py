@@ -19,6 +19,12 @@ RESTIR_DEFAULT_SEED = 0x5EED0001
 RESTIR_MAX_N = 32
 RESTIR_ROMIS_MAX_TECHNIQUES = 8
 RESTIR_RCCL_ID_BYTES = 128
+RESTIR_ABI_VERSION = 5
+RESTIR_HALO_OP_SEND, RESTIR_HALO_OP_RECV = 0, 1
+# restir_halo_event.what (include/restir_c.h)
+(RESTIR_HALO_EV_PACK, RESTIR_HALO_EV_RECORD, RESTIR_HALO_EV_WAIT, RESTIR_HALO_EV_GROUP_START, RESTIR_HALO_EV_SEND,
+ RESTIR_HALO_EV_RECV, RESTIR_HALO_EV_GROUP_END, RESTIR_HALO_EV_INTERIOR, RESTIR_HALO_EV_UNPACK,
+ RESTIR_HALO_EV_BORDER) = range(10)
 
 LIGHT_POINT, LIGHT_SEGMENT, LIGHT_PARALLELOGRAM = 0, 1, 2
 MODE_RESTIR, MODE_RMIS, MODE_ROMIS = 0, 1, 2
@@ -97,12 +103,23 @@ class HaloSegment(C.Structure):
                 ("height", C.c_uint32), ("offset", C.c_uint64), ("bytes", C.c_uint64)]
 
 
+class HaloOp(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("peer", C.c_uint32), ("offset", C.c_uint64), ("bytes", C.c_uint64),
+                ("x0", C.c_uint32), ("y0", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32)]
+
+
+class HaloEvent(C.Structure):
+    _fields_ = [("what", C.c_uint32), ("stream", C.c_uint32), ("peer", C.c_uint32), ("pass_", C.c_uint32),
+                ("offset", C.c_uint64), ("bytes", C.c_uint64)]
+
+
 class Tile(C.Structure):
     _fields_ = [("global_width", C.c_uint32), ("global_height", C.c_uint32),
                 ("x0", C.c_uint32), ("y0", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32),
                 ("gx0", C.c_uint32), ("gy0", C.c_uint32), ("gwidth", C.c_uint32), ("gheight", C.c_uint32)]
 
 
+assert C.sizeof(HaloOp) == 40 and C.sizeof(HaloEvent) == 32
 assert C.sizeof(Light) == 88
 assert C.sizeof(Material) == 36
 assert C.sizeof(Mesh) == 80 and C.sizeof(Texture) == 16
@@ -185,6 +202,10 @@ SIGNATURES = {
     "restir_halo_attach_rccl": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32]),
     "restir_halo_attach_comm": (C.c_int, [_P, _P]),
     "restir_halo_pass": (C.c_int, [_P]),
+    "restir_halo_ops": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                  C.POINTER(HaloOp), C.POINTER(C.c_uint32)]),
+    "restir_halo_record": (C.c_int, [_P, C.c_int]),
+    "restir_halo_log": (C.c_int, [_P, C.POINTER(HaloEvent), C.POINTER(C.c_uint32)]),
     "restir_rgb_to_rgba8": (C.c_int, [_P, C.c_size_t, _P]),
     "restir_encode_bmp": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "restir_write_bmp": (C.c_int, [C.c_char_p, _P, C.c_uint32, C.c_uint32]),

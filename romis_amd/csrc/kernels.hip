@@ -1864,8 +1864,10 @@ ROMIS_SPATIAL1_KERNEL(true, k_spatial1_dbg)
 //    the whole Z loop (K + 1 target pdfs at the inputs' pixels and their shadow rays) is skipped exactly then;
 //  - Z's own-pixel term is p-hat(pixel, held sample) = the value W uses (the same evaluation), and the term of the
 //    input the held sample came from is that input's p-hat of its own sample at its own pixel = the producer's pdf
-//    cache there (rp_in[q], the same evaluation on the same G-buffer record): one target pdf each instead of a
-//    recomputation;
+//    cache there (rp_nb[q], the same evaluation on the same G-buffer record): one target pdf each instead of a
+//    recomputation.  rp_nb is the cache as seen at neighbour pixels: the caller passes null when a neighbour may lie
+//    where the producer did not write it (a halo pass's border strips read the exchanged ring, whose reservoirs
+//    arrive without their pdfs), and the term is then evaluated;
 //  - the shadow rays (VIS) traverse the block's LDS copy of the BVH.
 // Only SoA planes (Region ps = 1) and K <= kLeanK take this path (launch_spatial checks).
 template <bool DBG, bool VIS>
@@ -1873,7 +1875,8 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
                                                v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                                const float4* __restrict__ ia, const float4* __restrict__ ib,
                                                float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
-                                               const float* __restrict__ rp_in, float* __restrict__ rp_out) {
+                                               const float* __restrict__ rp_in, const float* __restrict__ rp_nb,
+                                               float* __restrict__ rp_out) {
     const Bvh bvh = VIS ? stage_bvh(s, g_lds) : global_bvh(s);   // ends with a barrier (every thread gets here)
     const GlTabs tb = gl_stage_tables();
     uint32_t tile;
@@ -1937,7 +1940,7 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
             if (n < K) {
                 const float4 qn = ld_at(n_t, qo[n]), qp = ld_at(p_mat, qo[n]);
                 const Px rp = make_px(s, qn, qp, origin, qo[n] >> 4);
-                const float pd = (src == n && rp_in) ? ld_at(rp_in, qo[n] >> 2) : target_pdf(s, f, rp, cmb.pos, cmb.col, tb);
+                const float pd = (src == n && rp_nb) ? ld_at(rp_nb, qo[n] >> 2) : target_pdf(s, f, rp, cmb.pos, cmb.col, tb);
                 if (pd > 0.0f && (!VIS || visible(bvh, rp.P, cmb.pos))) Z += Mn[n];
             }
         }
@@ -1956,8 +1959,9 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
                                                                            const float4* n_t, const float4* p_mat,      \
                                                                            const float4* ia, const float4* ib,          \
                                                                            float4* oa, float4* ob, float2* odbg,        \
-                                                                           const float* rp_in, float* rp_out) {         \
-        spatial1u_body<DBG, VIS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);      \
+                                                                           const float* rp_in, const float* rp_nb,      \
+                                                                           float* rp_out) {                             \
+        spatial1u_body<DBG, VIS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_nb, rp_out); \
     }
 ROMIS_SPATIAL1U_KERNEL(false, false, k_spatial1u)
 ROMIS_SPATIAL1U_KERNEL(true, false, k_spatial1u_dbg)
@@ -3025,8 +3029,8 @@ hipError_t launch_temporal(const SceneDev& s, const Region& rg0, const FeaturesD
 
 hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
                           const float4* n_t, const float4* p_mat, const float4* ia, const float4* ib, float4* oa,
-                          float4* ob, float2* odbg, const float* rp_in, float* rp_out, bool* rp_written,
-                          const Tuning& tu, hipStream_t stream) {
+                          float4* ob, float2* odbg, const float* rp_in, const float* rp_nb, float* rp_out,
+                          bool* rp_written, const Tuning& tu, hipStream_t stream) {
     if (rp_written) *rp_written = false;
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     Region rg = with_map(rg0, tu.spatial_xcd);   // XCD-banded order works on 2D tiles
@@ -3046,12 +3050,13 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         if (rg.xcd_rows) grid = 8u * ((((nty + rg.xcd_rows - 1) / rg.xcd_rows) + 7u) / 8u) * rg.xcd_rows * ntx;
         auto k = f.spatial_vis ? (odbg ? k_spatial1u_vis_dbg : k_spatial1u_vis) : (odbg ? k_spatial1u_dbg : k_spatial1u);
         ROMIS_LAUNCH(k, dim3(grid), dim3(kBlock), f.spatial_vis ? bvh_bytes : 0, stream, s, rg, f, key, o[0], o[1], o[2],
-                     n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
+                     n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_in ? rp_nb : nullptr, rp_out);
         if (rp_written) *rp_written = rp_out != nullptr;
         return hipGetLastError();
     }
-    if (lean2 && !f.unbiased && f.R <= kLdsSpatialR) {
-        // N = 2 biased: one block per tile in the XCD chunk order (xcd_tile)
+    if (lean2 && !f.unbiased && f.R <= kLdsSpatialR && tu.spatial_lds == 3u) {
+        // N = 2 biased: one block per tile in the XCD chunk order (xcd_tile); spatial.lds != 3 selects the general
+        // kernel for A/B runs, as for N = 1.  No pdf cache at N = 2 (*rp_written stays false)
         const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
         rg.xcd_rows = tu.spatial_xcd_rows == kXcdRowsAuto ? std::max(1u, std::min(8u, 8192u / std::max(rg.rw, 1u)))
                                                           : tu.spatial_xcd_rows;

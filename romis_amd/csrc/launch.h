@@ -25,8 +25,8 @@ hipError_t launch_temporal(const SceneDev& s, const Region& rg, const FeaturesDe
                            const float* rp_in, float* rp_out, const Tuning& tu, hipStream_t stream);
 hipError_t launch_spatial(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
                           const float4* n_t, const float4* p_mat, const float4* ia, const float4* ib, float4* oa,
-                          float4* ob, float2* odbg, const float* rp_in, float* rp_out, bool* rp_written,
-                          const Tuning& tu, hipStream_t stream);
+                          float4* ob, float2* odbg, const float* rp_in, const float* rp_nb, float* rp_out,
+                          bool* rp_written, const Tuning& tu, hipStream_t stream);
 hipError_t launch_final(const SceneDev& s, const Region& rg, const FeaturesDev& f, const float* origin,
                         const float4* n_t, const float4* p_mat, const float4* ra, const float4* rb, float* rgb,
                         const Tuning& tu, hipStream_t stream);

@@ -239,6 +239,8 @@ struct restir_ctx {
         HaloSegs send{}, recv{};
         uint64_t send_bytes = 0, recv_bytes = 0;
         uint32_t send_rank[RESTIR_MAX_HALO_SEGS] = {}, recv_rank[RESTIR_MAX_HALO_SEGS] = {};
+        restir_halo_op ops[2 * RESTIR_MAX_HALO_SEGS] = {};   // what restir_halo_pass posts (restir_halo_ops)
+        uint32_t nops = 0;
         uint32_t rank = 0, nranks = 0;   // this frame's tile (rank) of tiles_x * tiles_y
         int cur = 0;
         bool fb_records = true;
@@ -247,6 +249,9 @@ struct restir_ctx {
         bool part_rp = false;        // every launch of the current pass wrote the pdf cache
     } halo;
     DevBuf halo_scratch;
+    // record-only restir_halo_pass (restir_halo_record): the steps it issues, no RCCL call
+    bool halo_record = false;
+    std::vector<restir_halo_event> halo_log;
     // native RCCL halo transport (restir_halo_attach_rccl / _comm, restir_halo_pass)
     struct {
         void* comm = nullptr;            // ncclComm_t
@@ -419,6 +424,42 @@ restir_status restir_halo_plan(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_
     return RESTIR_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// The operations restir_halo_pass posts, from a plan: send i then recv i per segment (restir_halo_ops)
+void halo_ops_from(const restir_halo_segment* send, const restir_halo_segment* recv, uint32_t n, restir_halo_op* ops) {
+    auto op = [](uint32_t kind, const restir_halo_segment& g) {
+        restir_halo_op o{};
+        o.kind = kind; o.peer = g.rank; o.offset = g.offset; o.bytes = g.bytes;
+        o.x0 = g.x0; o.y0 = g.y0; o.width = g.width; o.height = g.height;
+        return o;
+    };
+    for (uint32_t i = 0; i < n; i++) {
+        ops[2 * i] = op(RESTIR_HALO_OP_SEND, send[i]);
+        ops[2 * i + 1] = op(RESTIR_HALO_OP_RECV, recv[i]);
+    }
+}
+}  // namespace
+
+extern "C" {
+
+restir_status restir_halo_ops(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t tiles_y, uint32_t rank, uint32_t radius,
+                              uint32_t N, restir_halo_op* ops, uint32_t* count) {
+    if (!count || !ops) return fail(RESTIR_ERR_INVALID, "restir_halo_ops: null argument");
+    restir_halo_segment sg[RESTIR_MAX_HALO_SEGS], rg_[RESTIR_MAX_HALO_SEGS];
+    uint32_t n = RESTIR_MAX_HALO_SEGS;
+    ST_TRY(restir_halo_plan(W, H, tiles_x, tiles_y, rank, radius, N, sg, rg_, &n));
+    if (*count < 2 * n) {
+        const uint32_t need = 2 * n;
+        *count = need;
+        return fail(RESTIR_ERR_INVALID, "restir_halo_ops: capacity for %u operations needed", need);
+    }
+    halo_ops_from(sg, rg_, n, ops);
+    *count = 2 * n;
+    return RESTIR_OK;
+}
+
 restir_status restir_device_count(int* out) {
     if (!out) return fail(RESTIR_ERR_INVALID, "restir_device_count: null");
     int n = 0;
@@ -553,6 +594,13 @@ restir_status ensure_work(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N, b
     return RESTIR_OK;
 }
 
+// A timing event: read only by hipEventElapsedTime after hipStreamSynchronize (collect_timings), so it needs no
+// system-scope release of its own -- with one, the timed kernel's completion waits for a cache writeback that
+// showed as 6.7 us before and 4.6 us after the C2 spatial pass (profiles/r4/gap).
+hipError_t timing_event_create(const restir_ctx* c, hipEvent_t* e) {
+    return c->tuning.timing_fence ? hipEventCreate(e) : hipEventCreateWithFlags(e, hipEventDisableSystemFence);
+}
+
 restir_status timed_begin(restir_ctx* c, int kernel, Pending& p) {
     p.kernel = kernel;
     p.start = p.stop = nullptr;
@@ -560,7 +608,7 @@ restir_status timed_begin(restir_ctx* c, int kernel, Pending& p) {
     if (!c->timing || !((c->tuning.timing_mask >> kernel) & 1u)) return RESTIR_OK;
     for (hipEvent_t* e : {&p.start, &p.stop}) {
         if (!c->free_events.empty()) { *e = c->free_events.back(); c->free_events.pop_back(); }
-        else HIP_TRY(hipEventCreate(e));
+        else HIP_TRY(timing_event_create(c, e));
     }
     set_launch_events(p.start, p.stop);   // recorded by the launch itself (hipExtLaunchKernelGGL)
     return RESTIR_OK;
@@ -1157,6 +1205,9 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
         TIMED(c, RESTIR_K_SPATIAL,
               launch_spatial(s, pr, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_SPATIAL, pass), camd.origin, fb.nt(cur), pm,
                              fb.ra(cur), fb.rb(cur), fb.ra(nxt), fb.rb(nxt), nullptr, rp_ok ? fb.rp(cur) : nullptr,
+                             // every neighbour of this pass lies in the region the cache's producer covered (RIS /
+                             // temporal: the whole view; pass p - 1: the owned rect grown by (P - p) R)
+                             rp_ok ? fb.rp(cur) : nullptr,
                              // the last pass's pdf cache has no reader (final shading re-shades; the next frame's
                              // temporal pass evaluates its own): not written
                              pass + 1 < passes ? fb.rp(nxt) : nullptr, &rp_ok, c->tuning, c->stream));
@@ -1409,7 +1460,8 @@ restir_status restir_stage_spatial(restir_ctx* c, const restir_camera* cam, cons
     TIMED(c, RESTIR_K_SPATIAL,
           launch_spatial(sd, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                          c->ra[cur].as<float4>(), c->rb[cur].as<float4>(), c->ra[nxt].as<float4>(), c->rb[nxt].as<float4>(),
-                         debug ? c->dbg[nxt].as<float2>() : nullptr, nullptr, nullptr, nullptr, c->tuning, c->stream));
+                         debug ? c->dbg[nxt].as<float2>() : nullptr, nullptr, nullptr, nullptr, nullptr, c->tuning,
+                         c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->cur = nxt;   // the pass output becomes "current" (RES_*), its input "prev" (PREV_*)
     return RESTIR_OK;
@@ -1612,6 +1664,8 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
     c->stage_ok = false;
     h.send = send; h.recv = recv; h.send_bytes = send_b; h.recv_bytes = recv_b;
     for (uint32_t i = 0; i < n; i++) { h.send_rank[i] = sg[i].rank; h.recv_rank[i] = rg_[i].rank; }
+    halo_ops_from(sg, rg_, n, h.ops);
+    h.nops = 2 * n;
     h.rank = rank;
     h.nranks = tiles_x * tiles_y;
     h.interior_done = false;
@@ -1714,8 +1768,9 @@ static HaloSplit halo_split(const Region& owned, uint32_t R) {
 }
 
 // one launch of the current pass over `rg` (a part of the owned rectangle); the pdf cache stays valid only if
-// every part wrote it
-static restir_status halo_spatial_part(restir_ctx* c, const Region& rg, bool& rp_written) {
+// every part wrote it.  The cache covers the owned rectangle only (the exchange moves reservoirs, not their
+// pdfs), so only the interior -- whose neighbourhoods stay inside it -- may read it at neighbour pixels.
+static restir_status halo_spatial_part(restir_ctx* c, const Region& rg, bool interior, bool& rp_written) {
     auto& h = c->halo;
     const int nxt = h.cur ^ 1;
     const FrameBufs fb{c, h.fb_records, (size_t)h.view.vw * h.view.vh, h.f.N};
@@ -1725,7 +1780,8 @@ static restir_status halo_spatial_part(restir_ctx* c, const Region& rg, bool& rp
     TIMED(c, RESTIR_K_SPATIAL,
           launch_spatial(sd, rg, h.f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_SPATIAL, h.pass), h.camd.origin,
                          fb.nt(h.cur), c->p_mat.as<float4>(), fb.ra(h.cur), fb.rb(h.cur), fb.ra(nxt), fb.rb(nxt), nullptr,
-                         h.rp_ok ? fb.rp(h.cur) : nullptr, fb.rp(nxt), &wrote, c->tuning, c->stream));
+                         h.rp_ok ? fb.rp(h.cur) : nullptr, h.rp_ok && interior ? fb.rp(h.cur) : nullptr, fb.rp(nxt),
+                         &wrote, c->tuning, c->stream));
     rp_written = rp_written && wrote;
     return RESTIR_OK;
 }
@@ -1737,7 +1793,7 @@ static restir_status halo_interior_locked(restir_ctx* c) {
     HIP_TRY(hipSetDevice(c->device));
     const HaloSplit hs = halo_split(h.owned, h.f.R);
     h.part_rp = true;
-    if (hs.part[0].rw && hs.part[0].rh) ST_TRY(halo_spatial_part(c, hs.part[0], h.part_rp));
+    if (hs.part[0].rw && hs.part[0].rh) ST_TRY(halo_spatial_part(c, hs.part[0], true, h.part_rp));
     h.interior_done = true;
     return RESTIR_OK;
 }
@@ -1748,7 +1804,7 @@ static restir_status halo_border_locked(restir_ctx* c) {
         return fail(RESTIR_ERR_STATE, "restir_halo_spatial_border before the pass's interior");
     HIP_TRY(hipSetDevice(c->device));
     const HaloSplit hs = halo_split(h.owned, h.f.R);
-    for (uint32_t i = 1; i <= hs.nb; i++) ST_TRY(halo_spatial_part(c, hs.part[i], h.part_rp));
+    for (uint32_t i = 1; i <= hs.nb; i++) ST_TRY(halo_spatial_part(c, hs.part[i], false, h.part_rp));
     h.rp_ok = h.part_rp;
     h.cur ^= 1;
     h.pass++;
@@ -1863,11 +1919,18 @@ static void release_rccl(restir_ctx* c) {
     q.recv.release();
 }
 
-static restir_status attach_comm_locked(restir_ctx* c, void* comm, bool owned) {
+// the communication stream and the pass's two events (a communicator's, or a record-only pass's)
+static restir_status comm_stream_locked(restir_ctx* c) {
     auto& q = c->rccl;
     if (!q.stream) HIP_TRY(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
     if (!q.packed) HIP_TRY(hipEventCreateWithFlags(&q.packed, hipEventDisableTiming));
     if (!q.moved) HIP_TRY(hipEventCreateWithFlags(&q.moved, hipEventDisableTiming));
+    return RESTIR_OK;
+}
+
+static restir_status attach_comm_locked(restir_ctx* c, void* comm, bool owned) {
+    auto& q = c->rccl;
+    ST_TRY(comm_stream_locked(c));
     if (q.comm && q.owned) RCCL_TRY(rccl_api().comm_destroy(static_cast<ncclComm_t>(q.comm)));
     q.comm = comm;
     q.owned = owned;
@@ -1917,45 +1980,93 @@ restir_status restir_halo_pass(restir_ctx* c) {
     std::lock_guard<std::mutex> lk(c->mu);
     auto& h = c->halo;
     auto& q = c->rccl;
-    if (!q.comm) return fail(RESTIR_ERR_STATE, "restir_halo_pass before restir_halo_attach_rccl / _comm");
+    const bool rec = c->halo_record;
+    if (!q.comm && !rec) return fail(RESTIR_ERR_STATE, "restir_halo_pass before restir_halo_attach_rccl / _comm");
     if (!h.active || h.pass >= h.passes || h.interior_done) return fail(RESTIR_ERR_STATE, "restir_halo_pass: no pass pending");
     // the plan's peers are tile ranks: the communicator must hold exactly the tiles, with this context's tile at
     // its own rank, or the halos would go to the wrong peers
-    if (q.nranks != (int)h.nranks || q.rank != (int)h.rank)
+    if (!rec && (q.nranks != (int)h.nranks || q.rank != (int)h.rank))
         return fail(RESTIR_ERR_INVALID, "restir_halo_pass: communicator rank %d of %d, halo frame is tile %u of %u",
                     q.rank, q.nranks, h.rank, h.nranks);
-    for (uint32_t i = 0; i < h.send.n; i++)
-        if (h.send_rank[i] >= h.nranks || h.recv_rank[i] >= h.nranks || h.send_rank[i] == h.rank)
-            return fail(RESTIR_ERR_INVALID, "restir_halo_pass: segment %u peers %u / %u outside the %u tiles", i,
-                        h.send_rank[i], h.recv_rank[i], h.nranks);
-    const RcclApi& api = rccl_api();
+    for (uint32_t i = 0; i < h.nops; i++)
+        if (h.ops[i].peer >= h.nranks || h.ops[i].peer == h.rank)
+            return fail(RESTIR_ERR_INVALID, "restir_halo_pass: operation %u peer %u outside the %u tiles", i, h.ops[i].peer,
+                        h.nranks);
     HIP_TRY(hipSetDevice(c->device));
+    ST_TRY(comm_stream_locked(c));
     ST_TRY(q.send.ensure(std::max<uint64_t>(h.send_bytes, 16)));
     ST_TRY(q.recv.ensure(std::max<uint64_t>(h.recv_bytes, 16)));
+    const uint32_t pass = h.pass;
+    auto log = [&](uint32_t what, uint32_t stream, uint32_t peer = 0, uint64_t off = 0, uint64_t bytes = 0) {
+        if (rec) c->halo_log.push_back(restir_halo_event{what, stream, peer, pass, off, bytes});
+    };
     const FrameBufs fb{c, h.fb_records, (size_t)h.view.vw * h.view.vh, h.f.N};
     // context stream: pack (after the previous pass's transfer released the send buffer -- stream order:
     // the previous pass waited on q.moved before its unpack)
     HIP_TRY(launch_halo_pack(h.view, h.send, h.f.N, fb.ra(h.cur), fb.rb(h.cur), q.send.as<float4>(), c->stream));
+    log(RESTIR_HALO_EV_PACK, 0, 0, 0, h.send_bytes);
     HIP_TRY(hipEventRecord(q.packed, c->stream));
-    // communication stream: the grouped point-to-point transfer of every plan segment
+    log(RESTIR_HALO_EV_RECORD, 0, 0);
+    // communication stream: the grouped point-to-point transfer of every plan segment (restir_halo_ops' list)
     HIP_TRY(hipStreamWaitEvent(q.stream, q.packed, 0));
-    const ncclComm_t comm = static_cast<ncclComm_t>(q.comm);
-    if (h.send.n) {
-        RCCL_TRY(api.group_start());
-        for (uint32_t i = 0; i < h.send.n; i++) {
-            const uint64_t so = (uint64_t)h.send.px0[i] * h.f.N * 32u, sb = (uint64_t)h.send.w[i] * h.send.h[i] * h.f.N * 32u;
-            const uint64_t ro = (uint64_t)h.recv.px0[i] * h.f.N * 32u, rb = (uint64_t)h.recv.w[i] * h.recv.h[i] * h.f.N * 32u;
-            RCCL_GROUP_TRY(api.send(static_cast<const char*>(q.send.p) + so, sb, ncclUint8, (int)h.send_rank[i], comm, q.stream));
-            RCCL_GROUP_TRY(api.recv(static_cast<char*>(q.recv.p) + ro, rb, ncclUint8, (int)h.recv_rank[i], comm, q.stream));
+    log(RESTIR_HALO_EV_WAIT, 1, 0);
+    if (h.nops) {
+        if (rec) {   // nothing moves: a zeroed receive buffer stands in for the transfer
+            HIP_TRY(hipMemsetAsync(q.recv.p, 0, h.recv_bytes, q.stream));
+        } else {
+            RCCL_TRY(rccl_api().group_start());
         }
-        RCCL_TRY(api.group_end());
+        log(RESTIR_HALO_EV_GROUP_START, 1);
+        const ncclComm_t comm = static_cast<ncclComm_t>(q.comm);
+        for (uint32_t i = 0; i < h.nops; i++) {
+            const restir_halo_op& o = h.ops[i];
+            if (o.kind == RESTIR_HALO_OP_SEND) {
+                if (!rec) RCCL_GROUP_TRY(rccl_api().send(static_cast<const char*>(q.send.p) + o.offset, o.bytes, ncclUint8,
+                                                         (int)o.peer, comm, q.stream));
+                log(RESTIR_HALO_EV_SEND, 1, o.peer, o.offset, o.bytes);
+            } else {
+                if (!rec) RCCL_GROUP_TRY(rccl_api().recv(static_cast<char*>(q.recv.p) + o.offset, o.bytes, ncclUint8,
+                                                         (int)o.peer, comm, q.stream));
+                log(RESTIR_HALO_EV_RECV, 1, o.peer, o.offset, o.bytes);
+            }
+        }
+        if (!rec) RCCL_TRY(rccl_api().group_end());
+        log(RESTIR_HALO_EV_GROUP_END, 1);
     }
     HIP_TRY(hipEventRecord(q.moved, q.stream));
+    log(RESTIR_HALO_EV_RECORD, 1, 1);
     // context stream: the interior overlaps the transfer; unpack + border strips after it
     ST_TRY(halo_interior_locked(c));
+    log(RESTIR_HALO_EV_INTERIOR, 0);
     HIP_TRY(hipStreamWaitEvent(c->stream, q.moved, 0));
+    log(RESTIR_HALO_EV_WAIT, 0, 1);
     HIP_TRY(launch_halo_unpack(h.view, h.recv, h.f.N, q.recv.as<float4>(), fb.ra(h.cur), fb.rb(h.cur), c->stream));
-    return halo_border_locked(c);
+    log(RESTIR_HALO_EV_UNPACK, 0, 0, 0, h.recv_bytes);
+    ST_TRY(halo_border_locked(c));
+    log(RESTIR_HALO_EV_BORDER, 0);
+    return RESTIR_OK;
+}
+
+restir_status restir_halo_record(restir_ctx* c, int on) {
+    if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->halo_record = on != 0;
+    c->halo_log.clear();
+    return RESTIR_OK;
+}
+
+restir_status restir_halo_log(restir_ctx* c, restir_halo_event* out, uint32_t* count) {
+    if (!c || !count || (*count && !out)) return fail(RESTIR_ERR_INVALID, "restir_halo_log: null argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    const size_t n = c->halo_log.size();
+    if (*count < n) {
+        *count = (uint32_t)n;
+        return fail(RESTIR_ERR_INVALID, "restir_halo_log: capacity for %zu entries needed", n);
+    }
+    std::copy(c->halo_log.begin(), c->halo_log.end(), out);
+    *count = (uint32_t)n;
+    c->halo_log.clear();
+    return RESTIR_OK;
 }
 
 restir_status restir_halo_end(restir_ctx* c, restir_frame** out_next, float* out_rgb) {
@@ -2001,7 +2112,7 @@ restir_status restir_enable_timing(restir_ctx* c, int enable) {
         const size_t want = 512;   // bench.py's default timed region (200 frames x 2) without growing; more on demand
         while (c->free_events.size() + c->pending.size() * 2 < want) {
             hipEvent_t e = nullptr;
-            HIP_TRY(hipEventCreate(&e));
+            HIP_TRY(timing_event_create(c, &e));
             c->free_events.push_back(e);
         }
     }
@@ -2039,6 +2150,16 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.th")) { if (v > 2) return fail(RESTIR_ERR_INVALID, "spatial.th: 0 (auto), 1 or 2"); t.spatial_th = v; }
     else if (!std::strcmp(key, "fuse.primary_ris")) t.fuse_primary_ris = v;
     else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;
+    else if (!std::strcmp(key, "timing.fence")) {
+        // the pooled events carry the old flags: drop the free ones (recreated on demand)
+        if (t.timing_fence != v) {
+            HIP_TRY(hipSetDevice(c->device));
+            ST_TRY(collect_timings(c));   // pending pairs return to the pool first
+            for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
+            c->free_events.clear();
+        }
+        t.timing_fence = v;
+    }
     else if (!std::strcmp(key, "ris.queue")) t.ris_queue = v;
     else if (!std::strcmp(key, "ris.compact")) t.ris_compact = v;
     else if (!std::strcmp(key, "bvh.max_leaf")) t.bvh_max_leaf = v;

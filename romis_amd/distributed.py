@@ -41,8 +41,13 @@ class HaloFrames:
                              f"{dist.get_rank(group)} of {dist.get_world_size(group)}: the halo peers are tile ranks")
         self.on_device = dist.get_backend(group) == "nccl"
         self.transport = transport or "torch"
-        if self.transport not in ("torch", "native"):
+        if self.transport not in ("torch", "native", "record"):
             raise ValueError(f"HaloFrames: unknown transport {self.transport!r}")
+        if self.transport == "record":
+            # the native pass without RCCL (restir_halo_record): every step it would issue is logged, nothing moves
+            # (zeroed receive buffers) -- the plumbing check of tests/test_gpu_halo.py, not a valid frame
+            self.r.halo_record(True)
+            return
         if self.transport == "native":
             # one rank draws the communicator id, every rank receives it over the torch group; its last byte says
             # whether rank 0 could draw one, so that every rank fails together (never some ranks waiting inside a
@@ -96,7 +101,7 @@ class HaloFrames:
     def render(self, prev, camera, want_rgb: bool = True, want_grid: bool = True):
         """One frame: (rgb of the owned tile [h][w][3], row 0 = top, or None; ReservoirGrid for temporal reuse)."""
         sb, rb = self.r.halo_begin(prev, camera, self.W, self.H, self.f, self.tiles, self.rank)
-        if self.transport == "native":
+        if self.transport in ("native", "record"):
             for _ in range(self.passes):
                 self.r.halo_pass()
             return self.r.halo_end(self.tile, want_rgb, want_grid)

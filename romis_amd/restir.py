@@ -151,6 +151,21 @@ class Renderer:
         """One spatial pass with the exchange over the attached communicator, overlapped with the interior."""
         check(self.lib, self.lib.restir_halo_pass(self.ctx), "restir_halo_pass")
 
+    def halo_record(self, on: bool = True) -> None:
+        """restir_halo_record: halo_pass logs the steps it issues instead of calling RCCL (no communicator needed)."""
+        check(self.lib, self.lib.restir_halo_record(self.ctx, 1 if on else 0), "restir_halo_record")
+
+    def halo_log(self) -> list:
+        """restir_halo_log: the record-only passes' steps in issue order (then cleared), as HaloEvent structs."""
+        n = C.c_uint32(0)
+        rc = self.lib.restir_halo_log(self.ctx, None, C.byref(n))
+        if rc != 0 and n.value == 0:
+            check(self.lib, rc, "restir_halo_log")
+        buf = (_abi.HaloEvent * max(1, n.value))()
+        n2 = C.c_uint32(n.value)
+        check(self.lib, self.lib.restir_halo_log(self.ctx, buf, C.byref(n2)), "restir_halo_log")
+        return list(buf[:n2.value])
+
     def halo_end(self, tile, want_rgb: bool = True, want_grid: bool = True):
         out = C.c_void_p()
         rgb = np.zeros((tile.height, tile.width, 3), np.float32) if want_rgb else None
@@ -318,6 +333,15 @@ def halo_plan(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, ra
     check(lib, lib.restir_halo_plan(width, height, tiles_x, tiles_y, rank, radius, N, send, recv, C.byref(n)),
           "restir_halo_plan")
     return list(send[:n.value]), list(recv[:n.value])
+
+
+def halo_ops(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, radius: int, N: int) -> list:
+    """restir_halo_ops: the sends / receives restir_halo_pass posts per spatial pass, in posting order."""
+    lib = _abi.load_library()
+    ops = (_abi.HaloOp * 16)()
+    n = C.c_uint32(16)
+    check(lib, lib.restir_halo_ops(width, height, tiles_x, tiles_y, rank, radius, N, ops, C.byref(n)), "restir_halo_ops")
+    return list(ops[:n.value])
 
 
 def tile_plan(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, ghost: int) -> _abi.Tile:

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol(abi_lib):
     for n in names:
         assert hasattr(abi_lib, n), n
     assert set(names) == set(_abi.SIGNATURES), "romis_amd/_abi.py must bind exactly the header's functions"
-    assert abi_lib.restir_abi_version() == 4
+    assert abi_lib.restir_abi_version() == _abi.RESTIR_ABI_VERSION == 5
 
 
 def test_rng_matches_oracle(abi_lib, oracle):

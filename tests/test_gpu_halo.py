@@ -23,13 +23,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _features(passes, N):
+def _features(passes, N, unbiased=0, vis=0):
     from romis_amd import _abi
-    return _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=passes, temporal_reuse=1)
+    return _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=passes, temporal_reuse=1,
+                                 unbiased_combination=unbiased, spatial_reuse_visibility_check=vis)
 
 
 def _worker(rank, world, port, tiles, passes, N, out_dir, name="nightclub_128pt", records=0, backend="gloo",
-            width=W, height=H):
+            width=W, height=H, unbiased=0, vis=0):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from romis_amd import _abi, distributed, restir, scene
@@ -42,7 +43,7 @@ def _worker(rank, world, port, tiles, passes, N, out_dir, name="nightclub_128pt"
     r.set_scene(sc)
     r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
     cam = scene.camera_for(name, W, H)
-    hf = distributed.HaloFrames(r, W, H, tiles, rank, _features(passes, N))
+    hf = distributed.HaloFrames(r, W, H, tiles, rank, _features(passes, N, unbiased, vis))
     prev = None
     for fr in range(FRAMES):
         rgb, prev = hf.render(prev, cam)
@@ -60,7 +61,7 @@ def _worker(rank, world, port, tiles, passes, N, out_dir, name="nightclub_128pt"
     dist.destroy_process_group()
 
 
-def _single_gpu_check(tmp_path, passes, N, name=_DEFAULT_SCENE, records=0, width=W, height=H):
+def _single_gpu_check(tmp_path, passes, N, name=_DEFAULT_SCENE, records=0, width=W, height=H, unbiased=0, vis=0):
     from romis_amd import _abi, restir, scene
     W, H = width, height
     r = restir.Renderer(0)
@@ -69,7 +70,7 @@ def _single_gpu_check(tmp_path, passes, N, name=_DEFAULT_SCENE, records=0, width
         r.set_scene(scene.bench_scene(name))
         r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
         cam = scene.camera_for(name, W, H)
-        f = _features(passes, N)
+        f = _features(passes, N, unbiased, vis)
         prev = None
         for fr in range(FRAMES):
             want, prev = r.render_restir(prev, cam, W, H, f)
@@ -83,16 +84,21 @@ def _single_gpu_check(tmp_path, passes, N, name=_DEFAULT_SCENE, records=0, width
 
 # Each rank is its own process and restir context on the box's one GPU; the pass runs as interior (issued
 # before the exchange) + border strips (after the unpack).  (8, (4, 2)): the C4 / C5 split; (8, (8, 1)): tiles
-# 12 px wide, narrower than 2R, so the interior is empty and the border strips cover the tile.
+# 12 px wide, narrower than 2R, so the interior is empty and the border strips cover the tile.  The unbiased cases
+# run the lean N = 1 unbiased pass (k_spatial1u[_vis]), whose Z term reads the pdf cache at neighbour pixels: in a
+# border strip those may lie in the exchanged ring, which carries no cache (restir.cpp halo_spatial_part).
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,tiles,passes,N,name,records", [
-    (2, (2, 1), 2, 1, _DEFAULT_SCENE, 0), (4, (2, 2), 2, 1, _DEFAULT_SCENE, 0), (4, (2, 2), 1, 2, _DEFAULT_SCENE, 0),
-    (2, (2, 1), 2, 1, _DEFAULT_SCENE, 1), (4, (2, 2), 1, 2, _DEFAULT_SCENE, 1),
-    (8, (4, 2), 2, 1, "cornell_1024", 0), (8, (8, 1), 1, 1, _DEFAULT_SCENE, 0)])
-def test_halo_frames_match_single_gpu_sequence(tmp_path, world, tiles, passes, N, name, records):
-    mp.spawn(_worker, args=(world, _free_port(), tiles, passes, N, str(tmp_path), name, records), nprocs=world,
-             join=True)
-    _single_gpu_check(tmp_path, passes, N, name, records)
+@pytest.mark.parametrize("world,tiles,passes,N,name,records,unbiased,vis", [
+    (2, (2, 1), 2, 1, _DEFAULT_SCENE, 0, 0, 0), (4, (2, 2), 2, 1, _DEFAULT_SCENE, 0, 0, 0),
+    (4, (2, 2), 1, 2, _DEFAULT_SCENE, 0, 0, 0),
+    (2, (2, 1), 2, 1, _DEFAULT_SCENE, 1, 0, 0), (4, (2, 2), 1, 2, _DEFAULT_SCENE, 1, 0, 0),
+    (8, (4, 2), 2, 1, "cornell_1024", 0, 0, 0), (8, (8, 1), 1, 1, _DEFAULT_SCENE, 0, 0, 0),
+    (2, (2, 1), 2, 1, _DEFAULT_SCENE, 0, 1, 0), (4, (2, 2), 1, 1, "cornell_1024", 0, 1, 1),
+    (8, (4, 2), 2, 1, "cornell_4096", 0, 1, 1), (4, (2, 2), 1, 2, _DEFAULT_SCENE, 0, 1, 1)])
+def test_halo_frames_match_single_gpu_sequence(tmp_path, world, tiles, passes, N, name, records, unbiased, vis):
+    mp.spawn(_worker, args=(world, _free_port(), tiles, passes, N, str(tmp_path), name, records, "gloo", W, H,
+                            unbiased, vis), nprocs=world, join=True)
+    _single_gpu_check(tmp_path, passes, N, name, records, unbiased=unbiased, vis=vis)
 
 
 # The native transport (restir_halo_pass: the library's own RCCL communicator, grouped ncclSend / ncclRecv on a
@@ -164,3 +170,59 @@ def test_native_rccl_halo_single_rank(tmp_path):
     skips = sorted(p for p in os.listdir(tmp_path) if p.startswith("skip"))
     assert not skips, open(os.path.join(tmp_path, skips[0])).read()
     _single_gpu_check(tmp_path, 2, 1)
+
+
+# Record-only restir_halo_pass (restir_halo_record): the native transport's plumbing on the box's one GPU.  For
+# every rank of a split, one context runs a frame's passes through restir_halo_pass without a communicator; its log
+# must show, per pass, the pack and its event on the context stream, the communication stream's wait for that
+# event, the group of sends / receives -- exactly restir_halo_ops' list (peer, offset, bytes), the list the CPU
+# suite moves over gloo (tests/test_multirank_gloo.py) -- and its completion event, then the interior launch, the
+# context stream's wait for the transfer, the unpack and the border launches; and every rank's sends must pair
+# with its peers' receives.
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,tiles,N", [(2, (2, 1), 1), (4, (2, 2), 2), (8, (4, 2), 1)])
+def test_native_halo_pass_record_only(world, tiles, N):
+    from romis_amd import _abi, restir, scene
+    passes = 2
+    f = _features(passes, N)
+    R = f.spatial_resample_radius
+    E = _abi
+    logs = {}
+    r = restir.Renderer(0)
+    try:
+        r.set_scene(scene.bench_scene(_DEFAULT_SCENE))
+        cam = scene.camera_for(_DEFAULT_SCENE, W, H)
+        r.halo_record(True)
+        for rank in range(world):
+            t = restir.tile_plan(W, H, tiles[0], tiles[1], rank, R)
+            sb, rb = r.halo_begin(None, cam, W, H, f, tiles, rank)
+            for _ in range(passes):
+                r.halo_pass()
+            r.halo_end(t, False, False)
+            r.synchronize()
+            logs[rank] = [(e.what, e.stream, e.peer, e.pass_, e.offset, e.bytes) for e in r.halo_log()]
+            ops = restir.halo_ops(W, H, tiles[0], tiles[1], rank, R, N)
+            assert sb == sum(o.bytes for o in ops if o.kind == E.RESTIR_HALO_OP_SEND)
+            assert rb == sum(o.bytes for o in ops if o.kind == E.RESTIR_HALO_OP_RECV)
+            want = []
+            for p in range(passes):
+                want += [(E.RESTIR_HALO_EV_PACK, 0, 0, p, 0, sb), (E.RESTIR_HALO_EV_RECORD, 0, 0, p, 0, 0),
+                         (E.RESTIR_HALO_EV_WAIT, 1, 0, p, 0, 0), (E.RESTIR_HALO_EV_GROUP_START, 1, 0, p, 0, 0)]
+                want += [(E.RESTIR_HALO_EV_SEND if o.kind == E.RESTIR_HALO_OP_SEND else E.RESTIR_HALO_EV_RECV, 1, o.peer,
+                          p, o.offset, o.bytes) for o in ops]
+                want += [(E.RESTIR_HALO_EV_GROUP_END, 1, 0, p, 0, 0), (E.RESTIR_HALO_EV_RECORD, 1, 1, p, 0, 0),
+                         (E.RESTIR_HALO_EV_INTERIOR, 0, 0, p, 0, 0), (E.RESTIR_HALO_EV_WAIT, 0, 1, p, 0, 0),
+                         (E.RESTIR_HALO_EV_UNPACK, 0, 0, p, 0, rb), (E.RESTIR_HALO_EV_BORDER, 0, 0, p, 0, 0)]
+            assert logs[rank] == want, f"rank {rank}"
+            for o in ops:   # the rectangle each send carries is one of the peer's receives, byte count included
+                if o.kind == E.RESTIR_HALO_OP_SEND:
+                    peer = restir.halo_ops(W, H, tiles[0], tiles[1], o.peer, R, N)
+                    m = [q for q in peer if q.kind == E.RESTIR_HALO_OP_RECV and q.peer == rank and
+                         (q.x0, q.y0, q.width, q.height, q.bytes) == (o.x0, o.y0, o.width, o.height, o.bytes)]
+                    assert len(m) == 1, f"send {rank}->{o.peer}"
+        r.halo_record(False)
+        with pytest.raises(_abi.RestirError, match="STATE"):   # no communicator outside record mode
+            r.halo_begin(None, cam, W, H, f, tiles, 0)
+            r.halo_pass()
+    finally:
+        r.close()

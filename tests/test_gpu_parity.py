@@ -717,6 +717,46 @@ def test_full_size_frames_c4_c5_band_parity(gpu, oracle, cfg):
         assert_bits(rgb[r0:r0 + rows], want, f"{cfg} rows {y0}..{y0 + rows - 1}")
 
 
+def test_full_size_c2_frame_band_parity(gpu, oracle):
+    """C2, the headline (BASELINE configs[1]), at its full size through the bench's own path: restir_render with the
+    fused primary + RIS kernel writing the pdf cache, k_spatial1_ntl reading it (no temporal pass between), final
+    shading.  The frame's RGB (want_grid=False, as bench.py renders it) and, from a second render of the same
+    frame, its returned grid, on sampled row bands against the oracle rendering those rows with the ghost rows its
+    spatial pass reads, bit for bit."""
+    name, Wf, Hf = "nightclub_128pt", 1920, 1080
+    s = get_scene(name)
+    gpu.set_scene(s)
+    cam = scene.camera_for(name, Wf, Hf)
+    f = _abi.default_features(initial_light_samples=32, num_samples_in_reservoir=1, num_neighbours_to_sample=5,
+                              spatial_resample_radius=10, spatial_resampling_passes=1, temporal_reuse=0)
+    gpu.set_seed(SEED, 0)
+    rgb, _ = gpu.render_restir(None, cam, Wf, Hf, f, want_grid=False)
+    gpu.set_seed(SEED, 0)
+    rgb2, grid = gpu.render_restir(None, cam, Wf, Hf, f)
+    assert_bits(rgb2, rgb, "C2 rgb with and without the returned grid")
+    pos, col, w, m = grid.download()
+    osc = oracle.OracleScene(s)
+    g = f.spatial_resample_radius
+    rows = 6
+    for y0 in (0, 97, 355, Hf // 2 - 3, 811, Hf - rows):
+        vy0 = max(0, y0 - g)
+        view = oracle.Rect(0, vy0, Wf, min(Hf, y0 + rows + g) - vy0)
+        rect = oracle.Rect(0, y0, Wf, rows)
+        want, res, _ = oracle.render_frame(osc, cam, f, Wf, Hf, SEED, 0, view=view, rect=rect, threads=16)
+        r0 = Hf - (y0 + rows)          # RGB row 0 = top of the image
+        assert_bits(rgb[r0:r0 + rows], want, f"C2 rgb rows {y0}..{y0 + rows - 1}")
+        a, b = res
+        sl = slice((y0 - vy0) * Wf, (y0 - vy0 + rows) * Wf)
+        a = a[:, sl].reshape(1, rows, Wf, 4)
+        b = b[:, sl].reshape(1, rows, Wf, 4)
+        gs = slice(y0, y0 + rows)
+        assert_bits(pos[:, gs], np.ascontiguousarray(a[..., :3]), f"C2 grid position rows {y0}..")
+        assert_bits(w[:, gs], np.ascontiguousarray(a[..., 3]), f"C2 grid W rows {y0}..")
+        assert_bits(col[:, gs], np.ascontiguousarray(b[..., :3]), f"C2 grid colour rows {y0}..")
+        assert np.array_equal(m[:, gs], np.ascontiguousarray(b[..., 3]).view(np.uint32)), f"C2 grid M rows {y0}.."
+    assert rgb.mean() > 0.01
+
+
 def test_full_size_c1_frame_matches_oracle(gpu, oracle):
     """C1 (BASELINE configs[0]) at its full size: CornellBox-Mirror 512x512, 1 parallelogram light, M = 32, RIS
     only -- the whole frame's RGB and returned grid against the oracle, bit for bit."""

@@ -215,3 +215,114 @@ def test_bench_halo_self_check_over_gloo(tmp_path, world, tiles, abi_lib, oracle
     for rank in range(world):
         with open(f"{result}.{rank}") as fh:
             assert fh.read().split() == ["0", "1", "1", "1"], rank
+
+
+# ---- the native RCCL halo transport's operations, moved over gloo ------------------------------------------
+# restir_halo_pass posts, per spatial pass, the list restir_halo_ops returns (one ncclSend then one ncclRecv per
+# plan segment, inside one group).  Here every rank takes that list from the library, fills its send buffer from
+# its owned reservoirs exactly as k_halo_pack lays them out ([sub-reservoir][pixel row-major][res_a, res_b]; the
+# reservoirs are synthetic, a function of global pixel, sub-reservoir and field), posts the same sends / receives
+# (peer, offset, bytes) over gloo, and checks that every received byte is the reservoir k_halo_unpack would
+# write at that ring pixel.  Every rank's sends must also equal its peers' receives (gathered and paired), and the
+# list must be the segments the torch transport moves (HaloFrames: restir_halo_plan).
+def _synthetic_reservoirs(x0, y0, w, h, N):
+    """[N][h*w][8] float32 words (res_a xyzw, res_b xyzw) of the global rectangle, bit patterns from the pixel id."""
+    ys, xs = np.mgrid[y0:y0 + h, x0:x0 + w]
+    g = (ys.astype(np.uint64) * 100003 + xs.astype(np.uint64)).reshape(-1)
+    out = np.zeros((N, w * h, 8), np.uint32)
+    for j in range(N):
+        for k in range(8):
+            out[j, :, k] = ((g * 8 + k) * 2654435761 + j * 40503 + 1) & 0x7F7FFFFF   # finite float bit patterns
+    return out.view(np.float32)
+
+
+def _native_ops_worker(rank, world, port, tiles, Wimg, Himg, R, N, result_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from romis_amd import _abi, restir
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    errs = []
+    ops = restir.halo_ops(Wimg, Himg, tiles[0], tiles[1], rank, R, N)
+    send, recv = restir.halo_plan(Wimg, Himg, tiles[0], tiles[1], rank, R, N)
+    # the posting order and the torch transport's segments
+    if len(ops) != 2 * len(send):
+        errs.append(f"{len(ops)} operations for {len(send)} segments")
+    for i, (s, r) in enumerate(zip(send, recv)):
+        o, p = ops[2 * i], ops[2 * i + 1]
+        for op, seg, kind in ((o, s, _abi.RESTIR_HALO_OP_SEND), (p, r, _abi.RESTIR_HALO_OP_RECV)):
+            want = (kind, seg.rank, seg.offset, seg.bytes, seg.x0, seg.y0, seg.width, seg.height)
+            got = (op.kind, op.peer, op.offset, op.bytes, op.x0, op.y0, op.width, op.height)
+            if got != want:
+                errs.append(f"op {2 * i + (kind == _abi.RESTIR_HALO_OP_RECV)}: {got} != segment {want}")
+    # pack as k_halo_pack does, then post exactly the listed operations
+    sb = sum(o.bytes for o in ops if o.kind == _abi.RESTIR_HALO_OP_SEND)
+    rb = sum(o.bytes for o in ops if o.kind == _abi.RESTIR_HALO_OP_RECV)
+    sendbuf = torch.zeros(max(1, sb), dtype=torch.uint8)
+    recvbuf = torch.full((max(1, rb),), 0xAB, dtype=torch.uint8)
+    t = restir.tile_plan(Wimg, Himg, tiles[0], tiles[1], rank, 0)
+    for o in ops:
+        if o.kind != _abi.RESTIR_HALO_OP_SEND:
+            continue
+        inside = t.x0 <= o.x0 and o.x0 + o.width <= t.x0 + t.width and t.y0 <= o.y0 and o.y0 + o.height <= t.y0 + t.height
+        if not inside:
+            errs.append(f"send to {o.peer}: rectangle outside the owned tile")
+        if o.bytes != o.width * o.height * N * 32:
+            errs.append(f"send to {o.peer}: {o.bytes} bytes for a {o.width}x{o.height} rectangle")
+        blob = _synthetic_reservoirs(o.x0, o.y0, o.width, o.height, N).tobytes()
+        sendbuf[o.offset:o.offset + o.bytes] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+    p2p = []
+    for o in ops:
+        if o.kind == _abi.RESTIR_HALO_OP_SEND:
+            p2p.append(dist.P2POp(dist.isend, sendbuf[o.offset:o.offset + o.bytes], o.peer))
+        else:
+            p2p.append(dist.P2POp(dist.irecv, recvbuf[o.offset:o.offset + o.bytes], o.peer))
+    if p2p:
+        for q in dist.batch_isend_irecv(p2p):
+            q.wait()
+    got = recvbuf.numpy()
+    ring = 0
+    for o in ops:
+        if o.kind != _abi.RESTIR_HALO_OP_RECV:
+            continue
+        want = _synthetic_reservoirs(o.x0, o.y0, o.width, o.height, N).view(np.uint8).reshape(-1)
+        if not np.array_equal(got[o.offset:o.offset + o.bytes], want):
+            errs.append(f"recv from {o.peer}: bytes differ from that rank's reservoirs at {o.x0},{o.y0} {o.width}x{o.height}")
+        # the received rectangle lies in this rank's ring: outside the owned tile, within R of it
+        for yy in (o.y0, o.y0 + o.height - 1):
+            for xx in (o.x0, o.x0 + o.width - 1):
+                owned = t.x0 <= xx < t.x0 + t.width and t.y0 <= yy < t.y0 + t.height
+                near = t.x0 - R <= xx < t.x0 + t.width + R and t.y0 - R <= yy < t.y0 + t.height + R
+                if owned or not near:
+                    errs.append(f"recv from {o.peer}: pixel {xx},{yy} not in the ring")
+        ring += o.width * o.height
+    # sends pair with the peers' receives: same rectangle, same bytes, one each
+    allops = [None] * world
+    dist.all_gather_object(allops, [(o.kind, o.peer, o.x0, o.y0, o.width, o.height, o.bytes) for o in ops])
+    for k, p, x0, y0, w, h, b in allops[rank]:
+        if k == _abi.RESTIR_HALO_OP_SEND:
+            match = [q for q in allops[p] if q == (_abi.RESTIR_HALO_OP_RECV, rank, x0, y0, w, h, b)]
+            if len(match) != 1:
+                errs.append(f"send {rank}->{p} {x0},{y0} {w}x{h}: {len(match)} matching receives")
+    # every ring pixel a spatial pass may read (+-R around the tile, clamped to the image) is received exactly once
+    need = sum(1 for yy in range(max(0, t.y0 - R), min(Himg, t.y0 + t.height + R))
+               for xx in range(max(0, t.x0 - R), min(Wimg, t.x0 + t.width + R))
+               if not (t.x0 <= xx < t.x0 + t.width and t.y0 <= yy < t.y0 + t.height))
+    if ring != need:
+        errs.append(f"{ring} ring pixels received, {need} needed")
+    with open(os.path.join(result_dir, f"rank{rank}.txt"), "w") as fh:
+        fh.write("\n".join(errs) if errs else "ok")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,tiles,Wimg,Himg,R,N", [(2, (2, 1), 96, 40, 10, 1), (4, (2, 2), 101, 67, 7, 2),
+                                                       (8, (4, 2), 3840 // 16, 2160 // 16, 10, 1),
+                                                       (8, (4, 2), 90, 33, 12, 3)])
+def test_native_halo_operations_over_gloo(tmp_path, world, tiles, Wimg, Himg, R, N, abi_lib):
+    mp.spawn(_native_ops_worker, args=(world, _free_port(), tiles, Wimg, Himg, R, N, str(tmp_path)), nprocs=world,
+             join=True)
+    for r in range(world):
+        msg = open(tmp_path / f"rank{r}.txt").read()
+        assert msg == "ok", f"rank {r}: {msg}"

@@ -21,10 +21,13 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import sys
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -55,6 +58,8 @@ def parse():
     ap.add_argument("--tile-height", type=int, default=None)
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
+    ap.add_argument("--no-cpu-stages", dest="cpu_stages", action="store_false", default=True,
+                    help="skip cpu_baseline.stages (per-stage oracle rates for C1 and C2)")
     ap.add_argument("--time-kernels", default="spatial", choices=["all", "spatial"],
                     help="kernels bracketed by HIP events in the timed region")
     ap.add_argument("--cpu-rows", type=int, default=None, help="rows of the workload the CPU baseline renders "
@@ -73,6 +78,9 @@ def parse():
                     help="4-GiB streaming-read sweeps (restir_measure_read_bandwidth, ~0.6 ms each) before the warm-up "
                          "frames: the clocks of an idle box ramp over the first ~25 ms of load (kernel durations fell "
                          "6-11 %% over a 50-frame run, profiles/r4/gap); the same sweeps give measured_read_peak")
+    ap.add_argument("--prewarm-gemm-ms", type=float, default=0.0,
+                    help="GPU clock pre-warm before the warm-up frames: fp32 GEMMs through torch for this long "
+                         "(compute-bound; the streaming-read sweeps of --prewarm do not raise the clocks)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="restir_set_tuning knobs for A/B runs (launch shapes and timing only; results are identical)")
     ap.add_argument("--traffic-csv", default=None,
@@ -116,6 +124,21 @@ def max_over_ranks(torch, world, value, local):
     t = torch.tensor([value], dtype=torch.float64, device=torch.device("cuda", local) if on_gpu else "cpu")
     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     return float(t.item())
+
+
+def gemm_prewarm(torch, local, ms):
+    """fp32 4096^3 GEMMs on this rank's GPU for `ms` milliseconds (not a frame, not timed): compute-bound work that
+    brings an idle box's shader clocks up before the warm-up frames."""
+    dev = torch.device("cuda", local)
+    a = torch.randn(4096, 4096, device=dev)
+    b = torch.randn(4096, 4096, device=dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(4):
+            a = torch.mm(a, b) * 1e-3
+        torch.cuda.synchronize(dev)
+    del a, b
 
 
 def committed_traffic(cfg):
@@ -231,6 +254,106 @@ def cpu_baseline(sc, cam_fn, features, rows, W, H):
             "reference_rng": {"value": round(px_ref / dt_ref / 1e6, 6), "unit": "Mpixel-reservoirs/s", "cores": threads,
                               "seconds": round(dt_ref, 3), "rows": rows_ref, "ghost_rows_computed": 2 * g,
                               "rng": "per-pixel std::random_device + std::mt19937, global rand() (oracle/ref_rng.cpp)"}}
+
+
+def cpu_stage_baseline(sc, cam, features, W, H, rows, reference_rng):
+    """Per-stage rates of the oracle (OpenMP over rows, the thread count cpu_baseline set) on a band of `rows` owned
+    rows of a W x H frame: primary rays and RIS / temporal over the band's view (owned rows + the passes * r ghost
+    rows the spatial passes read), the spatial passes and final shading over the owned rows.  Mpixel-reservoirs/s
+    per stage (pixels the stage computes x N / seconds) -- BASELINE.md's per-stage CPU baseline (render_utils.cpp:
+    36-52, 87-140, 142-177; render.cpp:45-57)."""
+    from oracle import pyoracle
+    from romis_amd import _abi
+    f = features
+    N = f.num_samples_in_reservoir
+    passes = f.spatial_resampling_passes if f.spatial_reuse else 0
+    g = passes * f.spatial_resample_radius
+    y0 = (H - rows) // 2
+    vy0, vy1 = max(0, y0 - g), min(H, y0 + rows + g)
+    view, rect = pyoracle.Rect(0, vy0, W, vy1 - vy0), pyoracle.Rect(0, y0, W, rows)
+    osc = pyoracle.OracleScene(sc)
+    cf = pyoracle.camera_frame(cam)
+    o = np.array(list(cf.origin), np.float32)
+    lib = pyoracle.lib()
+    nv = view.w * view.h
+    n_t, p_mat = np.zeros((nv, 4), np.float32), np.zeros((nv, 4), np.float32)
+    out = {}
+
+    def rate(name, px, fn):
+        t0 = time.perf_counter()
+        fn()
+        dt = time.perf_counter() - t0
+        out[name] = {"value": round(px * N / dt / 1e6, 6), "pixels": int(px), "seconds": round(dt, 4)}
+
+    pyoracle.set_rng_mode(reference_rng)
+    try:
+        rate("primary", nv, lambda: lib.or_primary(osc.handle, C.byref(cf), W, H, view, view, pyoracle.fp(n_t),
+                                                   pyoracle.fp(p_mat)))
+        res = {}
+
+        def ris(tag, key):
+            a, b, _ = pyoracle.empty_reservoirs(N, nv)
+            lib.or_ris(osc.handle, C.byref(f), key, pyoracle.fp(o), W, H, view, view, pyoracle.fp(n_t),
+                       pyoracle.fp(p_mat), pyoracle.fp(a), pyoracle.fp(b), None)
+            res[tag] = (a, b)
+        seed = _abi.RESTIR_DEFAULT_SEED
+        rate("ris", nv, lambda: ris("cur", restir_key(seed, 1, _abi.RESTIR_STAGE_RIS, 0)))
+        ris("prev", restir_key(seed, 0, _abi.RESTIR_STAGE_RIS, 0))   # a predecessor grid for the temporal stage
+
+        def temporal():
+            a, b, _ = pyoracle.empty_reservoirs(N, nv)
+            lib.or_temporal(osc.handle, C.byref(f), restir_key(seed, 1, _abi.RESTIR_STAGE_TEMPORAL, 0), pyoracle.fp(o), W,
+                            H, view, view, pyoracle.fp(n_t), pyoracle.fp(p_mat), pyoracle.fp(res["cur"][0]),
+                            pyoracle.fp(res["cur"][1]), pyoracle.fp(res["prev"][0]), pyoracle.fp(res["prev"][1]),
+                            pyoracle.fp(a), pyoracle.fp(b), None)
+        rate("temporal", nv, temporal)
+        cur = res["cur"]
+        if passes:
+            px = 0
+            t0 = time.perf_counter()
+            for p in range(passes):
+                gp = (passes - 1 - p) * f.spatial_resample_radius
+                ry0, ry1 = max(0, y0 - gp), min(H, y0 + rows + gp)
+                pr = pyoracle.Rect(0, ry0, W, ry1 - ry0)
+                a, b, _ = pyoracle.empty_reservoirs(N, nv)
+                a[:], b[:] = cur[0], cur[1]
+                lib.or_spatial_pass(osc.handle, C.byref(f), restir_key(seed, 1, _abi.RESTIR_STAGE_SPATIAL, p),
+                                    pyoracle.fp(o), W, H, view, pr, pyoracle.fp(n_t), pyoracle.fp(p_mat),
+                                    pyoracle.fp(cur[0]), pyoracle.fp(cur[1]), pyoracle.fp(a), pyoracle.fp(b), None)
+                cur = (a, b)
+                px += pr.w * pr.h
+            dt = time.perf_counter() - t0
+            out["spatial"] = {"value": round(px * N / dt / 1e6, 6), "pixels": int(px), "seconds": round(dt, 4),
+                              "passes": passes}
+        rgb = np.zeros((rows, W, 3), np.float32)
+        rate("final", rect.w * rect.h, lambda: lib.or_final(osc.handle, C.byref(f), pyoracle.fp(o), W, H, view, rect,
+                                                            pyoracle.fp(n_t), pyoracle.fp(p_mat), pyoracle.fp(cur[0]),
+                                                            pyoracle.fp(cur[1]), pyoracle.fp(rgb)))
+    finally:
+        pyoracle.set_rng_mode(False)
+    out["rows"] = {"owned": rows, "view": view.h, "of": [W, H]}
+    return out
+
+
+def restir_key(seed, frame, stage, pass_):
+    from romis_amd import restir
+    return restir.rng_key(seed, frame, stage, pass_)
+
+
+def cpu_stages(cf_name, sc_fn, cam_fn, features_fn, threads):
+    """cpu_baseline.stages: per-stage oracle rates for C1 and C2 (BASELINE.md's per-stage CPU baseline), keyed RNG
+    and the reference's own generators, on bounded bands (the reference generators serialise on rand()'s lock)."""
+    out = {"cores": threads, "unit": "Mpixel-reservoirs/s"}
+    for name in ("c1", "c2"):
+        cf = CONFIGS[name]
+        W, H = cf.get("image") or cf["tile"]
+        sc = sc_fn(cf["scene"])
+        cam = cam_fn(cf["scene"], W, H)
+        f = features_fn(cf)
+        rows_keyed = min(H, max(8, 1036800 // W))
+        out[name] = {"keyed": cpu_stage_baseline(sc, cam, f, W, H, rows_keyed, False),
+                     "reference_rng": cpu_stage_baseline(sc, cam, f, W, H, max(16, rows_keyed // 16), True)}
+    return out
 
 
 # BASELINE.json configs.  "weak": each rank owns a tile x tile_h tile of a (tx*tile) x (ty*tile_h) image;
@@ -389,6 +512,8 @@ def main():
     # GPU pre-warm (not a frame, not timed): streaming reads over 4 GiB bring an idle box's clocks up before the
     # warm-up frames, and give the practical HBM-read ceiling reported beside the roofline
     measured = r.measure_read_bandwidth(4 << 30, max(1, args.prewarm)) if args.prewarm > 0 else None
+    if args.prewarm_gemm_ms > 0:
+        gemm_prewarm(torch, local, args.prewarm_gemm_ms)
     for _ in range(args.warmup):
         step()
     # Timed region: the spatial kernel (the roofline's) carries a HIP start / stop event pair recorded inside its
@@ -454,6 +579,14 @@ def main():
     if rank == 0 and world == 1 and args.cpu_baseline:
         rows = args.cpu_rows or min(GH, max(8, 1036800 // GW))   # ~1 Mpx of the workload, ~0.3 s on 16 cores
         cpu = cpu_baseline(sc, lambda w, h: scene.camera_for(cf["scene"], w, h), f, rows, GW, GH)
+        if args.cpu_stages:
+            def feats(c):   # the config's frame at N, k, r of this run
+                return _abi.default_features(initial_light_samples=c["M"], num_samples_in_reservoir=args.N,
+                                             num_neighbours_to_sample=args.k, spatial_resample_radius=args.r,
+                                             spatial_resampling_passes=c["passes"],
+                                             spatial_reuse=1 if c["passes"] > 0 else 0, temporal_reuse=c["temporal"],
+                                             unbiased_combination=c["unbiased"], spatial_reuse_visibility_check=c["vis"])
+            cpu["stages"] = cpu_stages(args.config, scene.bench_scene, scene.camera_for, feats, cpu["cores"])
 
     kernels = {k: {"us_per_launch": round(v[0] / v[1] * 1e3, 2) if v[1] else None, "launches": int(v[1])}
                for k, v in kt_all.items()}

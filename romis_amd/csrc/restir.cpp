@@ -280,6 +280,7 @@ struct restir_ctx {
     std::vector<hipEvent_t> free_events;
     double ms[RESTIR_K_COUNT] = {0};
     uint64_t launches[RESTIR_K_COUNT] = {0};
+    uint64_t timing_seq[RESTIR_K_COUNT] = {0};   // launches seen per kernel (timing.every sampling)
 };
 
 // ---------------------------------------------------------------------------------------------------------
@@ -606,6 +607,7 @@ restir_status timed_begin(restir_ctx* c, int kernel, Pending& p) {
     p.start = p.stop = nullptr;
     set_launch_events(nullptr, nullptr);
     if (!c->timing || !((c->tuning.timing_mask >> kernel) & 1u)) return RESTIR_OK;
+    if (c->tuning.timing_every > 1u && (c->timing_seq[kernel]++ % c->tuning.timing_every) != 0u) return RESTIR_OK;
     for (hipEvent_t* e : {&p.start, &p.stop}) {
         if (!c->free_events.empty()) { *e = c->free_events.back(); c->free_events.pop_back(); }
         else HIP_TRY(timing_event_create(c, e));
@@ -2150,6 +2152,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.th")) { if (v > 2) return fail(RESTIR_ERR_INVALID, "spatial.th: 0 (auto), 1 or 2"); t.spatial_th = v; }
     else if (!std::strcmp(key, "fuse.primary_ris")) t.fuse_primary_ris = v;
     else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;
+    else if (!std::strcmp(key, "timing.every")) { t.timing_every = v ? v : 1u; for (auto& q : c->timing_seq) q = 0; }
     else if (!std::strcmp(key, "timing.fence")) {
         // the pooled events carry the old flags: drop the free ones (recreated on demand)
         if (t.timing_fence != v) {

@@ -58,6 +58,18 @@ VARIANTS = {
                    (r"rand01\(draw\(ps, 4u \* c \+ 3u\)\)", "0.5f")],
     "ris_no_update": [(r"res_update<NT>\(r, N, pos, col, weight\(pd\), rand01\(draw\(ps, 4u \* c \+ 3u\)\), pd\);",
                        "r[0].wsum += weight(pd); r[0].pos = vadd(r[0].pos, pos);")],
+    # round 4: what the keyed hash itself costs with the light fetch still random per lane --
+    # the draws as the bare Weyl sequence ps + slot * G (no mixing), as a one-multiply xorshift-multiply-xorshift,
+    # and the light index by shift (umulhi(d, L) == d >> 25 exactly for L = 128, C2's point lights)
+    "ris_rng_weyl": [(r"uniform_index\(draw\(ps, 4u \* c\), L\)", "uniform_index(ps + 4u * c * 0x9E3779B9u, L)"),
+                     (r"rand01\(draw\(ps, 4u \* c \+ 3u\)\)", "rand01(ps + (4u * c + 3u) * 0x9E3779B9u)")],
+    "ris_rng_1mul": [(r"uniform_index\(draw\(ps, 4u \* c\), L\)", "uniform_index(draw1(ps, 4u * c), L)"),
+                     (r"rand01\(draw\(ps, 4u \* c \+ 3u\)\)", "rand01(draw1(ps, 4u * c + 3u))"),
+                     (r"const uint32_t ps = pix_state\(key, y \* rg\.W \+ x\);",
+                      "const uint32_t ps = pix_state(key, y * rg.W + x);\n"
+                      "            auto draw1 = [](uint32_t ps_, uint32_t slot) { uint32_t h = ps_ + slot * 0x9E3779B9u; "
+                      "h ^= h >> 16; h *= 0x7feb352du; return h ^ (h >> 15); };")],
+    "ris_lidx_shift": [(r"uniform_index\(draw\(ps, 4u \* c\), L\)", "(draw(ps, 4u * c) >> 25)")],
     # pieces of the target pdf itself (shared device functions: every kernel changes, RIS is the one timed)
     "risg_no_pow": [(r"return pow_pre\(x, px, pw, job\) \? pw : pow_core\(tb, job, px\.kd_sh\.w\);",
                      "return x * px.kd_sh.w;")],

@@ -378,6 +378,30 @@ __device__ __forceinline__ float target_pdf(const SceneDev& s, const FeaturesDev
     return vlength(shade_ref(s, f, px, lpos, lcol, tb));
 }
 
+// target_pdf(...) > 0.0f, exactly, without the tail of computeShading where the comparison is decided before it
+// (the unbiased combine's Z, reservoir.cpp:84-96, needs only the sign).  For a ks = 0 material (ROMIS_POW_SKIP:
+// the specular term is a +-0 vector) in a scene whose colour x reflectance products are finite, with
+// a finite dotNL >= 0: the shaded vector is v_c = RN(RN(A_c dotNL) / D), A_c = lcol_c kd_c, D = RN(d' d') (d' = 1
+// below 1e-5); p = sqrt(sum RN(v_c^2)) is > 0 iff some RN(v_c^2) > 0, i.e. some |v_c| > 2^-75.  RN is monotone, so
+// max |v_c| = RN(e / D) with e = RN(max |A_c| dotNL); e > 2^-60 D decides true and e < 2^-90 D false (2^15 of margin
+// against any rounding); anything else -- other materials, non-finite or tiny values -- takes the full evaluation.
+__device__ __forceinline__ bool target_pdf_positive(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,
+                                                    const GlTabs& tb) {
+    if (f.shading && s.shade_finite && __float_as_uint(px.ks_pm.w) == ROMIS_POW_SKIP) {
+        const ShadePre sp = shade_pre(px, lpos);
+        if (sp.dotNL < 0.0f) return false;   // computeShading's back-facing exit: the zero vector
+        if (__builtin_isfinite(sp.dotNL)) {
+            const float A = fmaxf(fmaxf(fabsf(lcol.x * px.kd_sh.x), fabsf(lcol.y * px.kd_sh.y)), fabsf(lcol.z * px.kd_sh.z));
+            const float e = A * sp.dotNL;
+            const float dd = fabsf(sp.d) < 1e-5f ? 1.0f : sp.d;
+            const float D = dd * dd;
+            if (e > 0x1p-60f * D) return true;
+            if (e < 0x1p-90f * D) return false;
+        }
+    }
+    return target_pdf(s, f, px, lpos, lcol, tb) > 0.0f;
+}
+
 // The block's LDS copy of powf's two tables (512 B): every p-hat evaluation indexes them twice per lane, and from
 // __constant__ memory each index is a vector-memory round trip in the middle of the dependent chain (two per
 // target pdf); from LDS it is a ds_read.  Every thread of the block must call this (it ends with a barrier).
@@ -1077,8 +1101,9 @@ __device__ __forceinline__ void spatial_pixel(const SceneDev& s, const Region& r
             unsigned long long tot = 0;
             for (uint32_t j = 0; j < N; j++) tot += __float_as_uint(ib[ridx(rg, j, q)].w);
             for (uint32_t j = 0; j < N; j++) {
-                const float pd = target_pdf(s, f, rp, cmb.out[j].pos, cmb.out[j].col);
-                if (pd > 0.0f && (!f.spatial_vis || visible(bvh, rp.P, cmb.out[j].pos))) Z[j] += tot;
+                if (target_pdf_positive(s, f, rp, cmb.out[j].pos, cmb.out[j].col, gl_global_tabs()) &&
+                    (!f.spatial_vis || visible(bvh, rp.P, cmb.out[j].pos)))
+                    Z[j] += tot;
             }
         }
         for (uint32_t j = 0; j < N; j++) {
@@ -1325,171 +1350,11 @@ __device__ __forceinline__ void spatial1_body(const SceneDev& s, const Region& r
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// k_spatial1_lds: the N = 1 biased pass with the tile's neighbourhood staged in LDS (north_star's screen-tile
-// staging).  The global-gather form is bound by its scattered accesses, not its arithmetic: every neighbour
-// costs three 16-byte gathers whose 64 lanes touch ~64 distinct cache lines each (a pass with the target pdfs
-// cut to a third took 92 of 99 us; removing the pixel's own pdf changed nothing).  Here a 256-thread block
-// owns a 32x8 tile and first copies the records of the tile grown by R -- (32 + 2R) x (8 + 2R) pixels of
-// n_t, res_a, res_b, 48 B each, 70 KB at R = 10 -- with row-coalesced loads into LDS; every neighbour read is
-// then an LDS read.  Two blocks fit a CU (2 waves per SIMD), so the kernel leans on instruction-level
-// parallelism instead of occupancy: the K neighbour target pdfs are independent of each other (only the
-// reservoir updates are ordered), so they are evaluated side by side before the ordered updates run.
-// Same arithmetic, RNG slots and update order as spatial1_pixel; R <= kLdsSpatialR (host check).
+// Screen-tile staging for the N = 1 / 2 biased passes: the tile's neighbourhood window, R <= kLdsSpatialR (host check).
+// (Round 4 removed k_spatial1_lds / k_spatial1_ldsr, which staged the reservoirs too -- 70 / 46 KB per block, measured
+// 130 / 106 us against 82 for n_t alone at C2, profiles/r2 -- their source is profiles/r4/pruned/spatial1_lds.diff.)
 constexpr uint32_t kLdsSpatialR = 10;
 constexpr uint32_t kApronMax = (kTileW + 2u * kLdsSpatialR) * (kTileH + 2u * kLdsSpatialR);   // 1456 px
-
-template <bool DBG, bool STAGE_NT>
-__device__ __forceinline__ void spatial1_lds_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
-                                                  v3 origin, const float4* __restrict__ n_t,
-                                                  const float4* __restrict__ p_mat, const float4* __restrict__ ia,
-                                                  const float4* __restrict__ ib, float4* __restrict__ oa,
-                                                  float4* __restrict__ ob, float2* __restrict__ odbg,
-                                                  const float* __restrict__ rp_in, float* __restrict__ rp_out) {
-    // STAGE_NT = false: only the reservoirs are staged (32 B per pixel, 3 blocks per CU); the neighbours'
-    // n_t records are gathered from global memory together with the staging loads (one round trip either way)
-    float4* const l_a = g_lds;
-    float4* const l_b = g_lds + kApronMax;
-    float4* const l_nt = g_lds + 2u * kApronMax;
-    uint32_t tile;
-    if (!xcd_tile(rg, num_tiles(rg), blockIdx.x, tile)) return;   // block-uniform
-    const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
-    const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTileH);
-    // neighbour clamp bounds (render_utils.cpp:109-110: the image; here also the stored view), global coords
-    const int xlo = max(0, (int)rg.vx0), xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1;
-    const int ylo = max(0, (int)rg.vy0), yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1;
-    const int R = (int)f.R;
-    // the staged rectangle: the tile grown by R, clipped to the clamp bounds (every neighbour lies inside)
-    const int ax0 = max(tx0 - R, xlo), ax1 = min(tx0 + (int)kTileW - 1 + R, xhi);
-    const int ay0 = max(ty0 - R, ylo), ay1 = min(ty0 + (int)kTileH - 1 + R, yhi);
-    const uint32_t AW = (uint32_t)(ax1 - ax0 + 1), n_apron = AW * (uint32_t)(ay1 - ay0 + 1);
-    // this lane's pixel: waves are 8x8 blocks of the tile (rg.map2d = 2)
-    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
-    const int x = tx0 + (int)(w * 8u + (l & 7u)), y = ty0 + (int)(l >> 3);
-    const bool live = x < (int)(rg.rx0 + rg.rw) && y < (int)(rg.ry0 + rg.rh);
-    const uint32_t pofs = ((uint32_t)(y - (int)rg.vy0) * rg.vw + (uint32_t)(x - (int)rg.vx0)) << 4;
-    // own records that are not staged, issued first
-    float4 cpm = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    float pd_cached = 0.0f;
-    if (live) {
-        cpm = ld_at(p_mat, pofs);
-        if (rp_in) pd_cached = ld_at(rp_in, pofs >> 2);
-    }
-    // stage: at most ceil(1456 / 256) = 6 pixels per thread, all loads in flight before the LDS stores
-    {
-        constexpr uint32_t kPer = (kApronMax + 255u) / 256u;
-        const uint32_t magic = 0xFFFFFFFFu / AW + 1u;   // i / AW for i < 2^16 (checked below)
-        float4 va[kPer], vb[kPer], vn[kPer];
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; k++) {
-            const uint32_t i = threadIdx.x + 256u * k;
-            if (i < n_apron) {
-                uint32_t r = __umulhi(i, magic);
-                if (r * AW > i) r--;
-                const uint32_t c = i - r * AW;
-                const uint32_t g = (((uint32_t)(ay0 - (int)rg.vy0) + r) * rg.vw + (uint32_t)(ax0 - (int)rg.vx0) + c) << 4;
-                if (STAGE_NT) vn[k] = ld_at(n_t, g);
-                va[k] = ld_at(ia, g);
-                vb[k] = ld_at(ib, g);
-            }
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; k++) {
-            const uint32_t i = threadIdx.x + 256u * k;
-            if (i < n_apron) {
-                if (STAGE_NT) l_nt[i] = vn[k];
-                l_a[i] = va[k];
-                l_b[i] = vb[k];
-            }
-        }
-    }
-    // neighbour draws while the staging loads are in flight
-    const uint32_t K = f.K;   // <= kLeanK (host check)
-    const uint32_t ps = pix_state(key, (uint32_t)y * rg.W + (uint32_t)x);
-    const uint32_t span = 2u * f.R + 1u;
-    uint32_t qi[kLeanK];
-    float4 gq[kLeanK];
-#pragma unroll
-    for (uint32_t n = 0; n < kLeanK; n++) {
-        qi[n] = 0u;
-        if (n < K) {
-            const int nx = min(max(x - R + (int)__umulhi(draw(ps, 2u * n), span), xlo), xhi);
-            const int ny = min(max(y - R + (int)__umulhi(draw(ps, 2u * n + 1u), span), ylo), yhi);
-            qi[n] = (uint32_t)(ny - ay0) * AW + (uint32_t)(nx - ax0);
-            if (!STAGE_NT && live)
-                gq[n] = ld_at(n_t, ((uint32_t)(ny - (int)rg.vy0) * rg.vw + (uint32_t)(nx - (int)rg.vx0)) << 4);
-        }
-    }
-    float4 cn_g = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (!STAGE_NT && live) cn_g = ld_at(n_t, pofs);
-    __syncthreads();
-    if (!live) return;   // no barrier follows
-    const uint32_t ci = (uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0);
-    const float4 cn = STAGE_NT ? l_nt[ci] : cn_g, ca = l_a[ci], cb = l_b[ci];
-    const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
-    // primary-ray miss: the pass's result is known (spatial1_pixel)
-    if (cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z) &&
-        __builtin_isfinite(ca.w) && __builtin_isfinite(cb.x + cb.y + cb.z)) {
-        st_at(oa, pofs, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-        st_at(ob, pofs, make_float4(0.0f, 0.0f, 0.0f, cb.w));
-        if (DBG) st_at(odbg, pofs >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
-        if (rp_out) st_at(rp_out, pofs >> 2, 0.0f);
-        return;
-    }
-    // depth / normal heuristic (render_utils.cpp:114-118), one shared reciprocal of the pixel's depth
-    const double rt = rcp_d(cur.t);
-    const bool rt_ok = div_fast_ok(cur.t);
-    bool ok[kLeanK];
-    float4 na[kLeanK], nb[kLeanK];
-    float pd[kLeanK];
-#pragma unroll
-    for (uint32_t n = 0; n < kLeanK; n++) {
-        ok[n] = false;
-        if (n < K) {
-            const float4 g = STAGE_NT ? l_nt[qi[n]] : gq[n];
-            na[n] = l_a[qi[n]];
-            nb[n] = l_b[qi[n]];
-            const float nd = vdot(xyz(g), cur.N);
-            float q = div_by_rcp_d(g.w, rt);
-            if (!rt_ok) q = g.w / cur.t;
-            ok[n] = !(nd < 0.90630778703f) && !(fabsf(1.0f - q) > 0.1f);
-        }
-    }
-    // the K target pdfs, independent of each other: evaluated side by side (rejected lanes' values unused)
-#pragma unroll
-    for (uint32_t n = 0; n < kLeanK; n++)
-        if (n < K) pd[n] = target_pdf(s, f, cur, xyz(na[n]), xyz(nb[n]));
-    const float pd_cur = rp_in ? pd_cached : target_pdf(s, f, cur, xyz(ca), xyz(cb));
-    Comb1 cmb;
-    cmb.pos = mk(0.0f, 0.0f, 0.0f); cmb.col = mk(0.0f, 0.0f, 0.0f);
-    cmb.wsum = ROMIS_FLT_MIN; cmb.chosen = 0.0f; cmb.pd = 0.0f; cmb.macc = 0u; cmb.has_pd = false;
-    cmb.h = ps + 2u * K * 0x9E3779B9u;
-#pragma unroll
-    for (uint32_t n = 0; n < kLeanK; n++)
-        if (n < K && ok[n]) cmb.take(pd[n], na[n].w, __float_as_uint(nb[n].w), xyz(na[n]), xyz(nb[n]));
-    cmb.take(pd_cur, ca.w, __float_as_uint(cb.w), xyz(ca), xyz(cb));
-    float p = cmb.pd;
-    if (!cmb.has_pd) p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, cmb.pos, cmb.col);
-    const float W = contribution_weight(p, cmb.macc, cmb.wsum);
-    st_at(oa, pofs, make_float4(cmb.pos.x, cmb.pos.y, cmb.pos.z, W));
-    st_at(ob, pofs, make_float4(cmb.col.x, cmb.col.y, cmb.col.z, __uint_as_float(cmb.macc)));
-    if (DBG) st_at(odbg, pofs >> 1, make_float2(cmb.wsum, cmb.chosen));
-    if (rp_out) st_at(rp_out, pofs >> 2, p);
-}
-
-#ifndef ROMIS_SPATIAL1_LDS_WPE
-#define ROMIS_SPATIAL1_LDS_WPE 2
-#endif
-#define ROMIS_SPATIAL1_LDS_KERNEL(DBG, STAGE_NT, WPE, NAME)                                                           \
-    extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void                        \
-    NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
-         const float4* p_mat, const float4* ia, const float4* ib, float4* oa, float4* ob, float2* odbg,               \
-         const float* rp_in, float* rp_out) {                                                                         \
-        spatial1_lds_body<DBG, STAGE_NT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out); \
-    }
-ROMIS_SPATIAL1_LDS_KERNEL(false, true, ROMIS_SPATIAL1_LDS_WPE, k_spatial1_lds)
-ROMIS_SPATIAL1_LDS_KERNEL(true, true, ROMIS_SPATIAL1_LDS_WPE, k_spatial1_lds_dbg)
-ROMIS_SPATIAL1_LDS_KERNEL(false, false, 3, k_spatial1_ldsr)
-ROMIS_SPATIAL1_LDS_KERNEL(true, false, 3, k_spatial1_ldsr_dbg)
 
 // k_spatial1_ntl: the N = 1 biased pass with only the tile's n_t neighbourhood staged in LDS.  The rocprof
 // counters of k_spatial1 (profiles/r2/r2q) put its bound in the vector-memory pipeline, not in HBM or VALU:
@@ -2123,8 +1988,9 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
             if (n < K) {
                 const float4 qn = ld_at(n_t, qo[n]), qp = ld_at(p_mat, qo[n]);
                 const Px rp = make_px(s, qn, qp, origin, qo[n] >> 4);
-                const float pd = (src == n && rp_nb) ? ld_at(rp_nb, qo[n] >> 2) : target_pdf(s, f, rp, cmb.pos, cmb.col, tb);
-                if (pd > 0.0f && (!VIS || visible(bvh, rp.P, cmb.pos))) Z += Mn[n];
+                const bool pos = (src == n && rp_nb) ? ld_at(rp_nb, qo[n] >> 2) > 0.0f
+                                                     : target_pdf_positive(s, f, rp, cmb.pos, cmb.col, tb);
+                if (pos && (!VIS || visible(bvh, rp.P, cmb.pos))) Z += Mn[n];
             }
         }
         if (pc > 0.0f && (!VIS || visible(bvh, cur.P, cmb.pos))) Z += __float_as_uint(cb.w);
@@ -3286,29 +3152,6 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
 #endif
             ROMIS_LAUNCH(odbg ? k_spatial1_ntl_dbg : k_spatial1_ntl, dim3(grid), dim3(kBlock),
                          kApronMax * 16u + ROMIS_NTL_EXTRA_LDS, stream,
-                         s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
-        } else if (tu.spatial_lds == 2u && f.R <= kLdsSpatialR) {
-            ROMIS_LAUNCH(odbg ? k_spatial1_ldsr_dbg : k_spatial1_ldsr, dim3(grid), dim3(kBlock), 2u * kApronMax * 16u, stream,
-                         s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
-        } else if (tu.spatial_lds && f.R <= kLdsSpatialR) {
-            // > 64 KB of dynamic LDS must be requested per kernel and device, once (contexts on several threads
-            // may get here together)
-            static std::mutex mu;
-            static std::set<int> devices_set;
-            int dev = 0;
-            hipError_t e = hipGetDevice(&dev);
-            if (e != hipSuccess) return e;
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                if (!devices_set.count(dev)) {
-                    for (const void* k : {(const void*)k_spatial1_lds, (const void*)k_spatial1_lds_dbg}) {
-                        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(3u * kApronMax * 16u));
-                        if (e != hipSuccess) return e;
-                    }
-                    devices_set.insert(dev);
-                }
-            }
-            ROMIS_LAUNCH(odbg ? k_spatial1_lds_dbg : k_spatial1_lds, dim3(grid), dim3(kBlock), 3u * kApronMax * 16u, stream,
                          s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
         } else {
             ROMIS_LAUNCH(odbg ? k_spatial1_dbg : k_spatial1, dim3(grid), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1],

@@ -2146,7 +2146,12 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.xcd")) t.spatial_xcd = v;
     else if (!std::strcmp(key, "spatial.blocks")) t.spatial_blocks = v;
     else if (!std::strcmp(key, "spatial.xcd_rows")) t.spatial_xcd_rows = v;
-    else if (!std::strcmp(key, "spatial.lds")) t.spatial_lds = v;
+    else if (!std::strcmp(key, "spatial.lds")) {
+        if (v == 1u || v == 2u || v > 4u)
+            return fail(RESTIR_ERR_INVALID, "spatial.lds: 0 (gathers), 3 (n_t window, default) or 4 (two lanes per pixel); "
+                                            "1 / 2 were removed in round 4");
+        t.spatial_lds = v;
+    }
     else if (!std::strcmp(key, "spatial.wave8")) t.spatial_wave8 = v;
     else if (!std::strcmp(key, "spatial.lean")) t.spatial_lean = v;
     else if (!std::strcmp(key, "spatial.th")) { if (v > 2) return fail(RESTIR_ERR_INVALID, "spatial.th: 0 (auto), 1 or 2"); t.spatial_th = v; }

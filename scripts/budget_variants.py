@@ -70,6 +70,13 @@ VARIANTS = {
                       "            auto draw1 = [](uint32_t ps_, uint32_t slot) { uint32_t h = ps_ + slot * 0x9E3779B9u; "
                       "h ^= h >> 16; h *= 0x7feb352du; return h ^ (h >> 15); };")],
     "ris_lidx_shift": [(r"uniform_index\(draw\(ps, 4u \* c\), L\)", "(draw(ps, 4u * c) >> 25)")],
+    # light grids (C4 / C5): no light-table read at all -- the drawn light's corner from its index by arithmetic
+    # (the upper bound of a closed-form regularLightGrid corner), its colour a constant
+    "ris_grid_noload": [(r"pos = vadd\(vadd\(xyz\(lt\[0\]\), vscale\(shared_row\(1\), a\)\), vscale\(shared_row\(2\), b\)\);\n"
+                         r"(\s+)const v3 gc = xyz\(lt\[1\]\);",
+                         "const uint32_t li_ = (uint32_t)(lt - lights) >> 1; "
+                         "pos = vadd(vadd(mk((float)(li_ >> 6) * 0.01f, 0.9f, (float)(li_ & 63u) * 0.01f), "
+                         "vscale(shared_row(1), a)), vscale(shared_row(2), b));\n\\1const v3 gc = mk(0.5f, 0.5f, 0.5f);")],
     # pieces of the target pdf itself (shared device functions: every kernel changes, RIS is the one timed)
     "risg_no_pow": [(r"return pow_pre\(x, px, pw, job\) \? pw : pow_core\(tb, job, px\.kd_sh\.w\);",
                      "return x * px.kd_sh.w;")],

@@ -40,8 +40,6 @@ VARIANTS = {
     "ris_q1024": {"ris.queue": 1024},
     "spatial_noxcd": {"spatial.xcd": 0},
     "spatial_band": {"spatial.xcd_rows": 0},
-    "spatial_lds": {"spatial.lds": 1},
-    "spatial_ldsr": {"spatial.lds": 2},
     "spatial_gather": {"spatial.lds": 0},
 
     "spatial_rows1": {"spatial.xcd_rows": 1},

@@ -198,12 +198,9 @@ def test_temporal_bit_exact(gpu, oracle, N, clamp):
 
 
 # spatial kernels of an N = 1 biased pass: k_spatial1 (gathers; XCD order in 4-row chunks or one band),
-# k_spatial1_lds (n_t + reservoirs staged in LDS), k_spatial1_ldsr (reservoirs staged), k_spatial1_ntl (n_t
-# staged, the default; _t2: 32x16 tiles), the general kernel
+# k_spatial1_ntl (n_t staged, the default; _t2: 32x16 tiles), k_spatial1_x2 (two lanes per pixel), the general kernel
 SPATIAL_VARIANTS = {"gather": {"spatial.lean": 1, "spatial.lds": 0},
                     "gather_band": {"spatial.lean": 1, "spatial.lds": 0, "spatial.xcd_rows": 0},
-                    "lds": {"spatial.lean": 1, "spatial.lds": 1},
-                    "ldsr": {"spatial.lean": 1, "spatial.lds": 2},
                     "ntl": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 1},
                     "ntl_rows2": {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 2},
                     "ntl_t2": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 2},

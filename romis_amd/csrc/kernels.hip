@@ -763,12 +763,31 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 }
             };
             auto weight = [&](float pd) { return s.light_scale != 0.0f ? pd * s.light_scale : pd / invL; };  // light.cpp:80
-            uint32_t c = 0;
-            for (; c < c_end; c++) {
-                v3 pos, col;
-                sample(c, pos, col);
-                const float pd = target_pdf(s, f, px, pos, col, tb);
-                res_update<NT>(r, N, pos, col, weight(pd), rand01(draw(ps, 4u * c + 3u)), pd);
+            if (NT == 1) {
+                // Reservoir::update (reservoir.cpp:10-32) keeping the accepted candidate's index instead of its
+                // sample: the sample is a function of the candidate's draws (slots 4c .. 4c + 2), so it is drawn
+                // again once after the loop -- two selects per candidate instead of nine
+                uint32_t best = 0xFFFFFFFFu;
+                for (uint32_t c = 0; c < c_end; c++) {
+                    v3 pos, col;
+                    sample(c, pos, col);
+                    const float pd = target_pdf(s, f, px, pos, col, tb);
+                    const float w = weight(pd);
+                    r[0].M += 1u;
+                    r[0].wsum += w;
+                    if (rand01(draw(ps, 4u * c + 3u)) < (w / r[0].wsum)) { best = c; r[0].chosen = w; r[0].pd = pd; }
+                }
+                if (best != 0xFFFFFFFFu) {
+                    sample(best, r[0].pos, r[0].col);
+                    r[0].has_pd = true;
+                }
+            } else {
+                for (uint32_t c = 0; c < c_end; c++) {
+                    v3 pos, col;
+                    sample(c, pos, col);
+                    const float pd = target_pdf(s, f, px, pos, col, tb);
+                    res_update<NT>(r, N, pos, col, weight(pd), rand01(draw(ps, 4u * c + 3u)), pd);
+                }
             }
             for (uint32_t j = 0; j < N; j++) {
                 // the held sample's target pdf: W's p-hat (light.cpp:90-93) and, N = 1, the pdf cache rp
@@ -1372,10 +1391,10 @@ constexpr uint32_t kApronMax = (kTileW + 2u * kLdsSpatialR) * (kTileH + 2u * kLd
 // for them (explicit s_waitcnt vmcnt(0)) before its barrier, so after it every wave may read every entry.
 // TH: tile height in 8-row units (blocks of 256 TH threads, a (32 + 2R) x (8 TH + 2R) window).
 constexpr uint32_t apron_max(uint32_t TH) { return (kTileW + 2u * kLdsSpatialR) * (kTileH * TH + 2u * kLdsSpatialR); }
-template <uint32_t TH = 1, uint32_t kThreads = 256u * TH>
+template <uint32_t TH = 1>
 __device__ __forceinline__ void ntl_stage_window(const Region& rg, const float4* __restrict__ n_t, float4* l_nt, int ax0,
                                                  int ay0, uint32_t AW, uint32_t n_apron) {
-    constexpr uint32_t kPer = (apron_max(TH) + kThreads - 1u) / kThreads;
+    constexpr uint32_t kThreads = 256u * TH, kPer = (apron_max(TH) + kThreads - 1u) / kThreads;
     const uint32_t magic = 0xFFFFFFFFu / AW + 1u;
     const uint32_t w64 = (threadIdx.x >> 6) << 6;
 #pragma unroll
@@ -1533,189 +1552,6 @@ ROMIS_SPATIAL1_NTL_KERNEL(true, k_spatial1_ntl_dbg)
     }
 ROMIS_SPATIAL1_T2_KERNEL(false, k_spatial1_ntl_t2)
 ROMIS_SPATIAL1_T2_KERNEL(true, k_spatial1_ntl_t2_dbg)
-
-// k_spatial1_x2: the N = 1 biased pass with each pixel's K + 1 inputs spread over two lanes (north_star's cross-lane
-// WRS).  A 512-thread block owns a 32x8 tile (the window of k_spatial1_ntl, LDS-DMA-staged by all
-// 512 threads); wave w covers the tile's 8x4 block (w & 3, w >> 2), lanes 2i and 2i + 1 the block's pixel i.  Lane
-// half 0 takes the inputs 0 .. ka - 1 (ka = ceil(K / 2)), half 1 the inputs ka .. K - 1 and the pixel's own: each
-// lane draws its neighbours, tests them, gathers the accepted ones' reservoirs (all in flight at once) and evaluates
-// their target pdfs -- the K + 1 independent p-hat chains run two lanes wide.  The reservoir update stays the
-// reference's serial prefix in input order (reservoir.cpp:10-32): half 0 runs its part from wSum = FLT_MIN, hands
-// its wSum and its count of taken inputs (the accept draw's slot) to half 1 by DPP, half 1 continues from there;
-// the later accept wins, the M sum is the two halves' sum.  Same arithmetic, RNG slots and update order as
-// spatial1_pixel.  Half 0 stores res_a, half 1 res_b (and the debug / pdf-cache planes).
-constexpr uint32_t kX2Slots = (kLeanK + 2u) / 2u;   // inputs per lane: ceil((K + 1) / 2) <= 3 for K <= 5
-__device__ __forceinline__ float x2_from_even(float v) {   // lane 2i + 1 reads lane 2i (quad_perm [0, 0, 2, 2])
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xA0, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float x2_from_odd(float v) {    // lane 2i reads lane 2i + 1 (quad_perm [1, 1, 3, 3])
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xF5, 0xF, 0xF, false));
-}
-__device__ __forceinline__ uint32_t x2_from_even_u(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false); }
-
-template <bool DBG>
-__device__ __forceinline__ void spatial1_x2_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
-                                                 v3 origin, const float4* __restrict__ n_t,
-                                                 const float4* __restrict__ p_mat, const float4* __restrict__ ia,
-                                                 const float4* __restrict__ ib, float4* __restrict__ oa,
-                                                 float4* __restrict__ ob, float2* __restrict__ odbg,
-                                                 const float* __restrict__ rp_in, float* __restrict__ rp_out) {
-    const GlTabs tb = gl_stage_tables<false>();   // made visible by the window's barrier below
-    float4* const l_nt = g_lds;
-    uint32_t tile;
-    const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
-    if (!xcd_tile(rg, ntx * ((rg.rh + kTileH - 1) / kTileH), blockIdx.x, tile)) return;   // block-uniform
-    const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTileH);
-    const int xlo = max(0, (int)rg.vx0), xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1;
-    const int ylo = max(0, (int)rg.vy0), yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1;
-    const int R = (int)f.R;
-    const int ax0 = max(tx0 - R, xlo), ax1 = min(tx0 + (int)kTileW - 1 + R, xhi);
-    const int ay0 = max(ty0 - R, ylo), ay1 = min(ty0 + (int)kTileH - 1 + R, yhi);
-    const uint32_t AW = (uint32_t)(ax1 - ax0 + 1), n_apron = AW * (uint32_t)(ay1 - ay0 + 1);
-    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u, hf = l & 1u, pl = l >> 1;
-    const int x = tx0 + (int)((w & 3u) * 8u + (pl & 7u)), y = ty0 + (int)((w >> 2) * 4u + (pl >> 3));
-    const bool live = x < (int)(rg.rx0 + rg.rw) && y < (int)(rg.ry0 + rg.rh);
-    const uint32_t pofs = ((uint32_t)(y - (int)rg.vy0) * rg.vw + (uint32_t)(x - (int)rg.vx0)) << 4;
-    float4 cpm = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ca = cpm, cb = cpm;
-    float pd_cached = 0.0f;
-    if (live) {
-        cpm = ld_at(p_mat, pofs);
-        ca = ld_at(ia, pofs);
-        cb = ld_at(ib, pofs);
-        if (rp_in && hf) pd_cached = ld_at(rp_in, pofs >> 2);
-    }
-    ntl_stage_window<1, 512>(rg, n_t, l_nt, ax0, ay0, AW, n_apron);
-    const uint32_t K = f.K;   // <= kLeanK (host check)
-    const uint32_t ka = (K + 1u) / 2u;
-    const uint32_t i0 = hf ? ka : 0u;                 // this lane's first input
-    const uint32_t i1 = hf ? K + 1u : ka;             // one past its last (input K = the pixel's own)
-    const uint32_t ps = pix_state(key, (uint32_t)y * rg.W + (uint32_t)x);
-    const uint32_t span = 2u * f.R + 1u;
-    uint32_t qi[kX2Slots], qo[kX2Slots];
-#pragma unroll
-    for (uint32_t k = 0; k < kX2Slots; k++) {
-        const uint32_t n = i0 + k;
-        qi[k] = 0u;
-        qo[k] = pofs;
-        if (n < i1 && n < K) {
-            const int nx = min(max(x - R + (int)__umulhi(draw(ps, 2u * n), span), xlo), xhi);
-            const int ny = min(max(y - R + (int)__umulhi(draw(ps, 2u * n + 1u), span), ylo), yhi);
-            qi[k] = (uint32_t)(ny - ay0) * AW + (uint32_t)(nx - ax0);
-            qo[k] = ((uint32_t)(ny - (int)rg.vy0) * rg.vw + (uint32_t)(nx - (int)rg.vx0)) << 4;
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's window copies, before the barrier
-    __syncthreads();
-    if (!live) return;   // both lanes of a pixel; no barrier follows
-    const float4 cn = l_nt[(uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0)];
-    const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
-    // primary-ray miss: the pass's result is known (spatial1_pixel); both lanes of the pixel take this exit
-    if (cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z) &&
-        __builtin_isfinite(ca.w) && __builtin_isfinite(cb.x + cb.y + cb.z)) {
-        if (!hf) {
-            st_at(oa, pofs, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-        } else {
-            st_at(ob, pofs, make_float4(0.0f, 0.0f, 0.0f, cb.w));
-            if (DBG) st_at(odbg, pofs >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
-            if (rp_out) st_at(rp_out, pofs >> 2, 0.0f);
-        }
-        return;
-    }
-    const double rt = rcp_d(cur.t);
-    const bool rt_all = __all(div_fast_ok(cur.t));
-    bool ok[kX2Slots];
-    float4 na[kX2Slots], nb[kX2Slots];
-#pragma unroll
-    for (uint32_t k = 0; k < kX2Slots; k++) {
-        const uint32_t n = i0 + k;
-        ok[k] = n < i1 && n == K;   // the pixel's own input (half 1's last), always combined
-        if (n < i1 && n < K) {
-            const float4 g = l_nt[qi[k]];
-            const float nd = vdot(xyz(g), cur.N);
-            float q = div_by_rcp_d(g.w, rt);
-            if (__builtin_expect(!rt_all, 0)) {
-                if (!div_fast_ok(cur.t)) q = g.w / cur.t;
-            }
-            ok[k] = !(nd < 0.90630778703f) && !(fabsf(1.0f - q) > 0.1f);
-            if (ok[k]) { na[k] = ld_at(ia, qo[k]); nb[k] = ld_at(ib, qo[k]); }
-        } else if (n == K) {
-            na[k] = ca; nb[k] = cb;
-        }
-    }
-    // the lane's target pdfs (independent of each other and of the other lane's)
-    float pd[kX2Slots];
-#pragma unroll
-    for (uint32_t k = 0; k < kX2Slots; k++) {
-        pd[k] = 0.0f;
-        const uint32_t n = i0 + k;
-        if (n == K && n < i1) pd[k] = rp_in ? pd_cached : target_pdf(s, f, cur, xyz(ca), xyz(cb), tb);
-        else if (ok[k]) pd[k] = target_pdf(s, f, cur, xyz(na[k]), xyz(nb[k]), tb);
-    }
-    // the serial reservoir update (Reservoir::update, reservoir.cpp:10-32), half 0 then half 1
-    float wsum = ROMIS_FLT_MIN;
-    uint32_t taken = 0u, macc = 0u;
-    int sel = -1;
-    float chosen = 0.0f;
-    auto chain = [&]() {
-#pragma unroll
-        for (uint32_t k = 0; k < kX2Slots; k++) {
-            if (ok[k]) {
-                const uint32_t M = __float_as_uint(nb[k].w);
-                const float wk = (pd[k] * na[k].w) * (float)M;          // reservoir.cpp:50
-                macc += M;
-                wsum += wk;
-                const float u = rand01(mix32(ps + (2u * K + taken) * 0x9E3779B9u));
-                taken++;
-                if (u < (wk / wsum)) { sel = (int)k; chosen = wk; }
-            }
-        }
-    };
-    if (!hf) chain();
-    const float wsum_a = x2_from_even(wsum);
-    const uint32_t taken_a = x2_from_even_u(taken);
-    if (hf) { wsum = wsum_a; taken = taken_a; chain(); }
-    // the held sample: half 1's last accept, else half 0's
-    v3 hp = mk(0.0f, 0.0f, 0.0f), hc = mk(0.0f, 0.0f, 0.0f);
-    float hpd = 0.0f;
-#pragma unroll
-    for (uint32_t k = 0; k < kX2Slots; k++)
-        if (sel == (int)k) { hp = xyz(na[k]); hc = xyz(nb[k]); hpd = pd[k]; }
-    const float a_px = x2_from_even(hp.x), a_py = x2_from_even(hp.y), a_pz = x2_from_even(hp.z);
-    const float a_cx = x2_from_even(hc.x), a_cy = x2_from_even(hc.y), a_cz = x2_from_even(hc.z);
-    const float a_pd = x2_from_even(hpd), a_ch = x2_from_even(chosen);
-    const uint32_t a_sel = x2_from_even_u((uint32_t)(sel + 1)), a_macc = x2_from_even_u(macc);
-    // half 1 finishes: M = routed sum, W from the held sample's target pdf (light.cpp:90-93 / reservoir.cpp:61-64);
-    // nothing accepted: the initial (0, 0) sample, whose shaded value is +-0 at a non-NaN position (W = 0)
-    float W = 0.0f;
-    if (hf) {
-        macc += a_macc;
-        bool has = sel >= 0;
-        if (!has && a_sel != 0u) {
-            hp = mk(a_px, a_py, a_pz); hc = mk(a_cx, a_cy, a_cz); hpd = a_pd; chosen = a_ch; has = true;
-        }
-        float p = hpd;
-        if (!has) p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, hp, hc, tb);
-        W = contribution_weight(p, macc, wsum);
-        st_at(ob, pofs, make_float4(hc.x, hc.y, hc.z, __uint_as_float(macc)));
-        if (DBG) st_at(odbg, pofs >> 1, make_float2(wsum, chosen));
-        if (rp_out) st_at(rp_out, pofs >> 2, p);
-    }
-    const float b_px = x2_from_odd(hp.x), b_py = x2_from_odd(hp.y), b_pz = x2_from_odd(hp.z), b_W = x2_from_odd(W);
-    if (!hf) st_at(oa, pofs, make_float4(b_px, b_py, b_pz, b_W));
-}
-
-#ifndef ROMIS_SPATIAL1_X2_WPE
-#define ROMIS_SPATIAL1_X2_WPE 6
-#endif
-#define ROMIS_SPATIAL1_X2_KERNEL(DBG, NAME)                                                                           \
-    extern "C" __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL1_X2_WPE))) void     \
-    NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
-         const float4* p_mat, const float4* ia, const float4* ib, float4* oa, float4* ob, float2* odbg,               \
-         const float* rp_in, float* rp_out) {                                                                         \
-        spatial1_x2_body<DBG>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);        \
-    }
-ROMIS_SPATIAL1_X2_KERNEL(false, k_spatial1_x2)
-ROMIS_SPATIAL1_X2_KERNEL(true, k_spatial1_x2_dbg)
 
 // k_spatial2_ntl: the biased pass for N = 2 sub-reservoirs (the reference's default, common.h:105), laid out like
 // k_spatial1_ntl (32x8 tiles in the XCD chunk order, the n_t window in LDS by LDS-DMA, one shared depth
@@ -3143,9 +2979,6 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
             ROMIS_LAUNCH(odbg ? k_spatial1_ntl_t2_dbg : k_spatial1_ntl_t2, dim3(grid), dim3(2u * kBlock),
                          apron_max(2) * 16u, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg,
                          rp_in, rp_out);
-        } else if (tu.spatial_lds == 4u && f.R <= kLdsSpatialR) {
-            ROMIS_LAUNCH(odbg ? k_spatial1_x2_dbg : k_spatial1_x2, dim3(grid), dim3(2u * kBlock), kApronMax * 16u, stream,
-                         s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
         } else if (tu.spatial_lds == 3u && f.R <= kLdsSpatialR) {
 #ifndef ROMIS_NTL_EXTRA_LDS
 #define ROMIS_NTL_EXTRA_LDS 0   // occupancy experiments (build variants): extra dynamic LDS per block

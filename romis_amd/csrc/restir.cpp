@@ -2147,9 +2147,9 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.blocks")) t.spatial_blocks = v;
     else if (!std::strcmp(key, "spatial.xcd_rows")) t.spatial_xcd_rows = v;
     else if (!std::strcmp(key, "spatial.lds")) {
-        if (v == 1u || v == 2u || v > 4u)
-            return fail(RESTIR_ERR_INVALID, "spatial.lds: 0 (gathers), 3 (n_t window, default) or 4 (two lanes per pixel); "
-                                            "1 / 2 were removed in round 4");
+        if (v != 0u && v != 3u)
+            return fail(RESTIR_ERR_INVALID, "spatial.lds: 0 (gathers) or 3 (n_t window, default); 1, 2 and 4 were measured "
+                                            "slower and removed in round 4 (profiles/r4/pruned)");
         t.spatial_lds = v;
     }
     else if (!std::strcmp(key, "spatial.wave8")) t.spatial_wave8 = v;

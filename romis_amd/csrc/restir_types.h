@@ -100,8 +100,8 @@ struct Tuning {
     uint32_t ris_compact = 1;      // N <= 2: compact light tables for point-light-only scenes and light grids (_pt /
                                    // _grid RIS kernels, kernels.hip ris_light_form)
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
-    uint32_t spatial_lds = 3;      // N = 1 biased: 3 the n_t window in LDS (k_spatial1_ntl, default), 4 two lanes per pixel
-                                   // (k_spatial1_x2), 0 no window (k_spatial1, gathers; also any R > 10)
+    uint32_t spatial_lds = 3;      // N = 1 biased: 3 the n_t window in LDS (k_spatial1_ntl, default), 0 no window
+                                   // (k_spatial1, gathers; also any R > 10)
     uint32_t spatial_xcd_rows = 255; // k_spatial1: XCD x takes every 8th chunk of this many tile rows (0: one band;
                                      // 255 = kXcdRowsAuto: as many as keep a chunk's records in one XCD's L2)
     uint32_t spatial_blocks = 0;

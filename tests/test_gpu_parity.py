@@ -198,14 +198,13 @@ def test_temporal_bit_exact(gpu, oracle, N, clamp):
 
 
 # spatial kernels of an N = 1 biased pass: k_spatial1 (gathers; XCD order in 4-row chunks or one band),
-# k_spatial1_ntl (n_t staged, the default; _t2: 32x16 tiles), k_spatial1_x2 (two lanes per pixel), the general kernel
+# k_spatial1_ntl (n_t staged, the default; _t2: 32x16 tiles), the general kernel
 SPATIAL_VARIANTS = {"gather": {"spatial.lean": 1, "spatial.lds": 0},
                     "gather_band": {"spatial.lean": 1, "spatial.lds": 0, "spatial.xcd_rows": 0},
                     "ntl": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 1},
                     "ntl_rows2": {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 2},
                     "ntl_t2": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 2},
                     "ntl_t2_band": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 2, "spatial.xcd_rows": 0},
-                    "x2": {"spatial.lean": 1, "spatial.lds": 4, "spatial.th": 1},
                     "general": {"spatial.lean": 0}}
 SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 255, "spatial.th": 0}
 
@@ -241,31 +240,6 @@ def test_spatial_pass_bit_exact(gpu, oracle, name, N, mode, lean):
     finally:
         for k, v in SPATIAL_DEFAULTS.items():
             gpu.set_tuning(k, v)
-
-
-@pytest.mark.parametrize("k", [0, 1, 2, 3, 4, 5])
-def test_spatial_x2_every_k_bit_exact(gpu, oracle, k):
-    """k_spatial1_x2 (a pixel's inputs over two lanes) for every K its split handles: half 0 takes ceil(K / 2)
-    neighbours, half 1 the rest and the pixel's own, the serial update handed across by DPP."""
-    for kk, v in SPATIAL_VARIANTS["x2"].items():
-        gpu.set_tuning(kk, v)
-    try:
-        _, osc, cam = setup(gpu, oracle, "nightclub_128pt", 1)
-        n_t, p_mat = oracle.gbuffer(osc, cam, W, H)
-        f = _abi.default_features(num_samples_in_reservoir=1, num_neighbours_to_sample=k, spatial_resample_radius=6)
-        a, b, _ = oracle_ris(oracle, osc, f, cam, n_t, p_mat)
-        for which, arr in [(_abi.BUF_GBUF_N_T, n_t), (_abi.BUF_GBUF_P_MAT, p_mat), (_abi.BUF_RES_A, a),
-                           (_abi.BUF_RES_B, b)]:
-            gpu.upload(which, arr)
-        kp = key(_abi.RESTIR_STAGE_SPATIAL, 0)
-        gpu.stage_spatial(cam, f, kp)
-        a2, b2, d2 = oracle.spatial_pass(osc, f, kp, origin(oracle, cam), W, H, n_t, p_mat, (a, b))
-        assert_bits(gpu.download(_abi.BUF_RES_A), a2, "res_a")
-        assert_bits(gpu.download(_abi.BUF_RES_B), b2, "res_b")
-        assert_bits(gpu.download(_abi.BUF_RES_DBG), d2, "wSum/chosen")
-    finally:
-        for kk, v in SPATIAL_DEFAULTS.items():
-            gpu.set_tuning(kk, v)
 
 
 @pytest.mark.parametrize("k,r", [(0, 10), (10, 30), (5, 1)])

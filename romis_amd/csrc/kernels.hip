@@ -685,9 +685,15 @@ extern "C" __global__ __launch_bounds__(256) void k_primary_lds(SceneDev s, Regi
 //   kLtPgram    every light a parallelogram with one colour at all four of its corners, edges free (the reference's
 //               default nightclub set, scene.cpp:30-66: two wall grids): SceneDev::light_c4, rows 0..3 of each record
 //               (v0, edge01, edge02, colour), 4 float4 per light instead of 7.
-constexpr int kLtGeneral = 0, kLtPoint = 1, kLtGrid = 2, kLtPgram = 3;
+//   kLtRegular  a light grid laid out as regularLightGrid does (SceneDev::lights_regular, host-verified bit for bit):
+//               the drawn light's corner is (start + s01 x) + s02 y, x = i >> log2(ny), y = i & (ny - 1), evaluated in
+//               float as the reference built it; only its colour is read, from SceneDev::light_col (one float4 per
+//               light instead of kLtGrid's two: C4 / C5's 1,024 / 4,096-light grids).
+constexpr int kLtGeneral = 0, kLtPoint = 1, kLtGrid = 2, kLtPgram = 3, kLtRegular = 4;
 // float4s per light of the table form LT
-__host__ __device__ constexpr uint32_t lt_stride(int lt) { return lt == kLtGeneral ? 7u : lt == kLtPgram ? 4u : 2u; }
+__host__ __device__ constexpr uint32_t lt_stride(int lt) {
+    return lt == kLtGeneral ? 7u : lt == kLtPgram ? 4u : lt == kLtRegular ? 1u : 2u;
+}
 template <int NT, int LT = kLtGeneral>
 __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                           const float4* lights, const Bvh& bvh, float4 nt, float4 pm, uint32_t x,
@@ -751,6 +757,16 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                     const v3 gc = xyz(lt[1]);
                     const v3 m = vmix(gc, gc, a);   // = vmix(c0, c1, a) = vmix(c2, c3, a): all four corners are gc
                     col = vmix(m, m, b);
+                } else if (LT == kLtRegular) {   // the corner of light i by arithmetic (scene.cpp:14-15)
+                    const uint32_t i = uniform_index(draw(ps, 4u * c), L);
+                    const float xl = (float)(i >> s.grid_ny_log2), yl = (float)(i & ((1u << s.grid_ny_log2) - 1u));
+                    const v3 v0 = vadd(vadd(xyz(s.grid_start), vscale(xyz(s.grid_s01), xl)), vscale(xyz(s.grid_s02), yl));
+                    float a = rand01(draw(ps, 4u * c + 1u));
+                    float b = rand01(draw(ps, 4u * c + 2u));
+                    pos = vadd(vadd(v0, vscale(shared_row(1), a)), vscale(shared_row(2), b));
+                    const v3 gc = xyz(lights[i]);
+                    const v3 m = vmix(gc, gc, a);
+                    col = vmix(m, m, b);
                 } else if (LT == kLtPgram) {
                     float a = rand01(draw(ps, 4u * c + 1u));
                     float b = rand01(draw(ps, 4u * c + 2u));
@@ -809,7 +825,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
 // The light table of form LT: the 7-float4 records or the compact (row 0, row 3) table.
 template <int LT>
 __device__ __forceinline__ const float4* global_lights(const SceneDev& s) {
-    return LT == kLtGeneral ? s.lights : LT == kLtPgram ? s.light_c4 : s.light_c2;
+    return LT == kLtGeneral ? s.lights : LT == kLtPgram ? s.light_c4 : LT == kLtRegular ? s.light_col : s.light_c2;
 }
 // Stage it into LDS at dst.  No barrier.
 template <int LT>
@@ -900,6 +916,8 @@ ROMIS_RIS_KERNEL_LT(1, true, kLtGrid, k_ris_n1_lds_grid, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(2, true, kLtGrid, k_ris_n2_lds_grid, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(1, false, kLtGrid, k_ris_n1_grid, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(2, false, kLtGrid, k_ris_n2_grid, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(1, false, kLtRegular, k_ris_n1_reg, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(1, true, kLtRegular, k_ris_n1_lds_reg, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(1, true, kLtPgram, k_ris_n1_lds_pg, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(2, true, kLtPgram, k_ris_n2_lds_pg, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(1, false, kLtPgram, k_ris_n1_pg, ROMIS_RIS_ATTR)
@@ -926,6 +944,8 @@ ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtGrid, k_primary_ris_n1_lds_grid, ROMIS_R
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, true, kLtGrid, k_primary_ris_n2_lds_grid, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtGrid, k_primary_ris_n1_grid, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, false, kLtGrid, k_primary_ris_n2_grid, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtRegular, k_primary_ris_n1_reg, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtRegular, k_primary_ris_n1_lds_reg, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtPgram, k_primary_ris_n1_lds_pg, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, true, kLtPgram, k_primary_ris_n2_lds_pg, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtPgram, k_primary_ris_n1_pg, ROMIS_RIS_ATTR)
@@ -2826,6 +2846,8 @@ inline size_t lights_lds_bytes(const SceneDev& s) { return (size_t)7 * s.num_lig
 inline int ris_light_form(const SceneDev& s, const FeaturesDev& f, const Tuning& tu) {
     if (!tu.ris_compact || s.num_lights == 0 || (f.N != 1 && f.N != 2)) return kLtGeneral;
     if (s.light_types == 1u) return kLtPoint;
+    // N = 1 (at N = 2 the form spills): ris.compact = 2 keeps the grid table (A/B runs)
+    if (s.lights_regular && tu.ris_compact == 1u && f.N == 1) return kLtRegular;
     if (s.lights_grid) return kLtGrid;
     if (s.lights_pgram) return kLtPgram;
     return kLtGeneral;
@@ -2862,7 +2884,8 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f
     const int lt = ris_light_form(s, f, tu);
     const size_t lds = ris_lights_lds_bytes(s, lt);
     const bool staged = tu.ris_lds && s.num_lights > 0 && lds <= kLdsBudget;
-    auto k = lt == kLtPoint ? (staged ? (f.N == 1 ? k_ris_n1_lds_pt : k_ris_n2_lds_pt) : (f.N == 1 ? k_ris_n1_pt : k_ris_n2_pt))
+    auto k = lt == kLtRegular ? (staged ? k_ris_n1_lds_reg : k_ris_n1_reg)
+           : lt == kLtPoint ? (staged ? (f.N == 1 ? k_ris_n1_lds_pt : k_ris_n2_lds_pt) : (f.N == 1 ? k_ris_n1_pt : k_ris_n2_pt))
            : lt == kLtGrid ? (staged ? (f.N == 1 ? k_ris_n1_lds_grid : k_ris_n2_lds_grid)
                                      : (f.N == 1 ? k_ris_n1_grid : k_ris_n2_grid))
            : lt == kLtPgram ? (staged ? (f.N == 1 ? k_ris_n1_lds_pg : k_ris_n2_lds_pg) : (f.N == 1 ? k_ris_n1_pg : k_ris_n2_pg))
@@ -2884,7 +2907,8 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
     const int lt = ris_light_form(s, f, tu);
     const size_t lights = ris_lights_lds_bytes(s, lt);
     const bool use_lights = tu.ris_lds && s.num_lights > 0 && bvh + lights <= kLdsBudget;
-    auto k = lt == kLtPoint ? (use_lights ? (f.N == 1 ? k_primary_ris_n1_lds_pt : k_primary_ris_n2_lds_pt)
+    auto k = lt == kLtRegular ? (use_lights ? k_primary_ris_n1_lds_reg : k_primary_ris_n1_reg)
+           : lt == kLtPoint ? (use_lights ? (f.N == 1 ? k_primary_ris_n1_lds_pt : k_primary_ris_n2_lds_pt)
                                           : (f.N == 1 ? k_primary_ris_n1_pt : k_primary_ris_n2_pt))
            : lt == kLtGrid ? (use_lights ? (f.N == 1 ? k_primary_ris_n1_lds_grid : k_primary_ris_n2_lds_grid)
                                          : (f.N == 1 ? k_primary_ris_n1_grid : k_primary_ris_n2_grid))

@@ -206,7 +206,8 @@ struct restir_ctx {
     std::mutex mu;
 
     // scene
-    DevBuf nodes, tri_v0, tri_e1, tri_e2, tri_n0, tri_n1, tri_n2, materials, lights, light_c2, light_c4, tex_texels, tex_dims, tri_uv;
+    DevBuf nodes, tri_v0, tri_e1, tri_e2, tri_n0, tri_n1, tri_n2, materials, lights, light_c2, light_c4, light_col, tex_texels,
+        tex_dims, tri_uv;
     SceneDev sdev{};
     bool has_scene = false;
 
@@ -779,7 +780,7 @@ void restir_destroy(restir_ctx* c) {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
         for (DevBuf* b : {&c->nodes, &c->tri_v0, &c->tri_e1, &c->tri_e2, &c->tri_n0, &c->tri_n1, &c->tri_n2,
-                          &c->materials, &c->lights, &c->tex_texels, &c->tex_dims, &c->tri_uv, &c->uv, &c->n_t, &c->p_mat, &c->ra[0], &c->ra[1], &c->rb[0], &c->rb[1],
+                          &c->materials, &c->lights, &c->light_c2, &c->light_c4, &c->light_col, &c->tex_texels, &c->tex_dims, &c->tri_uv, &c->uv, &c->n_t, &c->p_mat, &c->ra[0], &c->ra[1], &c->rb[0], &c->rb[1],
                           &c->dbg[0], &c->dbg[1], &c->rgb, &c->queue_ctr, &c->halo_scratch, &c->rec[0], &c->rec[1], &c->rp[0], &c->rp[1]})
             b->release();
         for (Pending& p : c->pending) { (void)hipEventDestroy(p.start); (void)hipEventDestroy(p.stop); }
@@ -809,6 +810,73 @@ restir_status restir_set_renders_dir(restir_ctx* c, const char* dir) {
 restir_status restir_set_scene(restir_ctx* c, const restir_mesh* meshes, uint32_t num_meshes, const restir_light* lights,
                                uint32_t num_lights) {
     return restir_set_scene_textured(c, meshes, num_meshes, lights, num_lights, nullptr, 0);
+}
+
+// regularLightGrid's layout (scene.cpp:5-28) recovered from a light grid's corners: light i = x * ny + y has its corner
+// at (start + s01 * float(x)) + s02 * float(y), computed in float as the reference does.  start = light 0's corner;
+// s01 / s02 per component from the corners of lights ny and 1 (their difference, then the nearest floats around it)
+// and accepted only when they reproduce every light's corner bit for bit; ny = the first power-of-two divisor of
+// the light count that works.  The RIS kernels' kLtRegular form then evaluates the same expression instead of
+// reading the corner from the table.
+struct RegularGrid {
+    bool ok = false;
+    uint32_t ny_log2 = 0;
+    float start[3] = {0, 0, 0}, s01[3] = {0, 0, 0}, s02[3] = {0, 0, 0};
+};
+static float grid_corner(float start, float s01, float s02, uint32_t x, uint32_t y) {
+    volatile float a = s01 * (float)x;   // float products and sums, no contraction (the reference's order)
+    volatile float b = start + a;
+    volatile float c = s02 * (float)y;
+    return b + c;
+}
+static RegularGrid find_regular_grid(const std::vector<float>& lt, uint32_t L) {
+    RegularGrid g;
+    if (L < 2) return g;
+    auto near_floats = [](float t, float* out) {   // t and its 64 float neighbours on either side
+        int n = 0;
+        out[n++] = t;
+        float up = t, dn = t;
+        for (int k = 0; k < 64; k++) {
+            up = std::nextafter(up, INFINITY);
+            dn = std::nextafter(dn, -INFINITY);
+            out[n++] = up;
+            out[n++] = dn;
+        }
+        return n;
+    };
+    for (uint32_t lg = 0; (1u << lg) <= L; lg++) {
+        const uint32_t ny = 1u << lg, nx = L / ny;
+        if (nx * ny != L) break;
+        if (ny < 2) continue;
+        bool all = true;
+        float st[3], a01[3], a02[3];
+        for (int cpt = 0; cpt < 3 && all; cpt++) {
+            const float start = lt[cpt];
+            float c01[129], c02[129];
+            const int n01 = nx > 1 ? near_floats(lt[28 * ny + cpt] - start, c01) : (c01[0] = 0.0f, 1);
+            const int n02 = near_floats(lt[28 * 1 + cpt] - start, c02);
+            bool found = false;
+            for (int i01 = 0; i01 < n01 && !found; i01++)
+                for (int i02 = 0; i02 < n02 && !found; i02++) {
+                    bool match = true;
+                    for (uint32_t i = 0; i < L && match; i++) {
+                        const float v = grid_corner(start, c01[i01], c02[i02], i >> lg, i & (ny - 1u));
+                        match = std::memcmp(&v, &lt[28 * i + cpt], 4) == 0;
+                    }
+                    if (match) { found = true; st[cpt] = start; a01[cpt] = c01[i01]; a02[cpt] = c02[i02]; }
+                }
+            all = found;
+        }
+        if (all) {
+            g.ok = true;
+            g.ny_log2 = lg;
+            for (int cpt = 0; cpt < 3; cpt++) {
+                g.start[cpt] = st[cpt]; g.s01[cpt] = a01[cpt]; g.s02[cpt] = a02[cpt];
+            }
+            return g;
+        }
+    }
+    return g;
 }
 
 restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes, uint32_t num_meshes,
@@ -941,6 +1009,7 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     }
     bool grid = pgram;
     for (uint32_t i = 0; grid && i < num_lights; i++) grid = std::memcmp(&lt[28 * i + 4], &lt[4], 8 * sizeof(float)) == 0;
+    const RegularGrid reg = grid ? find_regular_grid(lt, num_lights) : RegularGrid{};
     std::vector<float> lc4(16 * std::max<uint32_t>(pgram ? num_lights : 1u, 1u), 0.0f);
     for (uint32_t i = 0; pgram && i < num_lights; i++) std::memcpy(&lc4[16 * i], &lt[28 * i], 64);
     ST_TRY(c->light_c4.upload(lc4.data(), lc4.size() * 4, c->stream));
@@ -950,6 +1019,9 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
         std::memcpy(&lc2[8 * i + 4], &lt[28 * i + 12], 16);
     }
     ST_TRY(c->light_c2.upload(lc2.data(), lc2.size() * 4, c->stream));
+    std::vector<float> lcol(4 * std::max<uint32_t>(num_lights, 1), 0.0f);   // c0 of every light (kLtRegular)
+    for (uint32_t i = 0; i < num_lights; i++) std::memcpy(&lcol[4 * i], &lt[28 * i + 12], 12);
+    ST_TRY(c->light_col.upload(lcol.data(), lcol.size() * 4, c->stream));
     // textures: texels as float4, images back to back; (width, height, first texel, 0) per image
     std::vector<float> texels;
     std::vector<uint32_t> dims;
@@ -1002,6 +1074,12 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     s.lights_grid = grid ? 1u : 0u;
     s.light_c4 = c->light_c4.as<float4>();
     s.lights_pgram = pgram ? 1u : 0u;
+    s.lights_regular = reg.ok ? 1u : 0u;
+    s.grid_ny_log2 = reg.ny_log2;
+    s.grid_start = make_float4(reg.start[0], reg.start[1], reg.start[2], 0.0f);
+    s.grid_s01 = make_float4(reg.s01[0], reg.s01[1], reg.s01[2], 0.0f);
+    s.grid_s02 = make_float4(reg.s02[0], reg.s02[1], reg.s02[2], 0.0f);
+    s.light_col = c->light_col.as<float4>();
     // w = p / (1/L) (light.cpp:80) equals p * L exactly when 1/L is a power of two
     s.light_scale = (num_lights && (num_lights & (num_lights - 1)) == 0) ? (float)num_lights : 0.0f;
     s.lights_finite = 1u;

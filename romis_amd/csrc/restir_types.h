@@ -56,6 +56,13 @@ struct SceneDev {
     uint32_t lights_grid;      // every light a parallelogram with light 0's edges (rows 1, 2) and c0 = c1 = c2 = c3
     const float4* light_c4;    // rows 0..3 of every light's record (v0, edge01, edge02, c0): the kLtPgram table
     uint32_t lights_pgram;     // every light a parallelogram with c0 = c1 = c2 = c3
+    // a light grid (lights_grid) laid out as regularLightGrid does (scene.cpp:5-28): light i's corner is
+    // (start + s01 * float(i / ny)) + s02 * float(i % ny) bit for bit (host-verified), ny a power of two -- the RIS
+    // kernels' kLtRegular form computes the corner and reads only the colour (light_col: c0 of every light)
+    uint32_t lights_regular;
+    uint32_t grid_ny_log2;
+    float4 grid_start, grid_s01, grid_s02;   // .xyz
+    const float4* light_col;
     uint32_t lights_finite;    // every light coordinate / colour is finite
     uint32_t shade_finite;     // every light colour x material kd / ks product is finite (shade()'s NaN tests)
     uint32_t normals_bounded;  // every vertex normal component finite with |n| <= 2^125: interpolated normals are

@@ -12,11 +12,10 @@ timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeo
     || { tail -40 $OUT/tests.log; exit 21; }
 tail -3 $OUT/tests.log
 for c in c2 c4 c5; do
-  for lib in shipped ris_wpe6 ris_grid_noload; do
-    [ $lib = ris_grid_noload ] && [ $c = c2 ] && continue
+  for lib in shipped ris_wpe6; do
     if [ $lib = shipped ]; then unset ROMIS_AMD_LIB; else export ROMIS_AMD_LIB="$REPO/romis_amd/_build/variants/$lib/libromis_amd.so"; fi
     timeout -k 10 300 python3 scripts/cfg_kbench.py --config $c --rounds 3 --frames $([ $c = c5 ] && echo 3 || echo 10) \
-        --variants default: > $OUT/kb_${c}_$lib.json 2> $OUT/kb_${c}_$lib.err || { tail -5 $OUT/kb_${c}_$lib.err; exit 22; }
+        --variants default: gridtable:ris.compact=2 > $OUT/kb_${c}_$lib.json 2> $OUT/kb_${c}_$lib.err || { tail -5 $OUT/kb_${c}_$lib.err; exit 22; }
     echo "$c $lib $(cat $OUT/kb_${c}_$lib.json)"
   done
 done

@@ -29,7 +29,12 @@ _scenes = {}
 
 def get_scene(name):
     if name not in _scenes:
-        _scenes[name] = scene.bench_scene(name) if name not in ("Cube", "CubeTextured") else scene.load_prebuilt(name)
+        if name == "cornell_1024_shuffled":   # a light grid whose order is not regularLightGrid's (no kLtRegular form)
+            base = scene.bench_scene("cornell_1024")
+            perm = np.random.default_rng(7).permutation(len(base.lights))
+            _scenes[name] = scene.Scene(base.meshes, [base.lights[i] for i in perm], name)
+        else:
+            _scenes[name] = scene.bench_scene(name) if name not in ("Cube", "CubeTextured") else scene.load_prebuilt(name)
     return _scenes[name]
 
 
@@ -298,15 +303,19 @@ def test_final_shading_binned_rays(gpu, oracle, name, binned, N):
 @pytest.mark.parametrize("name,N,compact,lds", [
     ("nightclub_128pt", 1, 1, 1), ("nightclub_128pt", 2, 1, 1), ("nightclub_128pt", 1, 1, 0), ("nightclub_128pt", 1, 0, 1),
     ("cornell_1024", 1, 1, 1), ("cornell_1024", 2, 1, 1), ("cornell_1024", 1, 1, 0), ("cornell_1024", 2, 0, 1),
+    ("cornell_1024", 1, 2, 1), ("cornell_1024", 1, 2, 0), ("cornell_4096", 1, 1, 1), ("cornell_4096", 1, 2, 1),
+    ("cornell_1024_shuffled", 1, 1, 1),
     ("nightclub_512", 1, 1, 1), ("nightclub_512", 2, 1, 1), ("nightclub_512", 2, 1, 0), ("nightclub_512", 2, 0, 1)])
 def test_ris_compact_light_tables(gpu, oracle, name, N, compact, lds):
     """ris.compact (default 1): point-light-only scenes (C2), light grids (C4 / C5: parallelograms sharing their
     edges, one colour per light) and one-colour parallelograms (the reference's 512-light nightclub) run the _pt /
     _grid / _pg RIS kernels over the compact light tables, staged
-    in LDS (ris.lds 1) or read from global memory (0); ris.compact 0: the general kernels on the same scene.  Each
-    bit-exact vs the oracle, through the unfused k_ris (stage_ris) and the fused k_primary_ris of a whole frame."""
+    in LDS (ris.lds 1) or read from global memory (0); ris.compact 0: the general kernels on the same scene.  Light
+    grids in regularLightGrid's order (cornell_1024 / _4096) take the _reg kernels at N = 1 (corner by arithmetic,
+    colour table only; ris.compact 2 keeps the _grid table form), a shuffled grid the _grid form.  Each bit-exact vs
+    the oracle, through the unfused k_ris (stage_ris) and the fused k_primary_ris of a whole frame."""
     s = get_scene(name)
-    if name == "cornell_1024":   # the scene must qualify as a light grid, or this would test the general form
+    if name.startswith("cornell_"):   # the scene must qualify as a light grid, or this would test the general form
         e = np.array([[*l.p1, *l.p2] for l in s.lights], np.float32)
         c = np.array([[*l.c0, *l.c1, *l.c2, *l.c3] for l in s.lights], np.float32).reshape(-1, 4, 3)
         assert (e.view(np.uint32) == e[0].view(np.uint32)).all() and (c.view(np.uint32) == c[:, :1].view(np.uint32)).all()

@@ -889,12 +889,19 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
 }
 
 // RIS: capped at 96 VGPRs = 5 waves per SIMD (uncapped the allocator takes 100 = 4 waves; 5 waves run the
-// latency-bound candidate loop 9 % faster, 6 waves spill -- scripts/ablate.py, profiles/r1).  N = 2 the same:
-// k_primary_ris_n2_lds 407 -> 381 us at C2 N = 2 (profiles/r3/r3_configs/n2_*_c2.json).
+// latency-bound candidate loop 9 % faster, 6 waves spilled -- scripts/ablate.py, profiles/r1).  N = 2 the same:
+// k_primary_ris_n2_lds 407 -> 381 us at C2 N = 2 (profiles/r3/r3_configs/n2_*_c2.json).  Round 4: with the accepted
+// candidate kept as an index (ris_pixel) the N = 1 kernels fit 80 VGPRs without spilling, and 6 waves per SIMD run
+// C2 RIS 319.5 -> 305.8 us, C4 379.6 -> 370.3, C5 2161 -> 2086 (cfg_kbench, profiles/r4/r4c).  (The unfused
+// k_ris_n1_lds_{grid,reg,pg} would spill 12 B at 6 and keep 5.)
 #ifndef ROMIS_RIS_WPE
 #define ROMIS_RIS_WPE 5
 #endif
+#ifndef ROMIS_RIS1_WPE
+#define ROMIS_RIS1_WPE 6
+#endif
 #define ROMIS_RIS_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_RIS_WPE)))
+#define ROMIS_RIS1_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_RIS1_WPE)))
 #define ROMIS_RIS_KERNEL_LT(NT, LDS, LT, NAME, ATTR)                                                                  \
     extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,   \
@@ -902,25 +909,25 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         ris_body<NT, LDS, LT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg, rp, wq);                         \
     }
 #define ROMIS_RIS_KERNEL(NT, LDS, NAME, ATTR) ROMIS_RIS_KERNEL_LT(NT, LDS, kLtGeneral, NAME, ATTR)
-ROMIS_RIS_KERNEL(1, false, k_ris_n1, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL(1, false, k_ris_n1, ROMIS_RIS1_ATTR)
 ROMIS_RIS_KERNEL(2, false, k_ris_n2, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL(0, false, k_ris_n0, )
-ROMIS_RIS_KERNEL(1, true, k_ris_n1_lds, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL(1, true, k_ris_n1_lds, ROMIS_RIS1_ATTR)
 ROMIS_RIS_KERNEL(2, true, k_ris_n2_lds, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL(0, true, k_ris_n0_lds, )
-ROMIS_RIS_KERNEL_LT(1, true, kLtPoint, k_ris_n1_lds_pt, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(1, true, kLtPoint, k_ris_n1_lds_pt, ROMIS_RIS1_ATTR)
 ROMIS_RIS_KERNEL_LT(2, true, kLtPoint, k_ris_n2_lds_pt, ROMIS_RIS_ATTR)
-ROMIS_RIS_KERNEL_LT(1, false, kLtPoint, k_ris_n1_pt, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(1, false, kLtPoint, k_ris_n1_pt, ROMIS_RIS1_ATTR)
 ROMIS_RIS_KERNEL_LT(2, false, kLtPoint, k_ris_n2_pt, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(1, true, kLtGrid, k_ris_n1_lds_grid, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(2, true, kLtGrid, k_ris_n2_lds_grid, ROMIS_RIS_ATTR)
-ROMIS_RIS_KERNEL_LT(1, false, kLtGrid, k_ris_n1_grid, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(1, false, kLtGrid, k_ris_n1_grid, ROMIS_RIS1_ATTR)
 ROMIS_RIS_KERNEL_LT(2, false, kLtGrid, k_ris_n2_grid, ROMIS_RIS_ATTR)
-ROMIS_RIS_KERNEL_LT(1, false, kLtRegular, k_ris_n1_reg, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(1, false, kLtRegular, k_ris_n1_reg, ROMIS_RIS1_ATTR)
 ROMIS_RIS_KERNEL_LT(1, true, kLtRegular, k_ris_n1_lds_reg, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(1, true, kLtPgram, k_ris_n1_lds_pg, ROMIS_RIS_ATTR)
 ROMIS_RIS_KERNEL_LT(2, true, kLtPgram, k_ris_n2_lds_pg, ROMIS_RIS_ATTR)
-ROMIS_RIS_KERNEL_LT(1, false, kLtPgram, k_ris_n1_pg, ROMIS_RIS_ATTR)
+ROMIS_RIS_KERNEL_LT(1, false, kLtPgram, k_ris_n1_pg, ROMIS_RIS1_ATTR)
 ROMIS_RIS_KERNEL_LT(2, false, kLtPgram, k_ris_n2_pg, ROMIS_RIS_ATTR)
 
 #define ROMIS_PRIMARY_RIS_KERNEL_LT(NT, LDS, LT, NAME, ATTR)                                                           \
@@ -930,25 +937,25 @@ ROMIS_RIS_KERNEL_LT(2, false, kLtPgram, k_ris_n2_pg, ROMIS_RIS_ATTR)
         primary_ris_body<NT, LDS, LT>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp);                          \
     }
 #define ROMIS_PRIMARY_RIS_KERNEL(NT, LDS, NAME, ATTR) ROMIS_PRIMARY_RIS_KERNEL_LT(NT, LDS, kLtGeneral, NAME, ATTR)
-ROMIS_PRIMARY_RIS_KERNEL(1, true, k_primary_ris_n1_lds, ROMIS_RIS_ATTR)
-ROMIS_PRIMARY_RIS_KERNEL(1, false, k_primary_ris_n1, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL(1, true, k_primary_ris_n1_lds, ROMIS_RIS1_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL(1, false, k_primary_ris_n1, ROMIS_RIS1_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(2, true, k_primary_ris_n2_lds, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(2, false, k_primary_ris_n2, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(0, true, k_primary_ris_n0_lds, )
 ROMIS_PRIMARY_RIS_KERNEL(0, false, k_primary_ris_n0, )
-ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtPoint, k_primary_ris_n1_lds_pt, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtPoint, k_primary_ris_n1_lds_pt, ROMIS_RIS1_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, true, kLtPoint, k_primary_ris_n2_lds_pt, ROMIS_RIS_ATTR)
-ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtPoint, k_primary_ris_n1_pt, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtPoint, k_primary_ris_n1_pt, ROMIS_RIS1_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, false, kLtPoint, k_primary_ris_n2_pt, ROMIS_RIS_ATTR)
-ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtGrid, k_primary_ris_n1_lds_grid, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtGrid, k_primary_ris_n1_lds_grid, ROMIS_RIS1_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, true, kLtGrid, k_primary_ris_n2_lds_grid, ROMIS_RIS_ATTR)
-ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtGrid, k_primary_ris_n1_grid, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtGrid, k_primary_ris_n1_grid, ROMIS_RIS1_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, false, kLtGrid, k_primary_ris_n2_grid, ROMIS_RIS_ATTR)
-ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtRegular, k_primary_ris_n1_reg, ROMIS_RIS_ATTR)
-ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtRegular, k_primary_ris_n1_lds_reg, ROMIS_RIS_ATTR)
-ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtPgram, k_primary_ris_n1_lds_pg, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtRegular, k_primary_ris_n1_reg, ROMIS_RIS1_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtRegular, k_primary_ris_n1_lds_reg, ROMIS_RIS1_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtPgram, k_primary_ris_n1_lds_pg, ROMIS_RIS1_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, true, kLtPgram, k_primary_ris_n2_lds_pg, ROMIS_RIS_ATTR)
-ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtPgram, k_primary_ris_n1_pg, ROMIS_RIS_ATTR)
+ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtPgram, k_primary_ris_n1_pg, ROMIS_RIS1_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, false, kLtPgram, k_primary_ris_n2_pg, ROMIS_RIS_ATTR)
 
 // ---------------------------------------------------------------------------------------------------------

@@ -74,13 +74,15 @@ def parse():
     ap.add_argument("--halo-transport", default="auto", choices=["auto", "native", "torch"],
                     help="halo transport: the library's own RCCL communicator (native), torch.distributed p2p (torch); "
                          "auto = native under nccl, torch under gloo")
-    ap.add_argument("--prewarm", type=int, default=40,
-                    help="4-GiB streaming-read sweeps (restir_measure_read_bandwidth, ~0.6 ms each) before the warm-up "
-                         "frames: the clocks of an idle box ramp over the first ~25 ms of load (kernel durations fell "
-                         "6-11 %% over a 50-frame run, profiles/r4/gap); the same sweeps give measured_read_peak")
-    ap.add_argument("--prewarm-gemm-ms", type=float, default=0.0,
-                    help="GPU clock pre-warm before the warm-up frames: fp32 GEMMs through torch for this long "
-                         "(compute-bound; the streaming-read sweeps of --prewarm do not raise the clocks)")
+    ap.add_argument("--prewarm-gemm-ms", type=float, default=500.0,
+                    help="GPU clock pre-warm before the warm-up frames (not frames, not timed): fp32 GEMMs through torch "
+                         "for this long.  An idle box's first ~40 frames run up to 10 %% slower (profiles/r4/gap); 500 ms "
+                         "of compute-bound work takes the driver's 20-frame C2 run 0.467 -> 0.451 ms (profiles/r4/r4c); "
+                         "streaming reads (restir_measure_read_bandwidth) do not raise the clocks")
+    ap.add_argument("--timing-every", type=int, default=4,
+                    help="HIP events on every n-th spatial launch of the timed region (the event-carrying dispatch "
+                         "costs ~9 us of stream gaps, profiles/r4/gap); the roofline's average launch time is over "
+                         "those launches")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="restir_set_tuning knobs for A/B runs (launch shapes and timing only; results are identical)")
     ap.add_argument("--traffic-csv", default=None,
@@ -509,11 +511,10 @@ def main():
         else:
             r.render_restir(None, cam, GW, GH, f, tile=tile, want_rgb=False, want_grid=False)
 
-    # GPU pre-warm (not a frame, not timed): streaming reads over 4 GiB bring an idle box's clocks up before the
-    # warm-up frames, and give the practical HBM-read ceiling reported beside the roofline
-    measured = r.measure_read_bandwidth(4 << 30, max(1, args.prewarm)) if args.prewarm > 0 else None
+    # GPU clock pre-warm (not a frame, not timed), then the practical HBM-read ceiling reported beside the roofline
     if args.prewarm_gemm_ms > 0:
         gemm_prewarm(torch, local, args.prewarm_gemm_ms)
+    measured = r.measure_read_bandwidth(4 << 30, 10)
     for _ in range(args.warmup):
         step()
     # Timed region: the spatial kernel (the roofline's) carries a HIP start / stop event pair recorded inside its
@@ -521,6 +522,8 @@ def main():
     # (profiles/r1), so the per-kernel breakdown comes from a separate run of the same frames.
     r.reset_timings()
     r.set_tuning("timing.mask", -1 if args.time_kernels == "all" else 1 << _abi.K_SPATIAL)
+    # a halo pass is several launches averaged per pass below: every launch keeps its events there
+    r.set_tuning("timing.every", 1 if halo else max(1, args.timing_every))
     r.enable_timing(True)
     barrier_sync(torch, world, r)
     t0 = time.perf_counter()
@@ -533,6 +536,7 @@ def main():
     kt = r.timings()
     r.reset_timings()
     r.set_tuning("timing.mask", -1)
+    r.set_tuning("timing.every", 1)
     r.enable_timing(True)
     for _ in range(min(args.steps, 20)):
         step()
@@ -569,9 +573,8 @@ def main():
                     "traffic": traffic, "traffic_source": traffic_src, "bytes_per_launch": bytes_per_launch,
                     "avg_launch_us": round(avg_s * 1e6, 2),
                     "read_only_frac": round(sp_px * (32 + 32 * args.N) / avg_s / 1e9 / HBM_PEAK_GBS, 4)}
-        # the practical ceiling next to the spec: a streaming-read kernel over 4 GiB (past the Infinity Cache)
-        if measured is None:
-            measured = r.measure_read_bandwidth(4 << 30, 10)
+        # the practical ceiling next to the spec: a streaming-read kernel over 4 GiB (past the Infinity Cache), run
+        # before the warm-up frames
         roofline["measured_read_peak"] = round(measured, 1)
         roofline["frac_of_measured_peak"] = round(achieved / measured, 4)
 

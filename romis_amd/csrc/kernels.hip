@@ -881,7 +881,7 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
     for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {
         uint32_t x, y;
         size_t p;
-        if (!work_pixel(rg, rg.rev ? items - 1u - item : item, x, y, p)) continue;
+        if (!work_pixel(rg, item, x, y, p)) continue;
         float4 nt, pm;
         primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, nt, pm);
         ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb);
@@ -2908,8 +2908,7 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
                               float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,
                               float* rp, const Tuning& tu, hipStream_t stream) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
-    Region rg = with_map(rg0, tu.primary_2d);
-    rg.rev = tu.ris_order;
+    const Region rg = with_map(rg0, tu.primary_2d);
     const size_t bvh = bvh_lds_bytes(s);
     if (bvh > kLdsBudget) return hipErrorInvalidValue;   // caller checks primary_ris_fits()
     const int lt = ris_light_form(s, f, tu);

@@ -2248,7 +2248,6 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     }
     else if (!std::strcmp(key, "ris.queue")) t.ris_queue = v;
     else if (!std::strcmp(key, "ris.compact")) t.ris_compact = v;
-    else if (!std::strcmp(key, "ris.order")) t.ris_order = v ? 1u : 0u;
     else if (!std::strcmp(key, "bvh.max_leaf")) t.bvh_max_leaf = v;
     else if (!std::strcmp(key, "final.sort")) t.final_sort = v;
     else if (!std::strcmp(key, "mis.chunk")) t.mis_chunk = v;   // applies from the next ensure_mis

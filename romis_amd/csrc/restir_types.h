@@ -93,7 +93,6 @@ struct Region {
     // [n_t, a_0, b_0, a_1, b_1, ...] (restir_render): ps = 1 + 2N, js = 2, with res_a = rec + 1, res_b = rec + 2.
     uint32_t ps, js;
     uint32_t xcd_rows;   // k_spatial1's XCD tile order (xcd_tile); 0 elsewhere
-    uint32_t rev;        // fused primary + RIS: work items in reverse order (the last dispatched first; ris.order)
 };
 
 // Launch-shape knobs (restir_set_tuning); they never change results, only speed.
@@ -105,7 +104,6 @@ struct Tuning {
     uint32_t ris_blocks = 0;
     uint32_t ris_lds = 1;          // stage the light table in LDS when it fits
     uint32_t ris_queue = 0;        // persistent blocks (this many) pulling tiles from a WorkQueue; 0 = off
-    uint32_t ris_order = 0;        // k_primary_ris work order: 0 natural (bottom tile row first), 1 reversed
     uint32_t ris_compact = 1;      // N <= 2: compact light tables for point-light-only scenes and light grids (_pt /
                                    // _grid RIS kernels, kernels.hip ris_light_form)
     uint32_t spatial_xcd = 1;      // XCD-banded tile order

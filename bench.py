@@ -83,6 +83,10 @@ def parse():
                     help="HIP events on every n-th spatial launch of the timed region (the event-carrying dispatch "
                          "costs ~9 us of stream gaps, profiles/r4/gap); the roofline's average launch time is over "
                          "those launches")
+    ap.add_argument("--inflight", type=int, default=2, choices=[1, 2],
+                    help="frames in flight (restir_set_tuning frames.inflight): 2 overlaps frame f's final shading with "
+                         "frame f + 1's primary rays + RIS on a second stream; the spatial pass still runs alone, so "
+                         "its timed duration is the pass's (halo-mode frames: always 1)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="restir_set_tuning knobs for A/B runs (launch shapes and timing only; results are identical)")
     ap.add_argument("--traffic-csv", default=None,
@@ -515,6 +519,8 @@ def main():
     if args.prewarm_gemm_ms > 0:
         gemm_prewarm(torch, local, args.prewarm_gemm_ms)
     measured = r.measure_read_bandwidth(4 << 30, 10)
+    if not halo:
+        r.set_tuning("frames.inflight", args.inflight)
     for _ in range(args.warmup):
         step()
     # Timed region: the spatial kernel (the roofline's) carries a HIP start / stop event pair recorded inside its
@@ -534,6 +540,8 @@ def main():
     r.enable_timing(False)
     elapsed = max_over_ranks(torch, world, t1 - t0, local)
     kt = r.timings()
+    # per-kernel breakdown: serial frames (no overlap), every launch timed
+    r.set_tuning("frames.inflight", 1)
     r.reset_timings()
     r.set_tuning("timing.mask", -1)
     r.set_tuning("timing.every", 1)

@@ -220,6 +220,22 @@ struct restir_ctx {
     DevBuf rp[2];                                   // their target-pdf cache planes (N = 1, planes layout)
     int cur = 0;
     uint32_t rgb_w = 0, rgb_h = 0;
+    // Frames in flight (tuning frames.inflight = 2): restir_render alternates two frame slots -- slot 0 is the buffers
+    // above on `stream`, slot 1 its own buffers on its own stream -- so that frame f + 1's primary rays and RIS run
+    // while frame f is shaded.  Only that overlap is allowed: a frame's RIS waits for the other slot's last spatial
+    // pass (`after_spatial`) and its spatial passes wait for the other slot's final shading (`after_final`), so a
+    // spatial pass never shares the GPU with another kernel (its timed duration stays the pass alone).
+    struct Slot1 {
+        hipStream_t stream = nullptr;
+        DevBuf n_t, p_mat, rec[2], rp[2], rgb, uv;
+    } slot1;
+    struct {
+        hipEvent_t after_spatial[2] = {nullptr, nullptr}, after_final[2] = {nullptr, nullptr}, joined = nullptr;
+        bool has[2] = {false, false};
+        int next = 0;          // the slot of the next pipelined frame
+        int last = 0;          // the slot holding the last frame's rgb
+        bool slot1_busy = false;   // slot 1 may have work the context stream has not waited for
+    } pipe;
 
     // launch-shape knobs (restir_set_tuning)
     Tuning tuning{};
@@ -531,7 +547,7 @@ FeaturesDev to_dev(const restir_features* f) {
 
 // The scene as one launch over a view of npx pixels sees it: the G-buffer texCoord plane (allocated for textured
 // scenes; k_primary writes it, every target pdf reads it) and whether diffuseAlbedo reads the textures.
-static restir_status scene_for(restir_ctx* c, const FeaturesDev& f, size_t npx, SceneDev& out);
+static restir_status scene_for(restir_ctx* c, const FeaturesDev& f, size_t npx, SceneDev& out, DevBuf* uv = nullptr);
 
 namespace {
 
@@ -633,6 +649,7 @@ restir_status timed_end(restir_ctx* c, Pending& p, hipError_t launch_err) {
 
 restir_status collect_timings(restir_ctx* c) {
     if (c->pending.empty()) return RESTIR_OK;
+    if (c->slot1.stream) HIP_TRY(hipStreamSynchronize(c->slot1.stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (Pending& p : c->pending) {
         float ms = 0.0f;
@@ -690,31 +707,41 @@ struct FrameBufs {
     bool records;
     size_t npx;
     uint32_t N;
-    float4* nt(int i) const { return records ? c->rec[i].as<float4>() : c->n_t.as<float4>(); }
-    float4* ra(int i) const { return c->rec[i].as<float4>() + (records ? 1 : 0); }
-    float4* rb(int i) const { return c->rec[i].as<float4>() + (records ? 2 : npx * N); }
-    float4* nt2() const { return records ? c->rec[1].as<float4>() : nullptr; }
+    int slot = 0;   // restir_render's frame slot (frames in flight); everything else uses slot 0
+    DevBuf* rec_() const { return slot ? c->slot1.rec : c->rec; }
+    DevBuf& n_t_() const { return slot ? c->slot1.n_t : c->n_t; }
+    DevBuf* rp_() const { return slot ? c->slot1.rp : c->rp; }
+    float4* pm() const { return (slot ? c->slot1.p_mat : c->p_mat).as<float4>(); }
+    DevBuf& rgb() const { return slot ? c->slot1.rgb : c->rgb; }
+    DevBuf& uv() const { return slot ? c->slot1.uv : c->uv; }
+    float4* nt(int i) const { return records ? rec_()[i].as<float4>() : n_t_().as<float4>(); }
+    float4* ra(int i) const { return rec_()[i].as<float4>() + (records ? 1 : 0); }
+    float4* rb(int i) const { return rec_()[i].as<float4>() + (records ? 2 : npx * N); }
+    float4* nt2() const { return records ? rec_()[1].as<float4>() : nullptr; }
     // the target-pdf cache planes (N = 1 planes layout only)
-    float* rp(int i) const { return (!records && N == 1) ? c->rp[i].as<float>() : nullptr; }
+    float* rp(int i) const { return (!records && N == 1) ? rp_()[i].as<float>() : nullptr; }
     const float4* pa(const restir_frame* f) const { return f->rec.as<float4>() + (records ? 1 : 0); }
     const float4* pb(const restir_frame* f) const { return f->rec.as<float4>() + (records ? 2 : npx * N); }
     Region region(Region r) const { return records ? with_records(r, N) : r; }
 };
 
-restir_status ensure_records(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N, FrameBufs& fb) {
+restir_status ensure_records(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N, FrameBufs& fb, int slot = 0) {
     const size_t npx = (size_t)vw * vh;
     fb = FrameBufs{c, c->tuning.records != 0, npx, N};
-    ST_TRY(c->p_mat.ensure(npx * 16));
-    if (!fb.records) ST_TRY(c->n_t.ensure(npx * 16));
+    fb.slot = slot;
+    const hipStream_t st = slot ? c->slot1.stream : c->stream;
+    ST_TRY((slot ? c->slot1.p_mat : c->p_mat).ensure(npx * 16));
+    if (!fb.records) ST_TRY(fb.n_t_().ensure(npx * 16));
     const size_t rec_bytes = npx * (fb.records ? 1u + 2u * N : 2u * N) * 16;
+    DevBuf* rec = fb.rec_();
     for (int i = 0; i < 2; i++) {
         // a buffer handed to a frame comes back through the pool (stream-ordered against its past users)
-        if (!c->rec[i].p && c->pool->take(rec_bytes, c->stream, c->rec[i])) continue;
-        ST_TRY(c->rec[i].ensure(rec_bytes));
+        if (!rec[i].p && c->pool->take(rec_bytes, st, rec[i])) continue;
+        ST_TRY(rec[i].ensure(rec_bytes));
     }
     if (!fb.records && N == 1)
-        for (int i = 0; i < 2; i++) ST_TRY(c->rp[i].ensure(npx * 4));
-    c->vw = vw; c->vh = vh; c->N = N;
+        for (int i = 0; i < 2; i++) ST_TRY(fb.rp_()[i].ensure(npx * 4));
+    if (!slot) { c->vw = vw; c->vh = vh; c->N = N; }
     return RESTIR_OK;
 }
 
@@ -732,13 +759,28 @@ Region grow_rect(const Region& base, uint32_t g) {
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------------------
-static restir_status scene_for(restir_ctx* c, const FeaturesDev& f, size_t npx, SceneDev& out) {
+static restir_status scene_for(restir_ctx* c, const FeaturesDev& f, size_t npx, SceneDev& out, DevBuf* uv) {
     out = c->sdev;
     if (c->sdev.num_textures) {
-        ST_TRY(c->uv.ensure(std::max<size_t>(npx, 1) * 8));
-        out.gbuf_uv = c->uv.as<float2>();
+        DevBuf& u = uv ? *uv : c->uv;
+        ST_TRY(u.ensure(std::max<size_t>(npx, 1) * 8));
+        out.gbuf_uv = u.as<float2>();
         out.tex_on = f.texture ? 1u : 0u;
     }
+    return RESTIR_OK;
+}
+
+// Frames in flight: the context stream waits for whatever slot 1 still has in flight (every entry point that works
+// on the context stream after a pipelined frame calls this; a no-op when frames were never pipelined).
+static restir_status join_slots(restir_ctx* c) {
+    c->pipe.last = 0;   // the caller works on slot 0 (its rgb is the context's)
+    if (!c->pipe.slot1_busy) return RESTIR_OK;
+    if (!c->pipe.joined) HIP_TRY(hipEventCreateWithFlags(&c->pipe.joined, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->pipe.joined, c->slot1.stream));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->pipe.joined, 0));
+    c->pipe.slot1_busy = false;
+    c->pipe.has[0] = c->pipe.has[1] = false;   // the next pipelined frame starts a fresh pair
+    c->pipe.next = 0;
     return RESTIR_OK;
 }
 
@@ -779,6 +821,13 @@ void restir_destroy(restir_ctx* c) {
         std::lock_guard<std::mutex> lk(c->mu);
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
+        if (c->slot1.stream) (void)hipStreamSynchronize(c->slot1.stream);
+        for (DevBuf* b : {&c->slot1.n_t, &c->slot1.p_mat, &c->slot1.rec[0], &c->slot1.rec[1], &c->slot1.rp[0],
+                          &c->slot1.rp[1], &c->slot1.rgb, &c->slot1.uv})
+            b->release();
+        for (hipEvent_t* e : {&c->pipe.after_spatial[0], &c->pipe.after_spatial[1], &c->pipe.after_final[0],
+                              &c->pipe.after_final[1], &c->pipe.joined})
+            if (*e) (void)hipEventDestroy(*e);
         for (DevBuf* b : {&c->nodes, &c->tri_v0, &c->tri_e1, &c->tri_e2, &c->tri_n0, &c->tri_n1, &c->tri_n2,
                           &c->materials, &c->lights, &c->light_c2, &c->light_c4, &c->light_col, &c->tex_texels, &c->tex_dims, &c->tri_uv, &c->uv, &c->n_t, &c->p_mat, &c->ra[0], &c->ra[1], &c->rb[0], &c->rb[1],
                           &c->dbg[0], &c->dbg[1], &c->rgb, &c->queue_ctr, &c->halo_scratch, &c->rec[0], &c->rec[1], &c->rp[0], &c->rp[1]})
@@ -787,6 +836,7 @@ void restir_destroy(restir_ctx* c) {
         for (hipEvent_t ev : c->free_events) (void)hipEventDestroy(ev);
         c->pool->close();   // frames still alive free their records themselves on release
         release_rccl(c);
+        if (c->slot1.stream) (void)hipStreamDestroy(c->slot1.stream);
         (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -986,7 +1036,8 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     std::vector<float> nodes = bvh.nodes;
     if (nodes.empty()) nodes.assign(8, 0.0f);
 
-    HIP_TRY(hipStreamSynchronize(c->stream));   // previous frames may still read the old scene
+    ST_TRY(join_slots(c));
+    HIP_TRY(hipStreamSynchronize(c->stream));   // previous frames (either slot) may still read the old scene
     ST_TRY(c->nodes.upload(nodes.data(), nodes.size() * 4, c->stream));
     ST_TRY(c->tri_v0.upload(v0.data(), v0.size() * 4, c->stream));
     ST_TRY(c->tri_e1.upload(e1.data(), e1.size() * 4, c->stream));
@@ -1201,6 +1252,7 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
         if (tile && (tile->global_width != width || tile->global_height != height || tile->x0 || tile->y0 ||
                      tile->width != width || tile->height != height))
             return fail(RESTIR_ERR_UNSUPPORTED, "R-MIS / R-OMIS render whole images only (no screen tiles)");
+        ST_TRY(join_slots(c));
         return render_mis(c, cam, features, width, height, out_rgb);
     }
 
@@ -1244,13 +1296,26 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                                                 "render such tiles with the halo-exchange stages (restir_halo_begin)");
         if (prev->records != (c->tuning.records != 0))
             return fail(RESTIR_ERR_INVALID, "temporal predecessor grid was rendered with the other buffer layout");
-        ST_TRY(use_prev(prev, c->device, c->stream));
     }
 
+    // frame slot (frames in flight, restir_ctx::Slot1): slot 0 = the context's buffers and stream
+    const bool pipe = c->tuning.inflight > 1u;
+    if (!pipe) ST_TRY(join_slots(c));
+    const int k = pipe ? c->pipe.next : 0;
+    if (k == 1 && !c->slot1.stream) HIP_TRY(hipStreamCreateWithFlags(&c->slot1.stream, hipStreamNonBlocking));
+    const hipStream_t st = k ? c->slot1.stream : c->stream;
+    if (pipe)
+        for (int e = 0; e < 2; e++)
+            if (!c->pipe.after_spatial[e]) {
+                HIP_TRY(hipEventCreateWithFlags(&c->pipe.after_spatial[e], hipEventDisableTiming));
+                HIP_TRY(hipEventCreateWithFlags(&c->pipe.after_final[e], hipEventDisableTiming));
+            }
+    const bool wait_other = pipe && c->pipe.has[k ^ 1];
+
     FrameBufs fb;
-    ST_TRY(ensure_records(c, t.gwidth, t.gheight, N, fb));
+    ST_TRY(ensure_records(c, t.gwidth, t.gheight, N, fb, k));
     c->stage_ok = false;   // ensure_records re-sized the shared view state: the stage API must be reconfigured
-    ST_TRY(c->rgb.ensure((size_t)t.width * t.height * 12));
+    ST_TRY(fb.rgb().ensure((size_t)t.width * t.height * 12));
     c->rgb_w = t.width; c->rgb_h = t.height;
 
     const CameraDev camd = camera_dev(cam);
@@ -1258,26 +1323,31 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     const Region owned = fb.region(make_region(width, height, t.gx0, t.gy0, t.gwidth, t.gheight, t.x0, t.y0, t.width, t.height));
     const uint32_t frame = c->frame_index++;
     SceneDev s;
-    ST_TRY(scene_for(c, f, (size_t)t.gwidth * t.gheight, s));
-    float4* pm = c->p_mat.as<float4>();
+    ST_TRY(scene_for(c, f, (size_t)t.gwidth * t.gheight, s, &fb.uv()));
+    float4* pm = fb.pm();
     int cur = 0;
 
+    // frames in flight: this frame's primary rays and RIS start once the other slot's spatial passes are done
+    if (wait_other) HIP_TRY(hipStreamWaitEvent(st, c->pipe.after_spatial[k ^ 1], 0));
     const uint32_t ris_key = restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, 0);
     if (c->tuning.fuse_primary_ris && primary_ris_fits(s)) {   // same region: one kernel (kernels.hip k_primary_ris)
         TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),
-                                                          fb.rb(cur), nullptr, fb.rp(cur), c->tuning, c->stream));
+                                                          fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st));
     } else {
-        TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, fb.nt(0), pm, fb.nt2(), c->tuning, c->stream));
+        TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, fb.nt(0), pm, fb.nt2(), c->tuning, st));
         TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, ris_key, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), nullptr,
-                                          fb.rp(cur), c->tuning, c->queue, c->stream));
+                                          fb.rp(cur), c->tuning, c->queue, st));
     }
     if (temporal) {
+        ST_TRY(use_prev(prev, c->device, st));   // the predecessor's records are complete (its producer's stream)
         TIMED(c, RESTIR_K_TEMPORAL,
               launch_temporal(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0), camd.origin, fb.nt(cur), pm,
                               fb.ra(cur), fb.rb(cur), fb.pa(prev), fb.pb(prev), fb.ra(cur), fb.rb(cur), nullptr,
-                              fb.rp(cur), fb.rp(cur), c->tuning, c->stream));
-        used_prev(prev, c->stream);
+                              fb.rp(cur), fb.rp(cur), c->tuning, st));
+        used_prev(prev, st);
     }
+    // ... and its spatial passes once the other slot's final shading is done: a spatial pass runs alone
+    if (wait_other) HIP_TRY(hipStreamWaitEvent(st, c->pipe.after_final[k ^ 1], 0));
     bool rp_ok = fb.rp(cur) != nullptr;   // the current grid's target-pdf cache holds its samples' pdfs
     for (uint32_t pass = 0; pass < passes; pass++) {
         const Region pr = grow_rect(owned, (passes - 1u - pass) * f.R);
@@ -1290,24 +1360,32 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                              rp_ok ? fb.rp(cur) : nullptr,
                              // the last pass's pdf cache has no reader (final shading re-shades; the next frame's
                              // temporal pass evaluates its own): not written
-                             pass + 1 < passes ? fb.rp(nxt) : nullptr, &rp_ok, c->tuning, c->stream));
+                             pass + 1 < passes ? fb.rp(nxt) : nullptr, &rp_ok, c->tuning, st));
         cur = nxt;
     }
-    TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), c->rgb.as<float>(),
-                                          c->tuning, c->stream));
+    if (pipe) HIP_TRY(hipEventRecord(c->pipe.after_spatial[k], st));
+    TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), fb.rgb().as<float>(),
+                                          c->tuning, st));
+    if (pipe) {
+        HIP_TRY(hipEventRecord(c->pipe.after_final[k], st));
+        c->pipe.has[k] = true;
+        c->pipe.next = k ^ 1;
+        if (k == 1) c->pipe.slot1_busy = true;
+    }
+    c->pipe.last = k;
     c->cur = cur;
 
     if (out_next) {
-        restir_frame* fr = make_frame(c->pool, c->device, c->stream);   // after the final kernel, the records' last reader
+        restir_frame* fr = make_frame(c->pool, c->device, st);   // after the final kernel, the records' last reader
         fr->W = width; fr->H = height; fr->vx0 = t.gx0; fr->vy0 = t.gy0; fr->vw = t.gwidth; fr->vh = t.gheight; fr->N = N;
         // hand the final grid's records to the frame (no copy); the context re-allocates lazily
-        std::swap(fr->rec, c->rec[cur]);
+        std::swap(fr->rec, fb.rec_()[cur]);
         fr->records = fb.records;
         *out_next = fr;
     }
     if (out_rgb) {
-        HIP_TRY(hipMemcpyAsync(out_rgb, c->rgb.p, (size_t)t.width * t.height * 12, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpyAsync(out_rgb, fb.rgb().p, (size_t)t.width * t.height * 12, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
     }
     return RESTIR_OK;
 }
@@ -1376,6 +1454,7 @@ restir_status restir_synchronize(restir_ctx* c) {
     if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
+    if (c->slot1.stream) HIP_TRY(hipStreamSynchronize(c->slot1.stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
@@ -1387,8 +1466,11 @@ restir_status restir_download_rgb(restir_ctx* c, float* out_rgb, size_t count) {
     if (need == 0) return fail(RESTIR_ERR_STATE, "nothing rendered yet");
     if (count < need) return fail(RESTIR_ERR_INVALID, "buffer holds %zu floats, need %zu", count, need);
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemcpyAsync(out_rgb, c->rgb.p, need * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    // the last frame's rgb: slot 1's buffer and stream when frames were in flight and it rendered last
+    const bool s1 = c->pipe.last == 1;
+    const hipStream_t st = s1 ? c->slot1.stream : c->stream;
+    HIP_TRY(hipMemcpyAsync(out_rgb, (s1 ? c->slot1.rgb : c->rgb).p, need * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     return RESTIR_OK;
 }
 
@@ -1398,6 +1480,7 @@ restir_status restir_stage_configure(restir_ctx* c, uint32_t width, uint32_t hei
     if (!c || width == 0 || height == 0 || n < 1 || n > RESTIR_MAX_N) return fail(RESTIR_ERR_INVALID, "bad stage size");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
+    ST_TRY(join_slots(c));
     ST_TRY(ensure_work(c, width, height, n, true));
     ST_TRY(c->rgb.ensure((size_t)width * height * 12));
     c->rgb_w = width; c->rgb_h = height;
@@ -1468,7 +1551,8 @@ restir_status restir_stage_download(restir_ctx* c, restir_buffer which, void* ho
     std::lock_guard<std::mutex> lk(c->mu);                                          \
     if (!c->stage_ok) return fail(RESTIR_ERR_STATE, "restir_stage_configure first"); \
     if (!c->has_scene) return fail(RESTIR_ERR_STATE, "restir_set_scene first");      \
-    HIP_TRY(hipSetDevice(c->device))
+    HIP_TRY(hipSetDevice(c->device));                                               \
+    ST_TRY(join_slots(c))
 
 restir_status restir_stage_primary(restir_ctx* c, const restir_camera* cam) {
     if (!cam) return fail(RESTIR_ERR_INVALID, "camera is NULL");
@@ -1659,6 +1743,7 @@ restir_status restir_measure_read_bandwidth(restir_ctx* c, uint64_t bytes, uint3
     if (!c || !out_gbps || iters == 0 || bytes < (1u << 20)) return fail(RESTIR_ERR_INVALID, "bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
+    ST_TRY(join_slots(c));
     const size_t n4 = (size_t)(bytes / 16);
     DevBuf buf, sink;
     ST_TRY(buf.ensure(n4 * 16));
@@ -1713,6 +1798,7 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
     std::lock_guard<std::mutex> lk(c->mu);
     if (!c->has_scene) return fail(RESTIR_ERR_STATE, "restir_halo_begin before restir_set_scene");
     HIP_TRY(hipSetDevice(c->device));
+    ST_TRY(join_slots(c));
     const FeaturesDev f = to_dev(features);
     const uint32_t passes = features->spatial_reuse ? features->spatial_resampling_passes : 0u;
     restir_tile t{};
@@ -2234,6 +2320,12 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.lean")) t.spatial_lean = v;
     else if (!std::strcmp(key, "spatial.th")) { if (v > 2) return fail(RESTIR_ERR_INVALID, "spatial.th: 0 (auto), 1 or 2"); t.spatial_th = v; }
     else if (!std::strcmp(key, "fuse.primary_ris")) t.fuse_primary_ris = v;
+    else if (!std::strcmp(key, "frames.inflight")) {
+        if (v < 1u || v > 2u) return fail(RESTIR_ERR_INVALID, "frames.inflight: 1 or 2");
+        HIP_TRY(hipSetDevice(c->device));
+        if (v == 1u) ST_TRY(join_slots(c));
+        t.inflight = v;
+    }
     else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;
     else if (!std::strcmp(key, "timing.every")) { t.timing_every = v ? v : 1u; for (auto& q : c->timing_seq) q = 0; }
     else if (!std::strcmp(key, "timing.fence")) {

@@ -117,6 +117,8 @@ struct Tuning {
     uint32_t spatial_lean = 1;     // N = 1 biased passes through k_spatial1 (0: the general kernel)
     uint32_t spatial_th = 0;       // N = 1 biased ntl pass: tile height in 8-row units (1: 32x8, 2: 32x16 k_spatial1_ntl_t2; 0: by width)
     uint32_t timing_mask = 0xFFFFFFFFu;   // kernels (bit = RESTIR_K_*) bracketed by HIP events when timing is on
+    uint32_t inflight = 1;         // restir_render frame slots: 2 overlaps frame f's final shading with frame f + 1's
+                                   // primary rays + RIS (restir_ctx::Slot1; every spatial pass still runs alone)
     uint32_t timing_every = 1;     // events on every n-th launch of a timed kernel (the others launch plain)
     uint32_t timing_fence = 0;     // 1: timing events with the default system-scope release (a cache writeback after
                                    // the timed kernel: 6.7 + 4.6 us of stream gaps per C2 frame, profiles/r4); 0:

@@ -832,3 +832,52 @@ def test_full_size_c3_sequence_band_parity(gpu, oracle, N):
         assert_bits(w[:, gs], np.ascontiguousarray(a[..., 3]), f"C3 grid W rows {y0}..")
         assert_bits(col[:, gs], np.ascontiguousarray(b[..., :3]), f"C3 grid colour rows {y0}..")
         assert np.array_equal(m[:, gs], np.ascontiguousarray(b[..., 3]).view(np.uint32)), f"C3 grid M rows {y0}.."
+
+
+@pytest.mark.parametrize("temporal,passes,N", [(0, 1, 1), (1, 2, 1), (1, 1, 2)])
+def test_frames_in_flight_match_serial_frames(gpu, oracle, temporal, passes, N):
+    """frames.inflight = 2: restir_render alternates two frame slots (buffers + stream), frame f + 1's primary rays
+    and RIS overlapping frame f's final shading.  A sequence of frames (temporal reuse threading each grid into the
+    next, predecessors released as it goes) must equal the serial frames bit for bit -- RGB, returned grids and
+    restir_download_rgb of the last frame -- and the stage API afterwards must see a joined context."""
+    name = "nightclub_128pt"
+    s = get_scene(name)
+    gpu.set_scene(s)
+    cam = scene.camera_for(name, W, H)
+    f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=passes, temporal_reuse=temporal)
+
+    def run(inflight, frames=5):
+        gpu.set_tuning("frames.inflight", inflight)
+        gpu.set_seed(SEED, 0)
+        out, prev = [], None
+        for fr in range(frames):
+            want_rgb = fr % 2 == 1                      # some frames asynchronous (no RGB read back)
+            rgb, grid = gpu.render_restir(prev if temporal else None, cam, W, H, f, want_rgb=want_rgb,
+                                          want_grid=bool(temporal) or fr == frames - 1)
+            out.append((rgb, grid.download() if grid is not None else None))
+            prev = grid
+        last = gpu.download_rgb(W, H)
+        gpu.set_tuning("frames.inflight", 1)
+        return out, last
+
+    try:
+        serial, last_s = run(1)
+        piped, last_p = run(2)
+        for fr, ((a, ga), (b, gb)) in enumerate(zip(serial, piped)):
+            if a is not None:
+                assert_bits(b, a, f"frame {fr} rgb")
+            if ga is not None:
+                for x, y in zip(ga, gb):
+                    assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), f"frame {fr} grid"
+        assert_bits(last_p, last_s, "download_rgb of the last frame")
+        # the stage API after pipelined frames (joined streams): RIS on the oracle's inputs stays bit-exact
+        _, osc, cam2 = setup(gpu, oracle, name, 1)
+        n_t, p_mat = oracle.gbuffer(osc, cam2, W, H)
+        gpu.upload(_abi.BUF_GBUF_N_T, n_t)
+        gpu.upload(_abi.BUF_GBUF_P_MAT, p_mat)
+        f1 = _abi.default_features(num_samples_in_reservoir=1)
+        gpu.stage_ris(cam2, f1, key(_abi.RESTIR_STAGE_RIS))
+        a, b, _ = oracle_ris(oracle, osc, f1, cam2, n_t, p_mat)
+        assert_bits(gpu.download(_abi.BUF_RES_A), a, "stage res_a after pipelined frames")
+    finally:
+        gpu.set_tuning("frames.inflight", 1)

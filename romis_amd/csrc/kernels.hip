@@ -1823,6 +1823,32 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
     na[0] = ld_at(ia, qo[0]);
     nb[0] = ld_at(ib, qo[0]);
     const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
+    // A primary-ray miss: the target pdf of any sample there is exactly 0 (zero normal, kd = ks = 0: the biased pass's
+    // shortcut), so with every input's W finite each weighs (0 W) M = +-0 -- nothing is accepted, wSum
+    // stays FLT_MIN, the held sample is the initial (0, 0) one and W = 0 (p-hat 0, reservoir.cpp:99).  Unlike the biased
+    // pass nothing is rejected (combineUnbiased takes every neighbour), so M sums all K + 1 inputs: their reservoirs are
+    // still read, their K target pdfs and the Z loop are not.  (C5: 87 % of the 8K frame's pixels miss the box.)
+    if (cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z) &&
+        (!rp_in || pd_cached == 0.0f)) {
+        bool fin = __builtin_isfinite(ca.w) && __builtin_isfinite(na[0].w);
+        uint32_t m = __float_as_uint(cb.w) + __float_as_uint(nb[0].w);
+#pragma unroll
+        for (uint32_t n = 1; n < kLeanK; n++) {
+            if (n < K) {
+                const float4 a = ld_at(ia, qo[n]), b = ld_at(ib, qo[n]);
+                fin = fin && __builtin_isfinite(a.w);
+                m += __float_as_uint(b.w);
+            }
+        }
+        if (K == 0u) { fin = __builtin_isfinite(ca.w); m = __float_as_uint(cb.w); }
+        if (fin) {
+            st_at(oa, pofs, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+            st_at(ob, pofs, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(m)));
+            if (DBG) st_at(odbg, pofs >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
+            if (rp_out) st_at(rp_out, pofs >> 2, 0.0f);
+            return;
+        }
+    }
     const float pd_cur = rp_in ? pd_cached : target_pdf(s, f, cur, xyz(ca), xyz(cb), tb);
     Comb1 cmb;
     cmb.pos = mk(0.0f, 0.0f, 0.0f); cmb.col = mk(0.0f, 0.0f, 0.0f);

@@ -1787,7 +1787,7 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
                                                const float4* __restrict__ ia, const float4* __restrict__ ib,
                                                float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
                                                const float* __restrict__ rp_in, const float* __restrict__ rp_nb,
-                                               float* __restrict__ rp_out) {
+                                               float* __restrict__ rp_out, uint8_t* __restrict__ vis_out) {
     const Bvh bvh = VIS ? stage_bvh(s, g_lds) : global_bvh(s);   // ends with a barrier (every thread gets here)
     const GlTabs tb = gl_stage_tables();
     uint32_t tile;
@@ -1846,6 +1846,7 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
             st_at(ob, pofs, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(m)));
             if (DBG) st_at(odbg, pofs >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
             if (rp_out) st_at(rp_out, pofs >> 2, 0.0f);
+            if (vis_out) vis_out[pofs >> 4] = 0u;
             return;
         }
     }
@@ -1870,6 +1871,7 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
     float pc = cmb.pd;
     if (!cmb.has_pd) pc = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, cmb.pos, cmb.col, tb);
     float W = 0.0f;
+    uint8_t vis_own = 0u;
     if (pc != 0.0f) {   // W = 0 whatever Z is when p-hat(pixel, held sample) == 0 (reservoir.cpp:99)
         unsigned long long Z = 0ull;
 #pragma unroll
@@ -1882,9 +1884,16 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
                 if (pos && (!VIS || visible(bvh, rp.P, cmb.pos))) Z += Mn[n];
             }
         }
-        if (pc > 0.0f && (!VIS || visible(bvh, cur.P, cmb.pos))) Z += __float_as_uint(cb.w);
+        if (pc > 0.0f) {
+            const bool v = !VIS || visible(bvh, cur.P, cmb.pos);
+            if (v) Z += __float_as_uint(cb.w);
+            vis_own = VIS ? (v ? 1u : 2u) : 0u;
+        }
         if (Z != 0ull) W = (rcp_rn(pc) * rcp_rn((float)Z)) * cmb.wsum;
     }
+    // the pixel's own shadow ray to the held sample is the ray final shading casts for this pixel (the same P and
+    // sample): its result is handed on (1 visible, 2 occluded, 0 not cast) when this pass's output is shaded next
+    if (vis_out) vis_out[pofs >> 4] = vis_own;
     st_at(oa, pofs, make_float4(cmb.pos.x, cmb.pos.y, cmb.pos.z, W));
     st_at(ob, pofs, make_float4(cmb.col.x, cmb.col.y, cmb.col.z, __uint_as_float(cmb.macc)));
     if (DBG) st_at(odbg, pofs >> 1, make_float2(cmb.wsum, cmb.chosen));
@@ -1898,8 +1907,9 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
                                                                            const float4* ia, const float4* ib,          \
                                                                            float4* oa, float4* ob, float2* odbg,        \
                                                                            const float* rp_in, const float* rp_nb,      \
-                                                                           float* rp_out) {                             \
-        spatial1u_body<DBG, VIS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_nb, rp_out); \
+                                                                           float* rp_out, uint8_t* vis_out) {           \
+        spatial1u_body<DBG, VIS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_nb, rp_out, \
+                                 vis_out);                                                                            \
     }
 ROMIS_SPATIAL1U_KERNEL(false, false, k_spatial1u)
 ROMIS_SPATIAL1U_KERNEL(true, false, k_spatial1u_dbg)
@@ -1971,7 +1981,7 @@ template <bool LDS_BVH, int NT>
 __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, v3 origin,
                                                   const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                                   const float4* __restrict__ ra, const float4* __restrict__ rb,
-                                                  float* __restrict__ rgb) {
+                                                  float* __restrict__ rgb, const uint8_t* __restrict__ vis_in) {
     // NT shadow rays per pixel (one per sub-reservoir): ray j * 256 + t is pixel t's sub-reservoir j
     constexpr uint32_t kRays = 256u * NT;
     __shared__ uint32_t s_hist[256];
@@ -1999,6 +2009,12 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
             sc[j] = shade(s, f, px, r[j].pos, r[j].col, tb);
             need[j] = sc[j].x != 0.0f || sc[j].y != 0.0f || sc[j].z != 0.0f;   // see final_body: no ray when sc == 0
         }
+    }
+    // N = 1 after an unbiased + visibility pass: that pass's own-pixel ray (same P, same sample) where it cast one
+    uint8_t known = 0u;
+    if (NT == 1 && vis_in && valid && need[0]) {
+        known = vis_in[p];
+        if (known) need[0] = false;
     }
     s_hist[t] = 0u;
     __syncthreads();
@@ -2050,6 +2066,7 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
     for (int j = 0; j < NT; j++) {
         v3 c = sc[j];
         if (need[j] && !s_vis[(uint32_t)j * 256u + t]) c = mk(0.0f, 0.0f, 0.0f);
+        if (j == 0 && known == 2u) c = mk(0.0f, 0.0f, 0.0f);   // the spatial pass's ray was occluded
         color = vadd(color, vscale(c, r[j].W));
     }
     color = vdivs(color, (float)NT);
@@ -2065,13 +2082,14 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
 
 extern "C" __global__ __launch_bounds__(256) void k_final_n1_sorted(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,
                                                                    float oz, const float4* n_t, const float4* p_mat,
-                                                                   const float4* ra, const float4* rb, float* rgb) {
-    final_sorted_body<true, 1>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb);
+                                                                   const float4* ra, const float4* rb, float* rgb,
+                                                                   const uint8_t* vis_in) {
+    final_sorted_body<true, 1>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, vis_in);
 }
 extern "C" __global__ __launch_bounds__(256) void k_final_n2_sorted(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,
                                                                    float oz, const float4* n_t, const float4* p_mat,
                                                                    const float4* ra, const float4* rb, float* rgb) {
-    final_sorted_body<true, 2>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb);
+    final_sorted_body<true, 2>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, nullptr);
 }
 
 #define ROMIS_FINAL_KERNEL(NT, LDS, NAME)                                                                              \
@@ -2972,8 +2990,9 @@ hipError_t launch_temporal(const SceneDev& s, const Region& rg0, const FeaturesD
 hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
                           const float4* n_t, const float4* p_mat, const float4* ia, const float4* ib, float4* oa,
                           float4* ob, float2* odbg, const float* rp_in, const float* rp_nb, float* rp_out,
-                          bool* rp_written, const Tuning& tu, hipStream_t stream) {
+                          bool* rp_written, const Tuning& tu, hipStream_t stream, uint8_t* vis_out, bool* vis_written) {
     if (rp_written) *rp_written = false;
+    if (vis_written) *vis_written = false;
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     Region rg = with_map(rg0, tu.spatial_xcd);   // XCD-banded order works on 2D tiles
     if (rg.map2d && tu.spatial_wave8) rg.map2d = 2u;
@@ -2991,9 +3010,11 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
                                                           : tu.spatial_xcd_rows;
         if (rg.xcd_rows) grid = 8u * ((((nty + rg.xcd_rows - 1) / rg.xcd_rows) + 7u) / 8u) * rg.xcd_rows * ntx;
         auto k = f.spatial_vis ? (odbg ? k_spatial1u_vis_dbg : k_spatial1u_vis) : (odbg ? k_spatial1u_dbg : k_spatial1u);
+        uint8_t* vo = f.spatial_vis ? vis_out : nullptr;   // the own-pixel shadow ray, for final shading (N = 1)
         ROMIS_LAUNCH(k, dim3(grid), dim3(kBlock), f.spatial_vis ? bvh_bytes : 0, stream, s, rg, f, key, o[0], o[1], o[2],
-                     n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_in ? rp_nb : nullptr, rp_out);
+                     n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_in ? rp_nb : nullptr, rp_out, vo);
         if (rp_written) *rp_written = rp_out != nullptr;
+        if (vis_written) *vis_written = vo != nullptr;
         return hipGetLastError();
     }
     if (lean2 && !f.unbiased && f.R <= kLdsSpatialR && tu.spatial_lds == 3u) {
@@ -3061,7 +3082,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
 
 hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev& f, const float* o, const float4* n_t,
                         const float4* p_mat, const float4* ra, const float4* rb, float* rgb, const Tuning& tu,
-                        hipStream_t stream) {
+                        hipStream_t stream, const uint8_t* vis_in) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, tu.final_2d);
     const size_t lds = bvh_lds_bytes(s);
@@ -3069,8 +3090,12 @@ hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev&
     auto k = use_lds ? (f.N == 1 ? k_final_n1_lds : (f.N == 2 ? k_final_n2_lds : k_final_n0_lds))
                      : (f.N == 1 ? k_final_n1 : (f.N == 2 ? k_final_n2 : k_final_n0));
     if (tu.final_sort && use_lds && (f.N == 1 || f.N == 2) && rg.map2d) {   // one tile per block
-        ROMIS_LAUNCH(f.N == 1 ? k_final_n1_sorted : k_final_n2_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, s,
-                     rg, f, o[0], o[1], o[2], n_t, p_mat, ra, rb, rgb);
+        if (f.N == 1)
+            ROMIS_LAUNCH(k_final_n1_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, s, rg, f, o[0], o[1], o[2], n_t,
+                         p_mat, ra, rb, rgb, vis_in);
+        else
+            ROMIS_LAUNCH(k_final_n2_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, s, rg, f, o[0], o[1], o[2], n_t,
+                         p_mat, ra, rb, rgb);
         return hipGetLastError();
     }
     ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.final_blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,

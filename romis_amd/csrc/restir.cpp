@@ -218,6 +218,7 @@ struct restir_ctx {
     DevBuf rec[2];                                  // restir_render / halo frames: per-pixel records
     std::shared_ptr<FramePool> pool = std::make_shared<FramePool>();
     DevBuf rp[2];                                   // their target-pdf cache planes (N = 1, planes layout)
+    DevBuf vis;                                     // unbiased + visibility pass -> final shading: own-pixel ray
     int cur = 0;
     uint32_t rgb_w = 0, rgb_h = 0;
     // Frames in flight (tuning frames.inflight = 2): restir_render alternates two frame slots -- slot 0 is the buffers
@@ -227,7 +228,7 @@ struct restir_ctx {
     // spatial pass never shares the GPU with another kernel (its timed duration stays the pass alone).
     struct Slot1 {
         hipStream_t stream = nullptr;
-        DevBuf n_t, p_mat, rec[2], rp[2], rgb, uv;
+        DevBuf n_t, p_mat, rec[2], rp[2], rgb, uv, vis;
     } slot1;
     struct {
         hipEvent_t after_spatial[2] = {nullptr, nullptr}, after_final[2] = {nullptr, nullptr}, joined = nullptr;
@@ -714,6 +715,7 @@ struct FrameBufs {
     float4* pm() const { return (slot ? c->slot1.p_mat : c->p_mat).as<float4>(); }
     DevBuf& rgb() const { return slot ? c->slot1.rgb : c->rgb; }
     DevBuf& uv() const { return slot ? c->slot1.uv : c->uv; }
+    DevBuf& vis() const { return slot ? c->slot1.vis : c->vis; }
     float4* nt(int i) const { return records ? rec_()[i].as<float4>() : n_t_().as<float4>(); }
     float4* ra(int i) const { return rec_()[i].as<float4>() + (records ? 1 : 0); }
     float4* rb(int i) const { return rec_()[i].as<float4>() + (records ? 2 : npx * N); }
@@ -823,7 +825,7 @@ void restir_destroy(restir_ctx* c) {
         (void)hipStreamSynchronize(c->stream);
         if (c->slot1.stream) (void)hipStreamSynchronize(c->slot1.stream);
         for (DevBuf* b : {&c->slot1.n_t, &c->slot1.p_mat, &c->slot1.rec[0], &c->slot1.rec[1], &c->slot1.rp[0],
-                          &c->slot1.rp[1], &c->slot1.rgb, &c->slot1.uv})
+                          &c->slot1.rp[1], &c->slot1.rgb, &c->slot1.uv, &c->slot1.vis, &c->vis})
             b->release();
         for (hipEvent_t* e : {&c->pipe.after_spatial[0], &c->pipe.after_spatial[1], &c->pipe.after_final[0],
                               &c->pipe.after_final[1], &c->pipe.joined})
@@ -1349,6 +1351,13 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     // ... and its spatial passes once the other slot's final shading is done: a spatial pass runs alone
     if (wait_other) HIP_TRY(hipStreamWaitEvent(st, c->pipe.after_final[k ^ 1], 0));
     bool rp_ok = fb.rp(cur) != nullptr;   // the current grid's target-pdf cache holds its samples' pdfs
+    // the last pass's own-pixel shadow rays (unbiased + visibility reuse, N = 1) go on to final shading
+    uint8_t* vis = nullptr;
+    bool vis_ok = false;
+    if (passes && features->unbiased_combination && features->spatial_reuse_visibility_check && N == 1) {
+        ST_TRY(fb.vis().ensure((size_t)t.gwidth * t.gheight));
+        vis = fb.vis().as<uint8_t>();
+    }
     for (uint32_t pass = 0; pass < passes; pass++) {
         const Region pr = grow_rect(owned, (passes - 1u - pass) * f.R);
         const int nxt = cur ^ 1;
@@ -1360,12 +1369,13 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                              rp_ok ? fb.rp(cur) : nullptr,
                              // the last pass's pdf cache has no reader (final shading re-shades; the next frame's
                              // temporal pass evaluates its own): not written
-                             pass + 1 < passes ? fb.rp(nxt) : nullptr, &rp_ok, c->tuning, st));
+                             pass + 1 < passes ? fb.rp(nxt) : nullptr, &rp_ok, c->tuning, st,
+                             pass + 1 == passes ? vis : nullptr, &vis_ok));
         cur = nxt;
     }
     if (pipe) HIP_TRY(hipEventRecord(c->pipe.after_spatial[k], st));
     TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), fb.rgb().as<float>(),
-                                          c->tuning, st));
+                                          c->tuning, st, vis_ok ? vis : nullptr));
     if (pipe) {
         HIP_TRY(hipEventRecord(c->pipe.after_final[k], st));
         c->pipe.has[k] = true;

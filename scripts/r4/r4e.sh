@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/r4e
 mkdir -p $OUT
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_halo.py -m gpu -x -q --timeout 300 \
-    --timeout-method thread -k "in_flight or full_size_c2 or c3_sequence or record_only or stitch or unbiased or c4_c5 or extreme" > $OUT/tests.log 2>&1 \
+    --timeout-method thread -k "in_flight or full_size_c2 or c3_sequence or record_only or stitch or unbiased or c4_c5 or extreme or render_frame_matches" > $OUT/tests.log 2>&1 \
     || { tail -30 $OUT/tests.log; exit 21; }
 tail -1 $OUT/tests.log
 for rep in 1 2; do

@@ -392,7 +392,8 @@ def assert_grid(grid, res, what):
 # ceiling lights), C5 (4096 lights, M=64, unbiased + visibility reuse), plus the default N=2 / two passes
 @pytest.mark.parametrize("name,N,passes,unbiased,M,vis", [
     ("cornell_parallelogram", 1, 0, 0, 32, 0), ("nightclub_128pt", 1, 1, 0, 32, 0), ("nightclub_512", 2, 2, 0, 32, 0),
-    ("cornell_parallelogram", 1, 2, 1, 32, 0), ("cornell_1024", 1, 1, 0, 32, 0), ("cornell_4096", 1, 1, 1, 64, 1)])
+    ("cornell_parallelogram", 1, 2, 1, 32, 0), ("cornell_1024", 1, 1, 0, 32, 0), ("cornell_4096", 1, 1, 1, 64, 1),
+    ("nightclub_128pt", 1, 2, 1, 32, 1), ("cornell_parallelogram", 1, 1, 1, 32, 1)])
 def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased, M, vis):
     s = get_scene(name)
     gpu.set_scene(s)

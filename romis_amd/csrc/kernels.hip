@@ -1375,10 +1375,28 @@ __device__ __forceinline__ bool xcd_tile(const Region& rg, uint32_t T, uint32_t 
         return j < q + (x < rem ? 1u : 0u);
     }
     const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
-    const uint32_t chunk = rg.xcd_rows * ntx;
-    const uint32_t i = j / chunk;
-    tile = ((x + 8u * i) * rg.xcd_rows) * ntx + (j - i * chunk);
-    return tile < T;
+    if (rg.xcd_cols == 0u || rg.xcd_cols >= ntx) {
+        const uint32_t chunk = rg.xcd_rows * ntx;
+        const uint32_t i = j / chunk;
+        tile = ((x + 8u * i) * rg.xcd_rows) * ntx + (j - i * chunk);
+        return tile < T;
+    }
+    // 2-D chunks of xcd_rows x xcd_cols tiles, numbered row-major over the image; XCD x takes chunks x, x + 8, ...
+    const uint32_t cw = rg.xcd_cols, ncx = (ntx + cw - 1u) / cw, chunk = rg.xcd_rows * cw;
+    const uint32_t i = j / chunk, k = j - i * chunk, c = x + 8u * i;
+    const uint32_t cr = c / ncx, tr = k / cw;
+    const uint32_t col = (c - cr * ncx) * cw + (k - tr * cw);
+    tile = (cr * rg.xcd_rows + tr) * ntx + col;
+    return col < ntx && tile < T;
+}
+
+// Blocks for xcd_tile's order over ntx x nty tiles (rg.xcd_rows, rg.xcd_cols set): every XCD gets as many as the one
+// that owns the most chunks.
+inline uint32_t xcd_grid(const Region& rg, uint32_t ntx, uint32_t nty) {
+    if (rg.xcd_rows == 0u) return ntx * nty;
+    const uint32_t cw = (rg.xcd_cols == 0u || rg.xcd_cols >= ntx) ? ntx : rg.xcd_cols;
+    const uint32_t chunks = ((nty + rg.xcd_rows - 1u) / rg.xcd_rows) * ((ntx + cw - 1u) / cw);
+    return 8u * ((chunks + 7u) / 8u) * rg.xcd_rows * cw;
 }
 
 template <bool DBG>
@@ -3008,7 +3026,8 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
         rg.xcd_rows = tu.spatial_xcd_rows == kXcdRowsAuto ? std::max(1u, std::min(8u, 8192u / std::max(rg.rw, 1u)))
                                                           : tu.spatial_xcd_rows;
-        if (rg.xcd_rows) grid = 8u * ((((nty + rg.xcd_rows - 1) / rg.xcd_rows) + 7u) / 8u) * rg.xcd_rows * ntx;
+        rg.xcd_cols = tu.spatial_xcd_cols;
+        if (rg.xcd_rows) grid = xcd_grid(rg, ntx, nty);
         auto k = f.spatial_vis ? (odbg ? k_spatial1u_vis_dbg : k_spatial1u_vis) : (odbg ? k_spatial1u_dbg : k_spatial1u);
         uint8_t* vo = f.spatial_vis ? vis_out : nullptr;   // the own-pixel shadow ray, for final shading (N = 1)
         ROMIS_LAUNCH(k, dim3(grid), dim3(kBlock), f.spatial_vis ? bvh_bytes : 0, stream, s, rg, f, key, o[0], o[1], o[2],
@@ -3023,7 +3042,8 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
         rg.xcd_rows = tu.spatial_xcd_rows == kXcdRowsAuto ? std::max(1u, std::min(8u, 8192u / std::max(rg.rw, 1u)))
                                                           : tu.spatial_xcd_rows;
-        if (rg.xcd_rows) grid = 8u * ((((nty + rg.xcd_rows - 1) / rg.xcd_rows) + 7u) / 8u) * rg.xcd_rows * ntx;
+        rg.xcd_cols = tu.spatial_xcd_cols;
+        if (rg.xcd_rows) grid = xcd_grid(rg, ntx, nty);
         ROMIS_LAUNCH(odbg ? k_spatial2_ntl_dbg : k_spatial2_ntl, dim3(grid), dim3(kBlock), kApronMax * 16u, stream, s, rg, f,
                      key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg);
         return hipGetLastError();
@@ -3038,10 +3058,8 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
             // 4 tile rows at 1920 px, 2 at 3840 (kbench: 4K 239 -> 225 us with 2, 1080p best with 4; r2bb)
             rg.xcd_rows = std::max(1u, std::min(8u, 8192u / std::max(rg.rw, 1u)));
         }
-        if (rg.xcd_rows) {
-            const uint32_t chunks = (nty + rg.xcd_rows - 1) / rg.xcd_rows;
-            grid = 8u * ((chunks + 7u) / 8u) * rg.xcd_rows * ntx;
-        }
+        rg.xcd_cols = tu.spatial_xcd_cols;
+        if (rg.xcd_rows) grid = xcd_grid(rg, ntx, nty);
         // 32x16 tiles (k_spatial1_ntl_t2) where the auto XCD chunk is at most 2 tile rows (wide images): C4 222 ->
         // 203 us, C2 76.8 -> 79.0 (cfg_kbench, profiles/r3/r3k); spatial.th = 1 / 2 forces either
         const uint32_t th = tu.spatial_th ? tu.spatial_th : (8192u / std::max(rg.rw, 1u) <= 2u ? 2u : 1u);
@@ -3049,8 +3067,9 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
             // 32x16 tiles: the chunks hold half as many (twice as tall) tile rows
             const uint32_t nty2 = (rg.rh + 2u * kTileH - 1) / (2u * kTileH);
             if (rg.xcd_rows) {
-                rg.xcd_rows = std::max(1u, rg.xcd_rows / 2u);
-                grid = 8u * ((((nty2 + rg.xcd_rows - 1) / rg.xcd_rows) + 7u) / 8u) * rg.xcd_rows * ntx;
+                // an explicit spatial.xcd_rows counts 32 x 16 tile rows here; the automatic one is halved
+                if (tu.spatial_xcd_rows == kXcdRowsAuto) rg.xcd_rows = std::max(1u, rg.xcd_rows / 2u);
+                grid = xcd_grid(rg, ntx, nty2);
             } else {
                 grid = ntx * nty2;
             }

@@ -93,6 +93,7 @@ struct Region {
     // [n_t, a_0, b_0, a_1, b_1, ...] (restir_render): ps = 1 + 2N, js = 2, with res_a = rec + 1, res_b = rec + 2.
     uint32_t ps, js;
     uint32_t xcd_rows;   // k_spatial1's XCD tile order (xcd_tile); 0 elsewhere
+    uint32_t xcd_cols;   // chunk width in tiles (xcd_tile); 0 = the whole row of tiles
 };
 
 // Launch-shape knobs (restir_set_tuning); they never change results, only speed.
@@ -111,6 +112,8 @@ struct Tuning {
                                    // (k_spatial1, gathers; also any R > 10)
     uint32_t spatial_xcd_rows = 255; // k_spatial1: XCD x takes every 8th chunk of this many tile rows (0: one band;
                                      // 255 = kXcdRowsAuto: as many as keep a chunk's records in one XCD's L2)
+    uint32_t spatial_xcd_cols = 0;   // chunk width in tiles (0: full rows); 2-D chunks keep the +-R window rows of
+                                     // consecutive tile rows in the XCD's L2 on wide images
     uint32_t spatial_blocks = 0;
     uint32_t spatial_wave8 = 1;    // waves cover 8x8 pixel blocks instead of 32x2 rows (-2..4 %, kbench)
     uint32_t fuse_primary_ris = 1; // restir_render: k_primary_ris instead of k_primary + k_ris when the BVH fits LDS

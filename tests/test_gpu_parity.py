@@ -210,8 +210,13 @@ SPATIAL_VARIANTS = {"gather": {"spatial.lean": 1, "spatial.lds": 0},
                     "ntl_rows2": {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 2},
                     "ntl_t2": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 2},
                     "ntl_t2_band": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 2, "spatial.xcd_rows": 0},
+                    # 2-D XCD chunks (2 x 2 tiles; the image's 3 tile columns leave a partial chunk on the right)
+                    "ntl_2d": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 1, "spatial.xcd_rows": 2,
+                               "spatial.xcd_cols": 2},
+                    "ntl_t2_2d": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 2, "spatial.xcd_rows": 1,
+                                  "spatial.xcd_cols": 2},
                     "general": {"spatial.lean": 0}}
-SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 255, "spatial.th": 0}
+SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 255, "spatial.xcd_cols": 0, "spatial.th": 0}
 
 
 # every (scene, N, combine mode) through the default knobs ("gather" selects the lean gather kernel for N = 1 biased
@@ -219,7 +224,9 @@ SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 255
 SPATIAL_CASES = ([("gather", name, N, mode) for name in ("nightclub_128pt", "cornell_parallelogram") for N in (1, 2, 3)
                   for mode in ("biased", "unbiased", "unbiased_vis")] +
                  [(lean, name, 1, "biased") for lean in SPATIAL_VARIANTS if lean != "gather"
-                  for name in ("nightclub_128pt", "cornell_parallelogram")])
+                  for name in ("nightclub_128pt", "cornell_parallelogram")] +
+                 [("ntl_2d", "cornell_parallelogram", N, mode) for N in (1, 2) for mode in ("unbiased_vis", "biased")
+                  if (N, mode) != (1, "biased")])
 
 
 @pytest.mark.parametrize("lean,name,N,mode", SPATIAL_CASES)

@@ -2321,6 +2321,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.blocks")) t.spatial_blocks = v;
     else if (!std::strcmp(key, "spatial.xcd_rows")) t.spatial_xcd_rows = v;
     else if (!std::strcmp(key, "spatial.xcd_cols")) t.spatial_xcd_cols = v;
+    else if (!std::strcmp(key, "ris.late")) t.ris_late = v;
     else if (!std::strcmp(key, "spatial.lds")) {
         if (v != 0u && v != 3u)
             return fail(RESTIR_ERR_INVALID, "spatial.lds: 0 (gathers) or 3 (n_t window, default); 1, 2 and 4 were measured "

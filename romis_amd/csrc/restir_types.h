@@ -107,6 +107,8 @@ struct Tuning {
     uint32_t ris_queue = 0;        // persistent blocks (this many) pulling tiles from a WorkQueue; 0 = off
     uint32_t ris_compact = 1;      // N <= 2: compact light tables for point-light-only scenes and light grids (_pt /
                                    // _grid RIS kernels, kernels.hip ris_light_form)
+    uint32_t ris_late = 1;         // fused primary + RIS, one tile per block: stage the light table only for tiles with
+                                   // a pixel that runs the candidate loop (0: every tile, before the primary rays)
     uint32_t spatial_xcd = 1;      // XCD-banded tile order
     uint32_t spatial_lds = 3;      // N = 1 biased: 3 the n_t window in LDS (k_spatial1_ntl, default), 0 no window
                                    // (k_spatial1, gathers; also any R > 10)

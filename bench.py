@@ -83,10 +83,12 @@ def parse():
                     help="HIP events on every n-th spatial launch of the timed region (the event-carrying dispatch "
                          "costs ~9 us of stream gaps, profiles/r4/gap); the roofline's average launch time is over "
                          "those launches")
-    ap.add_argument("--inflight", type=int, default=2, choices=[1, 2],
+    ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
                     help="frames in flight (restir_set_tuning frames.inflight): 2 overlaps frame f's final shading with "
                          "frame f + 1's primary rays + RIS on a second stream; the spatial pass still runs alone, so "
-                         "its timed duration is the pass's (halo-mode frames: always 1)")
+                         "its timed duration is the pass's (halo-mode frames: always 1).  Measured slower at C2 "
+                         "(0.461 -> 0.480 ms: RIS and final shading co-running take as long as in series; "
+                         "profiles/r4/r4e), so 1 is the default")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="restir_set_tuning knobs for A/B runs (launch shapes and timing only; results are identical)")
     ap.add_argument("--traffic-csv", default=None,

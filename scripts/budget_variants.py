@@ -77,6 +77,11 @@ VARIANTS = {
                          "const uint32_t li_ = (uint32_t)(lt - lights) >> 1; "
                          "pos = vadd(vadd(mk((float)(li_ >> 6) * 0.01f, 0.9f, (float)(li_ & 63u) * 0.01f), "
                          "vscale(shared_row(1), a)), vscale(shared_row(2), b));\n\\1const v3 gc = mk(0.5f, 0.5f, 0.5f);")],
+    # kLtRegular (C4 / C5): the drawn light's colour gather replaced by a value of its index (no memory access)
+    "ris_reg_noload": [(r"const v3 gc = xyz\(lights\[i\]\);",
+                        "const v3 gc = mk(0.5f + (float)(i & 7u) * 0.01f, 0.5f, 0.5f);")],
+    # no candidate loop at all (every pixel takes the miss path): primary rays + stores, the kernel's floor
+    "ris_no_cand": [(r"\? 0u : f\.M;", "? 0u : 0u;")],
     # pieces of the target pdf itself (shared device functions: every kernel changes, RIS is the one timed)
     "risg_no_pow": [(r"return pow_pre\(x, px, pw, job\) \? pw : pow_core\(tb, job, px\.kd_sh\.w\);",
                      "return x * px.kd_sh.w;")],

@@ -36,6 +36,9 @@ for c in c4 c5 c2; do
         --variants late:ris.late=1 early:ris.late=0 > $OUT/late_$c.json 2> $OUT/late_$c.err || { tail -5 $OUT/late_$c.err; exit 27; }
     cat $OUT/late_$c.json
 done
+# RIS ablations at C5 / C4 (scripts/budget_variants.py): the colour gather of kLtRegular, the candidate loop
+bash scripts/ab_libs_cfg.sh r4f/ab c5 "--rounds 3 --frames 3" ris_reg_noload ris_no_cand || exit 28
+bash scripts/ab_libs_cfg.sh r4f/ab c4 "--rounds 3 --frames 8" ris_reg_noload ris_no_cand || exit 29
 timeout -k 10 60 scripts/probes/_bin/fetch_probe > $OUT/fetch_probe.jsonl 2>&1 || { cat $OUT/fetch_probe.jsonl; exit 24; }
 cat $OUT/fetch_probe.jsonl
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/probe_FETCH_SIZE -o run -- \

@@ -1159,6 +1159,9 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
         finite = finite && tfinite;   // texels are diffuse colours too
         kmax = std::max(kmax, tmax);
         s.shade_finite = (finite && cmax * kmax <= 0x1p120) ? 1u : 0u;
+        bool miss_zero = s.lights_finite && cmax <= 0x1p126;
+        for (int a : {0, 1, 2, 4, 5, 6}) miss_zero = miss_zero && mats[12 * num_meshes + a] == 0.0f;
+        s.miss_shade_zero = miss_zero ? 1u : 0u;
     }
     s.normals_bounded = 1u;
     for (const std::vector<float>* nv : {&n0, &n1, &n2})
@@ -2322,6 +2325,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.xcd_rows")) t.spatial_xcd_rows = v;
     else if (!std::strcmp(key, "spatial.xcd_cols")) t.spatial_xcd_cols = v;
     else if (!std::strcmp(key, "ris.late")) t.ris_late = v;
+    else if (!std::strcmp(key, "final.miss")) t.final_miss = v;
     else if (!std::strcmp(key, "spatial.lds")) {
         if (v != 0u && v != 3u)
             return fail(RESTIR_ERR_INVALID, "spatial.lds: 0 (gathers) or 3 (n_t window, default); 1, 2 and 4 were measured "

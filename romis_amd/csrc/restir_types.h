@@ -67,6 +67,9 @@ struct SceneDev {
     uint32_t shade_finite;     // every light colour x material kd / ks product is finite (shade()'s NaN tests)
     uint32_t normals_bounded;  // every vertex normal component finite with |n| <= 2^125: interpolated normals are
                                // finite, so a miss pixel's zero normal rejects every neighbour (dot = +-0)
+    uint32_t miss_shade_zero;  // the miss material's kd and ks are 0 and every light colour is finite with |c| <= 2^126
+                               // (so every light sample's colour, a convex mix, is finite): a miss pixel shades any
+                               // light sample to +-0 (k_final's miss shortcut)
     // Textures (Material::kdTexture): texels as float4 (rgb, 0), all images back to back; tex_dims[i] =
     // (width, height, first texel, 0); per-triangle texture coordinates by original index, 2 float4 each:
     // (t0.xy, t1.xy), (t2.xy, 0, 0).  materials[3m + 2].w = bits(kd_texture), 0 = none.
@@ -133,6 +136,7 @@ struct Tuning {
     uint32_t final_blocks = 0;
     uint32_t final_lds = 1;
     uint32_t final_2d = 1;
+    uint32_t final_miss = 1;       // k_final_n*_sorted: primary-ray misses read p_mat + (pos, W) only (SceneDev::miss_shade_zero)
     uint32_t final_sort = 1;       // N = 1: bin each tile's shadow rays by target before tracing (-2.4 %, r2ah)
     uint32_t mis_chunk = 0;        // R-OMIS samples per k_romis_samples / k_romis_accum pair; 0 = the scratch budget
 };

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/r4f
 mkdir -p $OUT
 timeout -k 10 700 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread \
-    -k "ntl_2d or ntl_t2_2d or compact_light or render_frame_matches or c4_c5 or full_size_c2" > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 21; }
+    -k "ntl_2d or ntl_t2_2d or compact_light or render_frame_matches or c4_c5 or full_size_c2 or final or extreme" > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 21; }
 tail -1 $OUT/tests.log
 # C4: spatial.xcd_rows counts 32 x 16 tile rows (k_spatial1_ntl_t2); 30 tiles = 960 px
 C4=("chunks:spatial.xcd_rows=255" "r2c30:spatial.xcd_rows=2,spatial.xcd_cols=30" "r4c30:spatial.xcd_rows=4,spatial.xcd_cols=30"
@@ -33,7 +33,7 @@ done
 # the light table staged after the primary rays, only for tiles with a hit (ris.late = 1, default) vs every tile
 for c in c4 c5 c2; do
     timeout -k 10 300 python3 scripts/cfg_kbench.py --config $c --rounds 4 --frames $([ $c = c5 ] && echo 3 || echo 8) \
-        --variants late:ris.late=1 early:ris.late=0 > $OUT/late_$c.json 2> $OUT/late_$c.err || { tail -5 $OUT/late_$c.err; exit 27; }
+        --variants late:ris.late=1 early:ris.late=0,final.miss=0 > $OUT/late_$c.json 2> $OUT/late_$c.err || { tail -5 $OUT/late_$c.err; exit 27; }
     cat $OUT/late_$c.json
 done
 # RIS ablations at C5 / C4 (scripts/budget_variants.py): the colour gather of kLtRegular, the candidate loop

@@ -21,6 +21,7 @@ SRC = os.path.join(build.CSRC, "kernels.hip")
 SPANS = {   # the function each variant patches: (first line, the text that follows the function)
     "spatial": ("__device__ __forceinline__ void spatial1_ntl_body(", "#ifndef ROMIS_SPATIAL1_NTL_WPE"),
     "ris": ("__device__ __forceinline__ void ris_pixel(", "// k_ris: genCanonicalSamples per pixel."),
+    "spatialu": ("__device__ __forceinline__ void spatial1u_body(", "#define ROMIS_SPATIAL1U_KERNEL"),
 }
 
 
@@ -82,6 +83,15 @@ VARIANTS = {
                         "const v3 gc = mk(0.5f + (float)(i & 7u) * 0.01f, 0.5f, 0.5f);")],
     # no candidate loop at all (every pixel takes the miss path): primary rays + stores, the kernel's floor
     "ris_no_cand": [(r"\? 0u : f\.M;", "? 0u : 0u;")],
+    # k_spatial1u (C5's unbiased + visibility pass): the Z loop's shadow rays, its sign-only target pdfs, its
+    # G-buffer gathers, and the combine's K target pdfs, each replaced by a data-dependent stand-in
+    "u_no_vis": [(r"\(!VIS \|\| visible\(bvh, rp\.P, cmb\.pos\)\)", "(!VIS || rp.P.x != cmb.pos.x)"),
+                 (r"const bool v = !VIS \|\| visible\(bvh, cur\.P, cmb\.pos\);", "const bool v = !VIS || cur.P.x != cmb.pos.x;")],
+    "u_no_zphat": [(r": target_pdf_positive\(s, f, rp, cmb\.pos, cmb\.col, tb\);", ": rp.P.y != cmb.pos.y;")],
+    "u_no_zload": [(r"const float4 qn = ld_at\(n_t, qo\[n\]\), qp = ld_at\(p_mat, qo\[n\]\);",
+                    "const float4 qn = cn, qp = make_float4(cpm.x + (float)n, cpm.y, cpm.z, cpm.w);")],
+    "u_no_comb": [(r"cmb\.take\(target_pdf\(s, f, cur, p, c, tb\), na\[n\]\.w",
+                   "cmb.take(p.x * c.y + cur.P.z, na[n].w")],
     # pieces of the target pdf itself (shared device functions: every kernel changes, RIS is the one timed)
     "risg_no_pow": [(r"return pow_pre\(x, px, pw, job\) \? pw : pow_core\(tb, job, px\.kd_sh\.w\);",
                      "return x * px.kd_sh.w;")],
@@ -106,7 +116,7 @@ def main():
         if name.startswith("risg_"):
             a, b = 0, len(src)
         else:
-            a, b = body_span(src, "ris" if name.startswith("ris_") else "spatial")
+            a, b = body_span(src, "ris" if name.startswith("ris_") else "spatialu" if name.startswith("u_") else "spatial")
         body = src[a:b]
         for pat, rep in subs:
             body, n = re.subn(pat, rep, body)

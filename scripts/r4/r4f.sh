@@ -39,6 +39,8 @@ done
 # RIS ablations at C5 / C4 (scripts/budget_variants.py): the colour gather of kLtRegular, the candidate loop
 bash scripts/ab_libs_cfg.sh r4f/ab c5 "--rounds 3 --frames 3" ris_reg_noload ris_no_cand || exit 28
 bash scripts/ab_libs_cfg.sh r4f/ab c4 "--rounds 3 --frames 8" ris_reg_noload ris_no_cand || exit 29
+# C5's unbiased + visibility pass: Z-loop rays / sign-only p-hats / G-buffer gathers, combine p-hats
+bash scripts/ab_libs_cfg.sh r4f/abu c5 "--rounds 3 --frames 3" u_no_vis u_no_zphat u_no_zload u_no_comb || exit 30
 timeout -k 10 60 scripts/probes/_bin/fetch_probe > $OUT/fetch_probe.jsonl 2>&1 || { cat $OUT/fetch_probe.jsonl; exit 24; }
 cat $OUT/fetch_probe.jsonl
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/probe_FETCH_SIZE -o run -- \

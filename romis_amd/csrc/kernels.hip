@@ -694,6 +694,9 @@ constexpr int kLtGeneral = 0, kLtPoint = 1, kLtGrid = 2, kLtPgram = 3, kLtRegula
 __host__ __device__ constexpr uint32_t lt_stride(int lt) {
     return lt == kLtGeneral ? 7u : lt == kLtPgram ? 4u : lt == kLtRegular ? 1u : 2u;
 }
+#ifndef ROMIS_RIS_PF
+#define ROMIS_RIS_PF 0   // build variant: software-pipelined colour loads for kLtRegular (ris_pixel)
+#endif
 template <int NT, int LT = kLtGeneral>
 __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                           const float4* lights, const Bvh& bvh, float4 nt, float4 pm, uint32_t x,
@@ -746,6 +749,16 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 asm volatile("" : "+s"(sh));
                 return xyz(sh[r]);
             };
+            // kLtRegular: candidate c drew light i, whose colour is gc
+            auto sample_reg = [&](uint32_t c, uint32_t i, v3 gc, v3& pos, v3& col) {
+                const float xl = (float)(i >> s.grid_ny_log2), yl = (float)(i & ((1u << s.grid_ny_log2) - 1u));
+                const v3 v0 = vadd(vadd(xyz(s.grid_start), vscale(xyz(s.grid_s01), xl)), vscale(xyz(s.grid_s02), yl));
+                float a = rand01(draw(ps, 4u * c + 1u));
+                float b = rand01(draw(ps, 4u * c + 2u));
+                pos = vadd(vadd(v0, vscale(shared_row(1), a)), vscale(shared_row(2), b));
+                const v3 m = vmix(gc, gc, a);
+                col = vmix(m, m, b);
+            };
             auto sample = [&](uint32_t c, v3& pos, v3& col) {
                 const float4* lt = record(c);
                 if (LT == kLtPoint) {
@@ -759,14 +772,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                     col = vmix(m, m, b);
                 } else if (LT == kLtRegular) {   // the corner of light i by arithmetic (scene.cpp:14-15)
                     const uint32_t i = uniform_index(draw(ps, 4u * c), L);
-                    const float xl = (float)(i >> s.grid_ny_log2), yl = (float)(i & ((1u << s.grid_ny_log2) - 1u));
-                    const v3 v0 = vadd(vadd(xyz(s.grid_start), vscale(xyz(s.grid_s01), xl)), vscale(xyz(s.grid_s02), yl));
-                    float a = rand01(draw(ps, 4u * c + 1u));
-                    float b = rand01(draw(ps, 4u * c + 2u));
-                    pos = vadd(vadd(v0, vscale(shared_row(1), a)), vscale(shared_row(2), b));
-                    const v3 gc = xyz(lights[i]);
-                    const v3 m = vmix(gc, gc, a);
-                    col = vmix(m, m, b);
+                    sample_reg(c, i, xyz(lights[i]), pos, col);
                 } else if (LT == kLtPgram) {
                     float a = rand01(draw(ps, 4u * c + 1u));
                     float b = rand01(draw(ps, 4u * c + 2u));
@@ -784,9 +790,22 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 // sample: the sample is a function of the candidate's draws (slots 4c .. 4c + 2), so it is drawn
                 // again once after the loop -- two selects per candidate instead of nine
                 uint32_t best = 0xFFFFFFFFu;
+                // ROMIS_RIS_PF (kLtRegular from global memory): candidate c + 1's colour is loaded while candidate c's
+                // target pdf runs (the same load, issued one iteration early)
+                constexpr bool kPf = ROMIS_RIS_PF && LT == kLtRegular;
+                uint32_t inext = 0u;
+                v3 gnext = mk(0.0f, 0.0f, 0.0f);
+                if (kPf && c_end) { inext = uniform_index(draw(ps, 0u), L); gnext = xyz(lights[inext]); }
                 for (uint32_t c = 0; c < c_end; c++) {
                     v3 pos, col;
-                    sample(c, pos, col);
+                    if (kPf) {
+                        const uint32_t ic = inext;
+                        const v3 gc = gnext;
+                        if (c + 1u < c_end) { inext = uniform_index(draw(ps, 4u * (c + 1u)), L); gnext = xyz(lights[inext]); }
+                        sample_reg(c, ic, gc, pos, col);
+                    } else {
+                        sample(c, pos, col);
+                    }
                     const float pd = target_pdf(s, f, px, pos, col, tb);
                     const float w = weight(pd);
                     r[0].M += 1u;

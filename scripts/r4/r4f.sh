@@ -37,7 +37,7 @@ for c in c4 c5 c2; do
     cat $OUT/late_$c.json
 done
 # RIS ablations at C5 / C4 (scripts/budget_variants.py): the colour gather of kLtRegular, the candidate loop
-bash scripts/ab_libs_cfg.sh r4f/ab c5 "--rounds 3 --frames 3" ris_reg_noload ris_no_cand || exit 28
+bash scripts/ab_libs_cfg.sh r4f/ab c5 "--rounds 3 --frames 3" ris_reg_noload ris_no_cand ris_pf || exit 28
 bash scripts/ab_libs_cfg.sh r4f/ab c4 "--rounds 3 --frames 8" ris_reg_noload ris_no_cand || exit 29
 # C5's unbiased + visibility pass: Z-loop rays / sign-only p-hats / G-buffer gathers, combine p-hats
 bash scripts/ab_libs_cfg.sh r4f/abu c5 "--rounds 3 --frames 3" u_no_vis u_no_zphat u_no_zload u_no_comb || exit 30

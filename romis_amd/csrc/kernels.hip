@@ -886,13 +886,15 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
                                                  const FeaturesDev& f, uint32_t key, float4* __restrict__ n_t,
                                                  float4* __restrict__ p_mat, float4* __restrict__ n_t2,
                                                  float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
-                                                 float* __restrict__ rp, uint32_t late_ok) {
+                                                 float* __restrict__ rp, uint32_t late_ok, uint8_t* __restrict__ tmiss) {
     const uint32_t bvh_f4 = 2u * s.num_nodes + 3u * s.num_tris;
     const float4* lights = global_lights<LT>(s);
     const uint32_t items = work_items(rg);
     // One tile per block: the light table is staged after the primary rays, and only if one of the tile's pixels will
-    // run the candidate loop (ris_pixel's miss test) -- at C4 / C5 87 % of the tiles see only background.
-    const bool late = LDS_LIGHTS && late_ok && gridDim.x >= items;
+    // run the candidate loop (ris_pixel's miss test) -- at C4 / C5 87 % of the tiles see only background.  The same
+    // vote is the tile's MissTiles flag (tmiss, one byte per tile; the launcher passes it only for one tile per block).
+    const bool one = gridDim.x >= items;
+    const bool late = LDS_LIGHTS && late_ok && one;
     if (LDS_LIGHTS) {
         if (!late) stage_lights<LT>(s, g_lds + bvh_f4);
         lights = g_lds + bvh_f4;
@@ -900,7 +902,7 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
     const Bvh bvh = stage_bvh(s, g_lds);   // ends with the barrier that also covers the light copy
     const GlTabs tb = gl_stage_tables();
     const v3 origin = mk(cam.origin[0], cam.origin[1], cam.origin[2]);
-    if (late) {
+    if (late || (one && tmiss)) {
         if (blockIdx.x >= items) return;   // block-uniform
         uint32_t x, y;
         size_t p;
@@ -911,7 +913,10 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         if (m >= s.num_materials) m = s.num_materials - 1u;
         const bool loop = live && s.num_lights != 0u &&
                           !(m == s.num_materials - 1u && s.lights_finite && !__builtin_isnan(pm.x + pm.y + pm.z));
-        if (__syncthreads_or(loop)) {
+        const bool any = __syncthreads_or(loop);
+        // flag 0: every live pixel is a miss with the known RIS result (lights present: no loop means a known miss)
+        if (tmiss && threadIdx.x == 0) tmiss[blockIdx.x] = (s.num_lights == 0u || any) ? 1u : 0u;
+        if (late && any) {
             stage_lights<LT>(s, g_lds + bvh_f4);
             __syncthreads();
         }
@@ -974,8 +979,8 @@ ROMIS_RIS_KERNEL_LT(2, false, kLtPgram, k_ris_n2_pg, ROMIS_RIS_ATTR)
     extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, CameraDev cam, FeaturesDev f,   \
                                                           uint32_t key, float4* n_t, float4* p_mat, float4* n_t2,      \
                                                           float4* ra, float4* rb, float2* rdbg, float* rp,             \
-                                                          uint32_t late_ok) {                                          \
-        primary_ris_body<NT, LDS, LT>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp, late_ok);                 \
+                                                          uint32_t late_ok, uint8_t* tmiss) {                          \
+        primary_ris_body<NT, LDS, LT>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp, late_ok, tmiss);          \
     }
 #define ROMIS_PRIMARY_RIS_KERNEL(NT, LDS, NAME, ATTR) ROMIS_PRIMARY_RIS_KERNEL_LT(NT, LDS, kLtGeneral, NAME, ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(1, true, k_primary_ris_n1_lds, ROMIS_RIS1_ATTR)
@@ -1440,6 +1445,19 @@ inline uint32_t xcd_grid(const Region& rg, uint32_t ntx, uint32_t nty) {
     return 8u * ((chunks + 7u) / 8u) * rg.xcd_rows * cw;
 }
 
+// MissTiles (restir_types.h): every RIS tile (32 x 8, numbered row-major over the view) meeting the pixel rect
+// [x0, x1] x [y0, y1] (global coordinates inside the view) is a background tile.  Block-uniform; the flags of the
+// rect's tile rows are OR-ed without early exits so their loads issue together.
+__device__ __forceinline__ bool tiles_known_miss(const MissTiles& mt, const Region& rg, int x0, int x1, int y0, int y1) {
+    const uint32_t ntxv = (rg.vw + kTileW - 1u) / kTileW;
+    const uint32_t cx0 = (uint32_t)(x0 - (int)rg.vx0) / kTileW, cx1 = (uint32_t)(x1 - (int)rg.vx0) / kTileW;
+    const uint32_t cy0 = (uint32_t)(y0 - (int)rg.vy0) / kTileH, cy1 = (uint32_t)(y1 - (int)rg.vy0) / kTileH;
+    uint32_t any = 0u;
+    for (uint32_t cy = cy0; cy <= cy1; cy++)
+        for (uint32_t cx = cx0; cx <= cx1; cx++) any |= mt.flags[cy * ntxv + cx];
+    return any == 0u;
+}
+
 template <bool DBG>
 __device__ __forceinline__ void spatial1_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
                                               v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
@@ -1503,7 +1521,8 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
                                                   const float4* __restrict__ p_mat, const float4* __restrict__ ia,
                                                   const float4* __restrict__ ib, float4* __restrict__ oa,
                                                   float4* __restrict__ ob, float2* __restrict__ odbg,
-                                                  const float* __restrict__ rp_in, float* __restrict__ rp_out) {
+                                                  const float* __restrict__ rp_in, float* __restrict__ rp_out,
+                                                  MissTiles mt) {
     const GlTabs tb = gl_stage_tables<false>();   // made visible by the window's barrier below
     float4* const l_nt = g_lds;
     uint32_t tile;
@@ -1511,6 +1530,23 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
     if (!xcd_tile(rg, ntx * ((rg.rh + kTH - 1) / kTH), blockIdx.x, tile)) return;   // block-uniform
     const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTH);
+    if (mt.m) {
+        // a tile of background pixels holding (0, W = 0), (0, M = mt.m): the miss shortcut's result below (W = 0, M the
+        // pixel's own, wSum FLT_MIN), written without reading the tile, its window or its neighbours
+        const int x1 = min(tx0 + (int)kTileW, (int)(rg.rx0 + rg.rw)) - 1, y1 = min(ty0 + (int)kTH, (int)(rg.ry0 + rg.rh)) - 1;
+        if (tiles_known_miss(mt, rg, tx0, x1, ty0, y1)) {
+            const uint32_t mw = threadIdx.x >> 6, ml = threadIdx.x & 63u;
+            const int mx = tx0 + (int)((mw & 3u) * 8u + (ml & 7u)), my = ty0 + (int)((mw >> 2) * 8u + (ml >> 3));
+            if (mx <= x1 && my <= y1) {
+                const uint32_t mo = ((uint32_t)(my - (int)rg.vy0) * rg.vw + (uint32_t)(mx - (int)rg.vx0)) << 4;
+                st_at(oa, mo, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+                st_at(ob, mo, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(mt.m)));
+                if (DBG) st_at(odbg, mo >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
+                if (rp_out) st_at(rp_out, mo >> 2, 0.0f);
+            }
+            return;   // block-uniform, before the window's barrier
+        }
+    }
     // neighbour clamp bounds (render_utils.cpp:109-110: the image; here also the stored view), global coords
     const int xlo = max(0, (int)rg.vx0), xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1;
     const int ylo = max(0, (int)rg.vy0), yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1;
@@ -1617,8 +1653,8 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL1_NTL_WPE))) void     \
     NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
          const float4* p_mat, const float4* ia, const float4* ib, float4* oa, float4* ob, float2* odbg,               \
-         const float* rp_in, float* rp_out) {                                                                         \
-        spatial1_ntl_body<DBG>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);       \
+         const float* rp_in, float* rp_out, MissTiles mt) {                                                           \
+        spatial1_ntl_body<DBG>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out, mt);   \
     }
 ROMIS_SPATIAL1_NTL_KERNEL(false, k_spatial1_ntl)
 ROMIS_SPATIAL1_NTL_KERNEL(true, k_spatial1_ntl_dbg)
@@ -1633,8 +1669,8 @@ ROMIS_SPATIAL1_NTL_KERNEL(true, k_spatial1_ntl_dbg)
     extern "C" __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL1_T2_WPE))) void     \
     NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
          const float4* p_mat, const float4* ia, const float4* ib, float4* oa, float4* ob, float2* odbg,               \
-         const float* rp_in, float* rp_out) {                                                                         \
-        spatial1_ntl_body<DBG, 2>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);    \
+         const float* rp_in, float* rp_out, MissTiles mt) {                                                           \
+        spatial1_ntl_body<DBG, 2>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out, mt);\
     }
 ROMIS_SPATIAL1_T2_KERNEL(false, k_spatial1_ntl_t2)
 ROMIS_SPATIAL1_T2_KERNEL(true, k_spatial1_ntl_t2_dbg)
@@ -1846,17 +1882,36 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
                                                const float4* __restrict__ ia, const float4* __restrict__ ib,
                                                float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
                                                const float* __restrict__ rp_in, const float* __restrict__ rp_nb,
-                                               float* __restrict__ rp_out, uint8_t* __restrict__ vis_out) {
-    const Bvh bvh = VIS ? stage_bvh(s, g_lds) : global_bvh(s);   // ends with a barrier (every thread gets here)
-    const GlTabs tb = gl_stage_tables();
+                                               float* __restrict__ rp_out, uint8_t* __restrict__ vis_out, MissTiles mt) {
     uint32_t tile;
-    if (!xcd_tile(rg, num_tiles(rg), blockIdx.x, tile)) return;   // block-uniform; no barrier follows
+    if (!xcd_tile(rg, num_tiles(rg), blockIdx.x, tile)) return;   // block-uniform, before any barrier
     const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
     const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTileH);
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
     const int x = tx0 + (int)(w * 8u + (l & 7u)), y = ty0 + (int)(l >> 3);
-    if (x >= (int)(rg.rx0 + rg.rw) || y >= (int)(rg.ry0 + rg.rh)) return;
     const uint32_t K = f.K;   // <= kLeanK (host check)
+    if (mt.m) {
+        // the tile and every pixel its neighbour draws can reach (grown by R, clamped to the image and the view) are
+        // background pixels holding (0, W = 0), (0, M = mt.m): the miss shortcut's result below with M = (K + 1) mt.m
+        const int x1 = min(tx0 + (int)kTileW, (int)(rg.rx0 + rg.rw)) - 1, y1 = min(ty0 + (int)kTileH, (int)(rg.ry0 + rg.rh)) - 1;
+        const int gx0 = max(max(tx0 - (int)f.R, 0), (int)rg.vx0), gy0 = max(max(ty0 - (int)f.R, 0), (int)rg.vy0);
+        const int gx1 = min(min(x1 + (int)f.R, (int)rg.W - 1), (int)(rg.vx0 + rg.vw) - 1);
+        const int gy1 = min(min(y1 + (int)f.R, (int)rg.H - 1), (int)(rg.vy0 + rg.vh) - 1);
+        if (tiles_known_miss(mt, rg, gx0, gx1, gy0, gy1)) {
+            if (x <= x1 && y <= y1) {
+                const uint32_t mo = ((uint32_t)(y - (int)rg.vy0) * rg.vw + (uint32_t)(x - (int)rg.vx0)) << 4;
+                st_at(oa, mo, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+                st_at(ob, mo, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((K + 1u) * mt.m)));
+                if (DBG) st_at(odbg, mo >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
+                if (rp_out) st_at(rp_out, mo >> 2, 0.0f);
+                if (vis_out) vis_out[mo >> 4] = 0u;
+            }
+            return;   // block-uniform, before the BVH's barrier
+        }
+    }
+    const Bvh bvh = VIS ? stage_bvh(s, g_lds) : global_bvh(s);   // ends with a barrier (every thread gets here)
+    const GlTabs tb = gl_stage_tables();
+    if (x >= (int)(rg.rx0 + rg.rw) || y >= (int)(rg.ry0 + rg.rh)) return;
     const int rx = x - (int)rg.vx0, ry = y - (int)rg.vy0;
     const uint32_t pofs = ((uint32_t)ry * rg.vw + (uint32_t)rx) << 4;
     const float4 cn = ld_at(n_t, pofs), cpm = ld_at(p_mat, pofs);
@@ -1966,9 +2021,10 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
                                                                            const float4* ia, const float4* ib,          \
                                                                            float4* oa, float4* ob, float2* odbg,        \
                                                                            const float* rp_in, const float* rp_nb,      \
-                                                                           float* rp_out, uint8_t* vis_out) {           \
+                                                                           float* rp_out, uint8_t* vis_out,             \
+                                                                           MissTiles mt) {                              \
         spatial1u_body<DBG, VIS>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_nb, rp_out, \
-                                 vis_out);                                                                            \
+                                 vis_out, mt);                                                                        \
     }
 ROMIS_SPATIAL1U_KERNEL(false, false, k_spatial1u)
 ROMIS_SPATIAL1U_KERNEL(true, false, k_spatial1u_dbg)
@@ -2036,20 +2092,49 @@ __device__ __forceinline__ uint32_t target_bin(const Bvh& b, v3 y) {
            ((qz & 1u) << 2) | ((qx & 1u) << 1) | (qy & 1u);
 }
 
+// exposureToneMapping (tone_mapping.cpp:8-11) of a finalShading colour; gamma = 1 (the Features default) skips the power
+// (pm_powf(x, 1) == x for every x)
+__device__ __forceinline__ v3 tone_map_rgb(const FeaturesDev& f, v3 color, const GlTabs& tb) {
+    if (!f.tone_map) return color;
+    const float g = 1.0f / f.gamma;
+    v3 e = vscale(mk(-color.x, -color.y, -color.z), f.exposure);
+    v3 mapped = mk(1.0f - gl_expf(tb, e.x), 1.0f - gl_expf(tb, e.y), 1.0f - gl_expf(tb, e.z));
+    return g == 1.0f ? mapped : mk(gl_powf(tb, mapped.x, g), gl_powf(tb, mapped.y, g), gl_powf(tb, mapped.z, g));
+}
+
 template <bool LDS_BVH, int NT>
 __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, v3 origin,
                                                   const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                                   const float4* __restrict__ ra, const float4* __restrict__ rb,
-                                                  float* __restrict__ rgb, const uint8_t* __restrict__ vis_in) {
+                                                  float* __restrict__ rgb, const uint8_t* __restrict__ vis_in,
+                                                  MissTiles mt) {
     // NT shadow rays per pixel (one per sub-reservoir): ray j * 256 + t is pixel t's sub-reservoir j
     constexpr uint32_t kRays = 256u * NT;
+    if (NT == 1 && mt.flags) {
+        // a tile of background pixels (MissTiles): after RIS and any biased / unbiased passes each holds W = 0 and the
+        // initial (0, 0) sample, which a miss pixel shades to +-0 (kd = ks = 0; a non-finite dotNL or power is cleaned
+        // up; the distance |P| is not NaN): the colour is +0 -- tone mapped as below, without reading anything
+        const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
+        const int tx0 = (int)(rg.rx0 + (blockIdx.x % ntx) * kTileW), ty0 = (int)(rg.ry0 + (blockIdx.x / ntx) * kTileH);
+        const int x1 = min(tx0 + (int)kTileW, (int)(rg.rx0 + rg.rw)) - 1, y1 = min(ty0 + (int)kTileH, (int)(rg.ry0 + rg.rh)) - 1;
+        if (tiles_known_miss(mt, rg, tx0, x1, ty0, y1)) {
+            uint32_t x, y;
+            size_t p;
+            if (work_pixel(rg, blockIdx.x, x, y, p)) {
+                const v3 color = tone_map_rgb(f, vdivs(mk(0.0f, 0.0f, 0.0f), (float)NT), gl_global_tabs());
+                const uint32_t row = rg.rh - 1u - (y - rg.ry0);
+                float* o = rgb + 3 * ((size_t)row * rg.rw + (x - rg.rx0));
+                o[0] = color.x; o[1] = color.y; o[2] = color.z;
+            }
+            return;   // block-uniform, before the BVH's barrier
+        }
+    }
     __shared__ uint32_t s_hist[256];
     __shared__ uint32_t s_wsum[4];
     __shared__ float4 s_from[kRays], s_to[kRays];
     __shared__ uint32_t s_vis[kRays];
     const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
     const GlTabs tb = gl_stage_tables();
-    const float g = 1.0f / f.gamma;
     const uint32_t t = threadIdx.x;
     uint32_t x, y;
     size_t p;
@@ -2150,12 +2235,7 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
         if (j == 0 && known == 2u) c = mk(0.0f, 0.0f, 0.0f);   // the spatial pass's ray was occluded
         color = vadd(color, vscale(c, r[j].W));
     }
-    color = vdivs(color, (float)NT);
-    if (f.tone_map) {
-        v3 e = vscale(mk(-color.x, -color.y, -color.z), f.exposure);
-        v3 mapped = mk(1.0f - gl_expf(tb, e.x), 1.0f - gl_expf(tb, e.y), 1.0f - gl_expf(tb, e.z));
-        color = g == 1.0f ? mapped : mk(gl_powf(tb, mapped.x, g), gl_powf(tb, mapped.y, g), gl_powf(tb, mapped.z, g));
-    }
+    color = tone_map_rgb(f, vdivs(color, (float)NT), tb);
     const uint32_t row = rg.rh - 1u - (y - rg.ry0);
     float* o = rgb + 3 * ((size_t)row * rg.rw + (x - rg.rx0));
     o[0] = color.x; o[1] = color.y; o[2] = color.z;
@@ -2164,13 +2244,13 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
 extern "C" __global__ __launch_bounds__(256) void k_final_n1_sorted(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,
                                                                    float oz, const float4* n_t, const float4* p_mat,
                                                                    const float4* ra, const float4* rb, float* rgb,
-                                                                   const uint8_t* vis_in) {
-    final_sorted_body<true, 1>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, vis_in);
+                                                                   const uint8_t* vis_in, MissTiles mt) {
+    final_sorted_body<true, 1>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, vis_in, mt);
 }
 extern "C" __global__ __launch_bounds__(256) void k_final_n2_sorted(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,
                                                                    float oz, const float4* n_t, const float4* p_mat,
                                                                    const float4* ra, const float4* rb, float* rgb) {
-    final_sorted_body<true, 2>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, nullptr);
+    final_sorted_body<true, 2>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, nullptr, MissTiles{nullptr, 0u});
 }
 
 #define ROMIS_FINAL_KERNEL(NT, LDS, NAME)                                                                              \
@@ -3031,9 +3111,11 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f
 
 hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const CameraDev& cam, const FeaturesDev& f, uint32_t key,
                               float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,
-                              float* rp, const Tuning& tu, hipStream_t stream) {
+                              float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, tu.primary_2d);
+    // MissTiles flags: one 32 x 8 tile per block, N = 1 (the caller allocates one byte per tile)
+    if (!rg.map2d || tu.ris_blocks || f.N != 1) tmiss = nullptr;
     const size_t bvh = bvh_lds_bytes(s);
     if (bvh > kLdsBudget) return hipErrorInvalidValue;   // caller checks primary_ris_fits()
     const int lt = ris_light_form(s, f, tu);
@@ -3049,7 +3131,7 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
            : use_lights ? (f.N == 1 ? k_primary_ris_n1_lds : (f.N == 2 ? k_primary_ris_n2_lds : k_primary_ris_n0_lds))
                         : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
     ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.ris_blocks), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
-                 cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr, tu.ris_late);
+                 cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr, tu.ris_late, tmiss);
     return hipGetLastError();
 }
 
@@ -3071,8 +3153,10 @@ hipError_t launch_temporal(const SceneDev& s, const Region& rg0, const FeaturesD
 hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
                           const float4* n_t, const float4* p_mat, const float4* ia, const float4* ib, float4* oa,
                           float4* ob, float2* odbg, const float* rp_in, const float* rp_nb, float* rp_out,
-                          bool* rp_written, const Tuning& tu, hipStream_t stream, uint8_t* vis_out, bool* vis_written) {
+                          bool* rp_written, const Tuning& tu, hipStream_t stream, uint8_t* vis_out, bool* vis_written,
+                          MissTiles mt) {
     if (rp_written) *rp_written = false;
+    if (!mt.flags) mt.m = 0u;
     if (vis_written) *vis_written = false;
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     Region rg = with_map(rg0, tu.spatial_xcd);   // XCD-banded order works on 2D tiles
@@ -3094,7 +3178,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         auto k = f.spatial_vis ? (odbg ? k_spatial1u_vis_dbg : k_spatial1u_vis) : (odbg ? k_spatial1u_dbg : k_spatial1u);
         uint8_t* vo = f.spatial_vis ? vis_out : nullptr;   // the own-pixel shadow ray, for final shading (N = 1)
         ROMIS_LAUNCH(k, dim3(grid), dim3(kBlock), f.spatial_vis ? bvh_bytes : 0, stream, s, rg, f, key, o[0], o[1], o[2],
-                     n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_in ? rp_nb : nullptr, rp_out, vo);
+                     n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_in ? rp_nb : nullptr, rp_out, vo, mt);
         if (rp_written) *rp_written = rp_out != nullptr;
         if (vis_written) *vis_written = vo != nullptr;
         return hipGetLastError();
@@ -3138,14 +3222,14 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
             }
             ROMIS_LAUNCH(odbg ? k_spatial1_ntl_t2_dbg : k_spatial1_ntl_t2, dim3(grid), dim3(2u * kBlock),
                          apron_max(2) * 16u, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg,
-                         rp_in, rp_out);
+                         rp_in, rp_out, mt);
         } else if (tu.spatial_lds == 3u && f.R <= kLdsSpatialR) {
 #ifndef ROMIS_NTL_EXTRA_LDS
 #define ROMIS_NTL_EXTRA_LDS 0   // occupancy experiments (build variants): extra dynamic LDS per block
 #endif
             ROMIS_LAUNCH(odbg ? k_spatial1_ntl_dbg : k_spatial1_ntl, dim3(grid), dim3(kBlock),
                          kApronMax * 16u + ROMIS_NTL_EXTRA_LDS, stream,
-                         s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
+                         s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out, mt);
         } else {
             ROMIS_LAUNCH(odbg ? k_spatial1_dbg : k_spatial1, dim3(grid), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1],
                          o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
@@ -3164,7 +3248,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
 
 hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev& f, const float* o, const float4* n_t,
                         const float4* p_mat, const float4* ra, const float4* rb, float* rgb, const Tuning& tu,
-                        hipStream_t stream, const uint8_t* vis_in) {
+                        hipStream_t stream, const uint8_t* vis_in, MissTiles mt) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, tu.final_2d);
     const size_t lds = bvh_lds_bytes(s);
@@ -3176,7 +3260,7 @@ hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev&
         if (!tu.final_miss) sf.miss_shade_zero = 0u;   // final.miss = 0: no miss shortcut (A/B runs)
         if (f.N == 1)
             ROMIS_LAUNCH(k_final_n1_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, sf, rg, f, o[0], o[1], o[2], n_t,
-                         p_mat, ra, rb, rgb, vis_in);
+                         p_mat, ra, rb, rgb, vis_in, rg.map2d ? mt : MissTiles{nullptr, 0u});
         else
             ROMIS_LAUNCH(k_final_n2_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, sf, rg, f, o[0], o[1], o[2], n_t,
                          p_mat, ra, rb, rgb);

@@ -219,6 +219,7 @@ struct restir_ctx {
     std::shared_ptr<FramePool> pool = std::make_shared<FramePool>();
     DevBuf rp[2];                                   // their target-pdf cache planes (N = 1, planes layout)
     DevBuf vis;                                     // unbiased + visibility pass -> final shading: own-pixel ray
+    DevBuf tmiss;                                   // RIS -> spatial passes / final shading: background tiles (MissTiles)
     int cur = 0;
     uint32_t rgb_w = 0, rgb_h = 0;
     // Frames in flight (tuning frames.inflight = 2): restir_render alternates two frame slots -- slot 0 is the buffers
@@ -228,7 +229,7 @@ struct restir_ctx {
     // spatial pass never shares the GPU with another kernel (its timed duration stays the pass alone).
     struct Slot1 {
         hipStream_t stream = nullptr;
-        DevBuf n_t, p_mat, rec[2], rp[2], rgb, uv, vis;
+        DevBuf n_t, p_mat, rec[2], rp[2], rgb, uv, vis, tmiss;
     } slot1;
     struct {
         hipEvent_t after_spatial[2] = {nullptr, nullptr}, after_final[2] = {nullptr, nullptr}, joined = nullptr;
@@ -716,6 +717,7 @@ struct FrameBufs {
     DevBuf& rgb() const { return slot ? c->slot1.rgb : c->rgb; }
     DevBuf& uv() const { return slot ? c->slot1.uv : c->uv; }
     DevBuf& vis() const { return slot ? c->slot1.vis : c->vis; }
+    DevBuf& tmiss() const { return slot ? c->slot1.tmiss : c->tmiss; }
     float4* nt(int i) const { return records ? rec_()[i].as<float4>() : n_t_().as<float4>(); }
     float4* ra(int i) const { return rec_()[i].as<float4>() + (records ? 1 : 0); }
     float4* rb(int i) const { return rec_()[i].as<float4>() + (records ? 2 : npx * N); }
@@ -825,7 +827,8 @@ void restir_destroy(restir_ctx* c) {
         (void)hipStreamSynchronize(c->stream);
         if (c->slot1.stream) (void)hipStreamSynchronize(c->slot1.stream);
         for (DevBuf* b : {&c->slot1.n_t, &c->slot1.p_mat, &c->slot1.rec[0], &c->slot1.rec[1], &c->slot1.rp[0],
-                          &c->slot1.rp[1], &c->slot1.rgb, &c->slot1.uv, &c->slot1.vis, &c->vis})
+                          &c->slot1.rp[1], &c->slot1.rgb, &c->slot1.uv, &c->slot1.vis, &c->vis,
+                          &c->slot1.tmiss, &c->tmiss})
             b->release();
         for (hipEvent_t* e : {&c->pipe.after_spatial[0], &c->pipe.after_spatial[1], &c->pipe.after_final[0],
                               &c->pipe.after_final[1], &c->pipe.joined})
@@ -1335,9 +1338,19 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     // frames in flight: this frame's primary rays and RIS start once the other slot's spatial passes are done
     if (wait_other) HIP_TRY(hipStreamWaitEvent(st, c->pipe.after_spatial[k ^ 1], 0));
     const uint32_t ris_key = restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, 0);
-    if (c->tuning.fuse_primary_ris && primary_ris_fits(s)) {   // same region: one kernel (kernels.hip k_primary_ris)
+    // background tiles (MissTiles): N = 1, no temporal reuse (its output is not the RIS result), the fused kernel with
+    // one 32 x 8 tile per block; the spatial shortcuts also need bounded normals (their miss tests)
+    uint8_t* tmiss = nullptr;
+    const bool fused = c->tuning.fuse_primary_ris && primary_ris_fits(s);
+    if (c->tuning.miss_tiles && fused && N == 1 && !temporal && c->tuning.primary_2d && !c->tuning.ris_blocks &&
+        s.normals_bounded && !fb.records) {
+        const size_t tiles = (size_t)((t.gwidth + 31u) / 32u) * ((t.gheight + 7u) / 8u);
+        ST_TRY(fb.tmiss().ensure(tiles));
+        tmiss = fb.tmiss().as<uint8_t>();
+    }
+    if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)
         TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),
-                                                          fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st));
+                                                          fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st, tmiss));
     } else {
         TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, fb.nt(0), pm, fb.nt2(), c->tuning, st));
         TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, ris_key, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), nullptr,
@@ -1373,12 +1386,15 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                              // the last pass's pdf cache has no reader (final shading re-shades; the next frame's
                              // temporal pass evaluates its own): not written
                              pass + 1 < passes ? fb.rp(nxt) : nullptr, &rp_ok, c->tuning, st,
-                             pass + 1 == passes ? vis : nullptr, &vis_ok));
+                             pass + 1 == passes ? vis : nullptr, &vis_ok,
+                             // a background pixel holds M = f.M after RIS and after every biased pass; an unbiased pass
+                             // sums its neighbours' M, which only pass 0 knows
+                             MissTiles{tmiss, (!f.unbiased || pass == 0) ? f.M : 0u}));
         cur = nxt;
     }
     if (pipe) HIP_TRY(hipEventRecord(c->pipe.after_spatial[k], st));
     TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), fb.rgb().as<float>(),
-                                          c->tuning, st, vis_ok ? vis : nullptr));
+                                          c->tuning, st, vis_ok ? vis : nullptr, MissTiles{tmiss, 0u}));
     if (pipe) {
         HIP_TRY(hipEventRecord(c->pipe.after_final[k], st));
         c->pipe.has[k] = true;
@@ -2325,6 +2341,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.xcd_rows")) t.spatial_xcd_rows = v;
     else if (!std::strcmp(key, "spatial.xcd_cols")) t.spatial_xcd_cols = v;
     else if (!std::strcmp(key, "ris.late")) t.ris_late = v;
+    else if (!std::strcmp(key, "miss.tiles")) t.miss_tiles = v;
     else if (!std::strcmp(key, "final.miss")) t.final_miss = v;
     else if (!std::strcmp(key, "spatial.lds")) {
         if (v != 0u && v != 3u)

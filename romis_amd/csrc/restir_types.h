@@ -99,6 +99,16 @@ struct Region {
     uint32_t xcd_cols;   // chunk width in tiles (xcd_tile); 0 = the whole row of tiles
 };
 
+// Background tiles (restir_render, N = 1, no temporal reuse): the fused primary + RIS kernel writes one byte per
+// 32 x 8 tile of its region (the view), 0 when every pixel of the tile is a primary-ray miss whose RIS reservoir is
+// known -- the miss material, P not NaN, finite lights, L != 0: (0, 0, 0, W = 0), (0, 0, 0, M = f.M), pdf 0 -- and
+// 1 otherwise.  The spatial passes and final shading then write such tiles' known results without reading them.
+// m: the M every such pixel holds at the pass's input (0: flags unused by this launch).
+struct MissTiles {
+    const uint8_t* flags;
+    uint32_t m;
+};
+
 // Launch-shape knobs (restir_set_tuning); they never change results, only speed.
 constexpr uint32_t kXcdRowsAuto = 255u;
 struct Tuning {
@@ -110,6 +120,8 @@ struct Tuning {
     uint32_t ris_queue = 0;        // persistent blocks (this many) pulling tiles from a WorkQueue; 0 = off
     uint32_t ris_compact = 1;      // N <= 2: compact light tables for point-light-only scenes and light grids (_pt /
                                    // _grid RIS kernels, kernels.hip ris_light_form)
+    uint32_t miss_tiles = 1;       // restir_render: background-tile flags (MissTiles) from RIS to the spatial passes
+                                   // and final shading
     uint32_t ris_late = 1;         // fused primary + RIS, one tile per block: stage the light table only for tiles with
                                    // a pixel that runs the candidate loop (0: every tile, before the primary rays)
     uint32_t spatial_xcd = 1;      // XCD-banded tile order

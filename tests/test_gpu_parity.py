@@ -889,3 +889,38 @@ def test_frames_in_flight_match_serial_frames(gpu, oracle, temporal, passes, N):
         assert_bits(gpu.download(_abi.BUF_RES_A), a, "stage res_a after pipelined frames")
     finally:
         gpu.set_tuning("frames.inflight", 1)
+
+
+@pytest.mark.parametrize("name,passes,unbiased,vis,tiled", [
+    ("cornell_1024", 1, 0, 0, 0), ("cornell_1024", 2, 0, 0, 0), ("cornell_4096", 1, 1, 1, 0),
+    ("cornell_4096", 2, 1, 1, 0), ("cornell_4096", 1, 1, 0, 0), ("nightclub_128pt", 1, 0, 0, 0),
+    ("cornell_1024", 2, 0, 0, 1), ("cornell_4096", 2, 1, 1, 1)])
+def test_miss_tiles_match_full_reads(gpu, name, passes, unbiased, vis, tiled):
+    """MissTiles (miss.tiles = 1, the default): RIS flags the 32 x 8 tiles whose pixels all missed the scene, and the
+    spatial passes and final shading write those tiles' known results without reading them.  Frames at 640 x 360
+    (the Cornell box fills the middle: most tiles, and most unbiased neighbourhoods, are background), whole and as a
+    ghost-zoned screen tile (2 x 2 plan, rank 3: the RIS, spatial and final regions start at different offsets), must
+    equal the frames rendered with the flags off bit for bit -- RGB and the returned grid."""
+    from romis_amd import restir
+    w, h = 640, 360
+    s = get_scene(name)
+    gpu.set_scene(s)
+    cam = scene.camera_for(name, w, h)
+    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=passes, unbiased_combination=unbiased,
+                              temporal_reuse=0, spatial_reuse_visibility_check=vis)
+    tile = restir.tile_plan(w, h, 2, 2, 3, passes * f.spatial_resample_radius) if tiled else None
+
+    def run(on):
+        gpu.set_tuning("miss.tiles", on)
+        gpu.set_seed(SEED, 0)
+        rgb, grid = gpu.render_restir(None, cam, w, h, f, tile=tile)
+        return rgb, grid.download()
+
+    try:
+        off_rgb, off_grid = run(0)
+        on_rgb, on_grid = run(1)
+    finally:
+        gpu.set_tuning("miss.tiles", 1)
+    assert_bits(on_rgb, off_rgb, f"{name} rgb")
+    for a, b in zip(off_grid, on_grid):
+        assert np.array_equal(np.asarray(a).view(np.uint32), np.asarray(b).view(np.uint32)), f"{name} grid"

@@ -44,6 +44,9 @@ def main():
         name, _, knobs = v.partition(":")
         variants[name] = dict((k, int(x)) for k, x in (kv.split("=") for kv in knobs.split(",") if kv))
     keys = sorted({k for kn in variants.values() for k in kn})
+    missing = [k for k in keys if k not in DEFAULTS]
+    if missing:   # every knob a variant sets needs its library default (scripts/kbench.py DEFAULTS) for the others
+        raise SystemExit(f"cfg_kbench: no default for {missing} in scripts/kbench.py DEFAULTS")
     r = restir.Renderer(0)
     r.set_scene(scene.bench_scene(cf["scene"]))
     cam = scene.camera_for(cf["scene"], W, H)

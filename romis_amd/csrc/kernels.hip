@@ -886,7 +886,8 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
                                                  const FeaturesDev& f, uint32_t key, float4* __restrict__ n_t,
                                                  float4* __restrict__ p_mat, float4* __restrict__ n_t2,
                                                  float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
-                                                 float* __restrict__ rp, uint32_t late_ok, uint8_t* __restrict__ tmiss) {
+                                                 float* __restrict__ rp, uint32_t late_ok, uint8_t* __restrict__ tmiss,
+                                                 uint32_t skip_res) {
     const uint32_t bvh_f4 = 2u * s.num_nodes + 3u * s.num_tris;
     const float4* lights = global_lights<LT>(s);
     const uint32_t items = work_items(rg);
@@ -920,7 +921,10 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
             stage_lights<LT>(s, g_lds + bvh_f4);
             __syncthreads();
         }
-        if (live) ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb);
+        // skip_res (the launcher's promise that no reader needs them): a background tile's known reservoirs and pdfs
+        // are not stored -- the biased lean passes and final shading substitute them from the flag
+        if (live && (any || !tmiss || !skip_res))
+            ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb);
         return;
     }
     for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {
@@ -979,8 +983,8 @@ ROMIS_RIS_KERNEL_LT(2, false, kLtPgram, k_ris_n2_pg, ROMIS_RIS_ATTR)
     extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, CameraDev cam, FeaturesDev f,   \
                                                           uint32_t key, float4* n_t, float4* p_mat, float4* n_t2,      \
                                                           float4* ra, float4* rb, float2* rdbg, float* rp,             \
-                                                          uint32_t late_ok, uint8_t* tmiss) {                          \
-        primary_ris_body<NT, LDS, LT>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp, late_ok, tmiss);          \
+                                                          uint32_t late_ok, uint8_t* tmiss, uint32_t skip_res) {       \
+        primary_ris_body<NT, LDS, LT>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp, late_ok, tmiss, skip_res); \
     }
 #define ROMIS_PRIMARY_RIS_KERNEL(NT, LDS, NAME, ATTR) ROMIS_PRIMARY_RIS_KERNEL_LT(NT, LDS, kLtGeneral, NAME, ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(1, true, k_primary_ris_n1_lds, ROMIS_RIS1_ATTR)
@@ -1448,14 +1452,25 @@ inline uint32_t xcd_grid(const Region& rg, uint32_t ntx, uint32_t nty) {
 // MissTiles (restir_types.h): every RIS tile (32 x 8, numbered row-major over the view) meeting the pixel rect
 // [x0, x1] x [y0, y1] (global coordinates inside the view) is a background tile.  Block-uniform; the flags of the
 // rect's tile rows are OR-ed without early exits so their loads issue together.
-__device__ __forceinline__ bool tiles_known_miss(const MissTiles& mt, const Region& rg, int x0, int x1, int y0, int y1) {
+__device__ __forceinline__ bool tiles_known_miss(const MissTiles& mt, const Region& rg, int x0, int x1, int y0, int y1,
+                                                 bool* some_known = nullptr) {
     const uint32_t ntxv = (rg.vw + kTileW - 1u) / kTileW;
     const uint32_t cx0 = (uint32_t)(x0 - (int)rg.vx0) / kTileW, cx1 = (uint32_t)(x1 - (int)rg.vx0) / kTileW;
     const uint32_t cy0 = (uint32_t)(y0 - (int)rg.vy0) / kTileH, cy1 = (uint32_t)(y1 - (int)rg.vy0) / kTileH;
-    uint32_t any = 0u;
+    uint32_t any = 0u, all = 1u;
     for (uint32_t cy = cy0; cy <= cy1; cy++)
-        for (uint32_t cx = cx0; cx <= cx1; cx++) any |= mt.flags[cy * ntxv + cx];
+        for (uint32_t cx = cx0; cx <= cx1; cx++) {
+            const uint32_t v = mt.flags[cy * ntxv + cx];
+            any |= v;
+            all &= v;
+        }
+    if (some_known) *some_known = all == 0u;   // some tile of the rect is a background tile
     return any == 0u;
+}
+// the flag of the RIS tile holding view pixel (x, y) (global coordinates)
+__device__ __forceinline__ uint32_t tile_flag_at(const MissTiles& mt, const Region& rg, int x, int y) {
+    const uint32_t ntxv = (rg.vw + kTileW - 1u) / kTileW;
+    return mt.flags[((uint32_t)(y - (int)rg.vy0) / kTileH) * ntxv + (uint32_t)(x - (int)rg.vx0) / kTileW];
 }
 
 template <bool DBG>
@@ -1530,11 +1545,12 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
     if (!xcd_tile(rg, ntx * ((rg.rh + kTH - 1) / kTH), blockIdx.x, tile)) return;   // block-uniform
     const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTH);
+    bool mixed = false;   // some of the tile's pixels lie in background tiles (whose RIS reservoirs may be unwritten)
     if (mt.m) {
         // a tile of background pixels holding (0, W = 0), (0, M = mt.m): the miss shortcut's result below (W = 0, M the
         // pixel's own, wSum FLT_MIN), written without reading the tile, its window or its neighbours
         const int x1 = min(tx0 + (int)kTileW, (int)(rg.rx0 + rg.rw)) - 1, y1 = min(ty0 + (int)kTH, (int)(rg.ry0 + rg.rh)) - 1;
-        if (tiles_known_miss(mt, rg, tx0, x1, ty0, y1)) {
+        if (tiles_known_miss(mt, rg, tx0, x1, ty0, y1, &mixed)) {
             const uint32_t mw = threadIdx.x >> 6, ml = threadIdx.x & 63u;
             const int mx = tx0 + (int)((mw & 3u) * 8u + (ml & 7u)), my = ty0 + (int)((mw >> 2) * 8u + (ml >> 3));
             if (mx <= x1 && my <= y1) {
@@ -1563,9 +1579,15 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     float pd_cached = 0.0f;
     if (live) {
         cpm = ld_at(p_mat, pofs);
-        ca = ld_at(ia, pofs);
-        cb = ld_at(ib, pofs);
-        if (rp_in) pd_cached = ld_at(rp_in, pofs >> 2);
+        // a pixel of a background tile holds the known (0, W = 0), (0, M = mt.m) and pdf 0: RIS may not have stored
+        // them (its skip_res), so they are not read (a block-uniform branch: only tiles that straddle RIS tiles)
+        if (mixed && tile_flag_at(mt, rg, x, y) == 0u) {
+            cb.w = __uint_as_float(mt.m);
+        } else {
+            ca = ld_at(ia, pofs);
+            cb = ld_at(ib, pofs);
+            if (rp_in) pd_cached = ld_at(rp_in, pofs >> 2);
+        }
     }
     ntl_stage_window<TH>(rg, n_t, l_nt, ax0, ay0, AW, n_apron);
     // neighbour draws while the loads are in flight
@@ -3111,7 +3133,7 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f
 
 hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const CameraDev& cam, const FeaturesDev& f, uint32_t key,
                               float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,
-                              float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss) {
+                              float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss, bool skip_res) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, tu.primary_2d);
     // MissTiles flags: one 32 x 8 tile per block, N = 1 (the caller allocates one byte per tile)
@@ -3131,11 +3153,19 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
            : use_lights ? (f.N == 1 ? k_primary_ris_n1_lds : (f.N == 2 ? k_primary_ris_n2_lds : k_primary_ris_n0_lds))
                         : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
     ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.ris_blocks), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
-                 cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr, tu.ris_late, tmiss);
+                 cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr, tu.ris_late, tmiss,
+                 (tmiss && skip_res) ? 1u : 0u);
     return hipGetLastError();
 }
 
 bool primary_ris_fits(const SceneDev& s) { return bvh_lds_bytes(s) <= kLdsBudget; }
+
+// launch_spatial's N = 1 biased pass reads background tiles through MissTiles (k_spatial1_ntl / _t2) for these
+// features and knobs, SoA planes -- the condition for RIS's skip_res
+bool spatial_biased_reads_flags(const FeaturesDev& f, const Tuning& tu) {
+    return !f.unbiased && f.N == 1 && f.K <= kLeanK && f.R <= kLdsSpatialR && tu.spatial_lean && tu.spatial_lds == 3u &&
+           tu.spatial_xcd && tu.spatial_wave8;
+}
 
 hipError_t launch_temporal(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
                            const float4* n_t, const float4* p_mat, const float4* ca, const float4* cb,

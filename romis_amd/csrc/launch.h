@@ -17,8 +17,11 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg, const FeaturesDev& f,
 // genPrimaryRayHits + genCanonicalSamples in one kernel over the same region (needs the BVH to fit in LDS)
 hipError_t launch_primary_ris(const SceneDev& s, const Region& rg, const CameraDev& cam, const FeaturesDev& f, uint32_t key,
                               float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,
-                              float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss = nullptr);
+                              float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss = nullptr,
+                              bool skip_res = false);
 bool primary_ris_fits(const SceneDev& s);
+// the N = 1 biased spatial pass reads background tiles through MissTiles for these features / knobs (SoA planes)
+bool spatial_biased_reads_flags(const FeaturesDev& f, const Tuning& tu);
 hipError_t launch_temporal(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
                            const float4* n_t, const float4* p_mat, const float4* ca, const float4* cb,
                            const float4* pa, const float4* pb, float4* oa, float4* ob, float2* odbg,

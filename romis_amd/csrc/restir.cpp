@@ -1348,9 +1348,13 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
         ST_TRY(fb.tmiss().ensure(tiles));
         tmiss = fb.tmiss().as<uint8_t>();
     }
+    // biased passes follow (k_spatial1_ntl / _t2 substitute a background tile's known reservoirs; final shading reads
+    // the last pass's output): RIS need not store those reservoirs
+    const bool skip_res = tmiss && passes > 0 && spatial_biased_reads_flags(f, c->tuning) &&
+                          (size_t)t.gwidth * t.gheight * 16u <= 0xFFFFFFFFull;
     if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)
         TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),
-                                                          fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st, tmiss));
+                                                          fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st, tmiss, skip_res));
     } else {
         TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, fb.nt(0), pm, fb.nt2(), c->tuning, st));
         TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, ris_key, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), nullptr,

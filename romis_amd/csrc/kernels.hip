@@ -1912,6 +1912,7 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
     const int x = tx0 + (int)(w * 8u + (l & 7u)), y = ty0 + (int)(l >> 3);
     const uint32_t K = f.K;   // <= kLeanK (host check)
+    bool mixed = false;   // some input lies in a background tile (whose RIS reservoir may be unwritten: substituted)
     if (mt.m) {
         // the tile and every pixel its neighbour draws can reach (grown by R, clamped to the image and the view) are
         // background pixels holding (0, W = 0), (0, M = mt.m): the miss shortcut's result below with M = (K + 1) mt.m
@@ -1919,7 +1920,7 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
         const int gx0 = max(max(tx0 - (int)f.R, 0), (int)rg.vx0), gy0 = max(max(ty0 - (int)f.R, 0), (int)rg.vy0);
         const int gx1 = min(min(x1 + (int)f.R, (int)rg.W - 1), (int)(rg.vx0 + rg.vw) - 1);
         const int gy1 = min(min(y1 + (int)f.R, (int)rg.H - 1), (int)(rg.vy0 + rg.vh) - 1);
-        if (tiles_known_miss(mt, rg, gx0, gx1, gy0, gy1)) {
+        if (tiles_known_miss(mt, rg, gx0, gx1, gy0, gy1, &mixed)) {
             if (x <= x1 && y <= y1) {
                 const uint32_t mo = ((uint32_t)(y - (int)rg.vy0) * rg.vw + (uint32_t)(x - (int)rg.vx0)) << 4;
                 st_at(oa, mo, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
@@ -1937,8 +1938,25 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
     const int rx = x - (int)rg.vx0, ry = y - (int)rg.vy0;
     const uint32_t pofs = ((uint32_t)ry * rg.vw + (uint32_t)rx) << 4;
     const float4 cn = ld_at(n_t, pofs), cpm = ld_at(p_mat, pofs);
-    const float4 ca = ld_at(ia, pofs), cb = ld_at(ib, pofs);
-    const float pd_cached = rp_in ? ld_at(rp_in, pofs >> 2) : 0.0f;
+    // an input pixel of a background tile holds the known (0, W = 0), (0, M = mt.m), pdf 0 (RIS may not have stored
+    // them, its skip_res): in blocks whose neighbourhood meets such a tile (block-uniform) they are not read
+    const uint32_t ntxv = (rg.vw + kTileW - 1u) / kTileW;
+    auto known = [&](int vx, int vy) {   // view-relative pixel in a background tile
+        return mixed && mt.flags[((uint32_t)vy / kTileH) * ntxv + (uint32_t)vx / kTileW] == 0u;
+    };
+    auto ld_res = [&](uint32_t q, bool kn, float4& a, float4& b) {
+        if (kn) {
+            a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            b = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(mt.m));
+        } else {
+            a = ld_at(ia, q);
+            b = ld_at(ib, q);
+        }
+    };
+    float4 ca, cb;
+    const bool own_known = known(rx, ry);
+    ld_res(pofs, own_known, ca, cb);
+    const float pd_cached = (rp_in && !own_known) ? ld_at(rp_in, pofs >> 2) : 0.0f;
     // neighbour draws (render_utils.cpp:108-111), clamped to the image, then to the stored view
     const int xlo = max(0, (int)rg.vx0) - (int)rg.vx0, xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1 - (int)rg.vx0;
     const int ylo = max(0, (int)rg.vy0) - (int)rg.vy0, yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1 - (int)rg.vy0;
@@ -1946,18 +1964,20 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
     const uint32_t span = 2u * f.R + 1u;
     const int bx = rx - (int)f.R, by = ry - (int)f.R;
     uint32_t qo[kLeanK];
+    bool qk[kLeanK];
 #pragma unroll
     for (uint32_t n = 0; n < kLeanK; n++) {
         qo[n] = pofs;
+        qk[n] = own_known;
         if (n < K) {
             const int nx = min(max(bx + (int)__umulhi(draw(ps, 2u * n), span), xlo), xhi);
             const int ny = min(max(by + (int)__umulhi(draw(ps, 2u * n + 1u), span), ylo), yhi);
             qo[n] = ((uint32_t)ny * rg.vw + (uint32_t)nx) << 4;
+            qk[n] = known(nx, ny);
         }
     }
     float4 na[kLeanK], nb[kLeanK];
-    na[0] = ld_at(ia, qo[0]);
-    nb[0] = ld_at(ib, qo[0]);
+    ld_res(qo[0], qk[0], na[0], nb[0]);
     const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
     // A primary-ray miss: the target pdf of any sample there is exactly 0 (zero normal, kd = ks = 0: the biased pass's
     // shortcut), so with every input's W finite each weighs (0 W) M = +-0 -- nothing is accepted, wSum
@@ -1971,7 +1991,8 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
 #pragma unroll
         for (uint32_t n = 1; n < kLeanK; n++) {
             if (n < K) {
-                const float4 a = ld_at(ia, qo[n]), b = ld_at(ib, qo[n]);
+                float4 a, b;
+                ld_res(qo[n], qk[n], a, b);
                 fin = fin && __builtin_isfinite(a.w);
                 m += __float_as_uint(b.w);
             }
@@ -1995,7 +2016,7 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
     uint32_t src = kLeanK;   // the input the held sample came from (kLeanK = the pixel itself)
 #pragma unroll
     for (uint32_t n = 0; n < kLeanK; n++) {
-        if (n + 1 < kLeanK && n + 1 < K) { na[n + 1] = ld_at(ia, qo[n + 1]); nb[n + 1] = ld_at(ib, qo[n + 1]); }
+        if (n + 1 < kLeanK && n + 1 < K) ld_res(qo[n + 1], qk[n + 1], na[n + 1], nb[n + 1]);
         Mn[n] = 0u;
         if (n < K) {
             const v3 p = xyz(na[n]), c = xyz(nb[n]);
@@ -3160,11 +3181,12 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
 
 bool primary_ris_fits(const SceneDev& s) { return bvh_lds_bytes(s) <= kLdsBudget; }
 
-// launch_spatial's N = 1 biased pass reads background tiles through MissTiles (k_spatial1_ntl / _t2) for these
-// features and knobs, SoA planes -- the condition for RIS's skip_res
-bool spatial_biased_reads_flags(const FeaturesDev& f, const Tuning& tu) {
-    return !f.unbiased && f.N == 1 && f.K <= kLeanK && f.R <= kLdsSpatialR && tu.spatial_lean && tu.spatial_lds == 3u &&
-           tu.spatial_xcd && tu.spatial_wave8;
+// launch_spatial's N = 1 pass reads background tiles through MissTiles (k_spatial1_ntl / _t2 biased, k_spatial1u[_vis]
+// unbiased) for these features and knobs, SoA planes -- the condition for RIS's skip_res
+bool spatial_reads_flags(const SceneDev& s, const FeaturesDev& f, const Tuning& tu) {
+    if (f.N != 1 || f.K > kLeanK || !tu.spatial_lean || !tu.spatial_xcd || !tu.spatial_wave8) return false;
+    if (f.unbiased) return !f.spatial_vis || bvh_lds_bytes(s) <= kLdsBudget;   // k_spatial1u[_vis]
+    return f.R <= kLdsSpatialR && tu.spatial_lds == 3u;                       // k_spatial1_ntl / _t2
 }
 
 hipError_t launch_temporal(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,

@@ -20,8 +20,8 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg, const CameraD
                               float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss = nullptr,
                               bool skip_res = false);
 bool primary_ris_fits(const SceneDev& s);
-// the N = 1 biased spatial pass reads background tiles through MissTiles for these features / knobs (SoA planes)
-bool spatial_biased_reads_flags(const FeaturesDev& f, const Tuning& tu);
+// the N = 1 spatial pass reads background tiles through MissTiles for this scene / features / knobs (SoA planes)
+bool spatial_reads_flags(const SceneDev& s, const FeaturesDev& f, const Tuning& tu);
 hipError_t launch_temporal(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
                            const float4* n_t, const float4* p_mat, const float4* ca, const float4* cb,
                            const float4* pa, const float4* pb, float4* oa, float4* ob, float2* odbg,

@@ -1349,8 +1349,10 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
         tmiss = fb.tmiss().as<uint8_t>();
     }
     // the first spatial pass substitutes a background tile's known reservoirs (k_spatial1_ntl / _t2, k_spatial1u); the
-    // later passes and final shading read the passes' outputs: RIS need not store those reservoirs
-    const bool skip_res = tmiss && passes > 0 && spatial_reads_flags(s, f, c->tuning) &&
+    // later passes and final shading read the passes' outputs, and with no ghost ring the last pass overwrites the
+    // whole returned grid: RIS need not store those reservoirs
+    const bool skip_res = tmiss && passes > 0 && t.gwidth == t.width && t.gheight == t.height &&
+                          spatial_reads_flags(s, f, c->tuning) &&
                           (size_t)t.gwidth * t.gheight * 16u <= 0xFFFFFFFFull;
     if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)
         TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),

@@ -11,9 +11,11 @@ timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_h
     -k "miss_tiles or render_frame_matches or c4_c5 or full_size or stitch or in_flight or spatial_pass_bit_exact or final or halo_frames" \
     > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 20; }
 tail -1 $OUT/tests.log
-timeout -k 10 300 python3 scripts/cfg_kbench.py --config c4 --rounds 4 --frames 8 --variants default: tiles0:miss.tiles=0 \
-    > $OUT/c4.json 2> $OUT/c4.err || { tail -5 $OUT/c4.err; exit 19; }
-cat $OUT/c4.json
+for c in c4 c5; do
+    timeout -k 10 300 python3 scripts/cfg_kbench.py --config $c --rounds 4 --frames $([ $c = c5 ] && echo 3 || echo 8) \
+        --variants default: tiles0:miss.tiles=0 > $OUT/$c.json 2> $OUT/$c.err || { tail -5 $OUT/$c.err; exit 19; }
+    cat $OUT/$c.json
+done
 V=("chunks:spatial.xcd_rows=255" "r8c20:spatial.xcd_rows=8,spatial.xcd_cols=20" "r8c12:spatial.xcd_rows=8,spatial.xcd_cols=12"
    "r6c20:spatial.xcd_rows=6,spatial.xcd_cols=20")
 timeout -k 10 400 python3 scripts/cfg_kbench.py --config c2 --rounds 8 --frames 10 --variants "${V[@]}" > $OUT/ab1.json 2> $OUT/ab1.err \

@@ -39,7 +39,7 @@ def main():
         W, H = cf.get("tile") or cf["image"]
         px = W * H
         times = json.load(open(os.path.join(src, f"{cfgname}_times.json")))["us_per_launch"]
-        orders = [("chunks", 255), ("bands", 0)] + ([("chunks_th1", 255)] if cfgname == "c4" else [])
+        orders = [("chunks", 255), ("bands", 0), ("tiles0", 255)] + ([("chunks_th1", 255)] if cfgname == "c4" else [])
         for order, rows in orders:
             f = os.path.join(src, f"{cfgname}_{order}_FETCH_SIZE", "run_counter_collection.csv")
             w = os.path.join(src, f"{cfgname}_{order}_WRITE_SIZE", "run_counter_collection.csv")
@@ -57,10 +57,13 @@ def main():
                 "algorithmic_bytes": alg, "ratio": round((fetch + write) / alg, 3),
                 "fetch_B_per_px": round(fetch / px, 1), "write_B_per_px": round(write / px, 1),
                 "spatial_us": times[order]["spatial"],
+                "miss_tiles": order != "tiles0",
                 "attribution_B_per_px": {
                     "algorithmic_read (G 32 + reservoir 32)": 64, "algorithmic_write (reservoir)": 32,
                     "pdf cache plane (rp) read + write": 8,
-                    "refetch of the +-R window rows across XCD work boundaries (fetch - 64 - 4)": round(fetch / px - 68, 1),
+                    # with the background-tile flags a background tile reads nothing, so fetch can fall below 68
+                    "fetch beyond the algorithmic 64 + 4 (window rows re-fetched across XCD work boundaries, minus the "
+                    "reads background tiles skip)": round(fetch / px - 68, 1),
                     "other write (write - 32 - 4)": round(write / px - 36, 1)}})
     c2 = next(e for e in entries if e["config"]["config"] == "c2" and e["xcd_order"] == "chunks")
     rec = {"source_hash": build.source_hash(), "kernel": "k_spatial1_ntl", "profile": args.profile,

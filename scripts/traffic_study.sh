@@ -1,6 +1,7 @@
 #!/bin/bash
 # HBM traffic of the spatial pass (FETCH_SIZE / WRITE_SIZE, separate --pmc passes) at C2 (1080p) and C4 (4K) for
-# the XCD chunk order (default) and one contiguous band per XCD (spatial.xcd_rows = 0), plus the kernel times of
+# the XCD chunk order (default), one contiguous band per XCD (spatial.xcd_rows = 0) and the background-tile flags off
+# (miss.tiles = 0), plus the kernel times of
 # the same variants; at C4 also 32x8 tiles (spatial.th = 1) beside the default 32x16.   scripts/traffic_study.sh <tag>
 set -o pipefail
 TAG=${1:-traffic}
@@ -10,7 +11,7 @@ mkdir -p "$OUT"
 cd "$REPO" || exit 1
 export TMPDIR=/tmp
 for CFG in c2 c4; do
-    VARS=("chunks:spatial.xcd_rows=255" "bands:spatial.xcd_rows=0")
+    VARS=("chunks:spatial.xcd_rows=255" "bands:spatial.xcd_rows=0" "tiles0:spatial.xcd_rows=255,miss.tiles=0")
     # C4: the default 32x16 tiles (k_spatial1_ntl_t2) against 32x8 ones
     [ $CFG = c4 ] && VARS+=("chunks_th1:spatial.xcd_rows=255,spatial.th=1")
     for V in "${VARS[@]}"; do

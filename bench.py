@@ -517,10 +517,11 @@ def main():
         else:
             r.render_restir(None, cam, GW, GH, f, tile=tile, want_rgb=False, want_grid=False)
 
-    # GPU clock pre-warm (not a frame, not timed), then the practical HBM-read ceiling reported beside the roofline
+    # the practical HBM-read ceiling reported beside the roofline, then the GPU clock pre-warm (not a frame, not timed)
+    # right before the warm-up frames
+    measured = r.measure_read_bandwidth(4 << 30, 10)
     if args.prewarm_gemm_ms > 0:
         gemm_prewarm(torch, local, args.prewarm_gemm_ms)
-    measured = r.measure_read_bandwidth(4 << 30, 10)
     if not halo:
         r.set_tuning("frames.inflight", args.inflight)
     for _ in range(args.warmup):

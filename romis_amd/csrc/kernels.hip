@@ -609,7 +609,7 @@ extern __shared__ __attribute__((aligned(16))) float4 g_lds[];
 __device__ __forceinline__ void primary_pixel(const SceneDev& s, const Region& rg, const CameraDev& cam, const Bvh& bvh,
                                               uint32_t x, uint32_t y, size_t p, float4* __restrict__ n_t2,
                                               float4* __restrict__ n_t, float4* __restrict__ p_mat, float4& nt_out,
-                                              float4& pm_out) {
+                                              float4& pm_out, bool store = true) {
     const v3 o = mk(cam.origin[0], cam.origin[1], cam.origin[2]);
     {
         float nx = (float)x / (float)rg.W * 2.0f - 1.0f;
@@ -637,11 +637,13 @@ __device__ __forceinline__ void primary_pixel(const SceneDev& s, const Region& r
         if (s.gbuf_uv) s.gbuf_uv[p] = tc;
         v3 P = vadd(o, vscale(d, t));
         const float4 nt = make_float4(n.x, n.y, n.z, t);
-        n_t[gidx(rg, p)] = nt;
-        if (n_t2) n_t2[gidx(rg, p)] = nt;   // the other record buffer of the ping-pong pair
         pm_out = make_float4(P.x, P.y, P.z, __uint_as_float(m));
-        p_mat[p] = pm_out;
         nt_out = nt;
+        if (store) {   // store = false: the caller stores the records (or not: primary_ris_body's background tiles)
+            n_t[gidx(rg, p)] = nt;
+            if (n_t2) n_t2[gidx(rg, p)] = nt;   // the other record buffer of the ping-pong pair
+            p_mat[p] = pm_out;
+        }
     }
 }
 
@@ -909,7 +911,8 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         size_t p;
         const bool live = work_pixel(rg, blockIdx.x, x, y, p);
         float4 nt = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pm = nt;
-        if (live) primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, nt, pm);
+        const bool skip_gbuf = tmiss && (skip_res & 2u);   // bit 1: a background tile's G-buffer records too
+        if (live) primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, nt, pm, !skip_gbuf);
         uint32_t m = __float_as_uint(pm.w);
         if (m >= s.num_materials) m = s.num_materials - 1u;
         const bool loop = live && s.num_lights != 0u &&
@@ -917,13 +920,19 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         const bool any = __syncthreads_or(loop);
         // flag 0: every live pixel is a miss with the known RIS result (lights present: no loop means a known miss)
         if (tmiss && threadIdx.x == 0) tmiss[blockIdx.x] = (s.num_lights == 0u || any) ? 1u : 0u;
+        if (skip_gbuf && live && any) {
+            n_t[gidx(rg, p)] = nt;
+            if (n_t2) n_t2[gidx(rg, p)] = nt;
+            p_mat[p] = pm;
+        }
         if (late && any) {
             stage_lights<LT>(s, g_lds + bvh_f4);
             __syncthreads();
         }
-        // skip_res (the launcher's promise that no reader needs them): a background tile's known reservoirs and pdfs
-        // are not stored -- the biased lean passes and final shading substitute them from the flag
-        if (live && (any || !tmiss || !skip_res))
+        // skip_res (the launcher's promise that no reader needs them): bit 0, a background tile's known reservoirs and
+        // pdfs are not stored -- the first spatial pass substitutes them from the flag; bit 1 (above), nor its G-buffer
+        // records (a single unbiased pass, which substitutes those too)
+        if (live && (any || !tmiss || !(skip_res & 1u)))
             ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb);
         return;
     }
@@ -1937,13 +1946,22 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
     if (x >= (int)(rg.rx0 + rg.rw) || y >= (int)(rg.ry0 + rg.rh)) return;
     const int rx = x - (int)rg.vx0, ry = y - (int)rg.vy0;
     const uint32_t pofs = ((uint32_t)ry * rg.vw + (uint32_t)rx) << 4;
-    const float4 cn = ld_at(n_t, pofs), cpm = ld_at(p_mat, pofs);
     // an input pixel of a background tile holds the known (0, W = 0), (0, M = mt.m), pdf 0 (RIS may not have stored
     // them, its skip_res): in blocks whose neighbourhood meets such a tile (block-uniform) they are not read
     const uint32_t ntxv = (rg.vw + kTileW - 1u) / kTileW;
     auto known = [&](int vx, int vy) {   // view-relative pixel in a background tile
         return mixed && mt.flags[((uint32_t)vy / kTileH) * ntxv + (uint32_t)vx / kTileW] == 0u;
     };
+    // ... nor its G-buffer records (skip_res bit 1): a miss's normal 0 and t = FLT_MAX; for its P, what the pass
+    // uses of it -- not NaN (the flag's promise) -- holds for 0, and its material is the miss material
+    float4 cn, cpm;
+    if (known(rx, ry)) {
+        cn = make_float4(0.0f, 0.0f, 0.0f, ROMIS_FLT_MAX);
+        cpm = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(s.num_materials - 1u));
+    } else {
+        cn = ld_at(n_t, pofs);
+        cpm = ld_at(p_mat, pofs);
+    }
     auto ld_res = [&](uint32_t q, bool kn, float4& a, float4& b) {
         if (kn) {
             a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -2033,7 +2051,9 @@ __device__ __forceinline__ void spatial1u_body(const SceneDev& s, const Region& 
         unsigned long long Z = 0ull;
 #pragma unroll
         for (uint32_t n = 0; n < kLeanK; n++) {
-            if (n < K) {
+            if (n < K && !qk[n]) {
+                // (a background neighbour: the miss material's p-hat of any sample is +-0 or a cleaned-up NaN, never
+                // positive -- no term, and its G-buffer is not read)
                 const float4 qn = ld_at(n_t, qo[n]), qp = ld_at(p_mat, qo[n]);
                 const Px rp = make_px(s, qn, qp, origin, qo[n] >> 4);
                 const bool pos = (src == n && rp_nb) ? ld_at(rp_nb, qo[n] >> 2) > 0.0f
@@ -3154,7 +3174,7 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f
 
 hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const CameraDev& cam, const FeaturesDev& f, uint32_t key,
                               float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,
-                              float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss, bool skip_res) {
+                              float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss, uint32_t skip_res) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, tu.primary_2d);
     // MissTiles flags: one 32 x 8 tile per block, N = 1 (the caller allocates one byte per tile)
@@ -3175,7 +3195,7 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
                         : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
     ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.ris_blocks), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
                  cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr, tu.ris_late, tmiss,
-                 (tmiss && skip_res) ? 1u : 0u);
+                 tmiss ? skip_res : 0u);
     return hipGetLastError();
 }
 
@@ -3183,6 +3203,11 @@ bool primary_ris_fits(const SceneDev& s) { return bvh_lds_bytes(s) <= kLdsBudget
 
 // launch_spatial's N = 1 pass reads background tiles through MissTiles (k_spatial1_ntl / _t2 biased, k_spatial1u[_vis]
 // unbiased) for these features and knobs, SoA planes -- the condition for RIS's skip_res
+// launch_final's k_final_n1_sorted writes background tiles from the flags without reading them
+bool final_reads_flags(const SceneDev& s, const FeaturesDev& f, const Tuning& tu) {
+    return f.N == 1 && tu.final_sort && tu.final_lds && tu.final_2d && bvh_lds_bytes(s) <= kLdsBudget;
+}
+
 bool spatial_reads_flags(const SceneDev& s, const FeaturesDev& f, const Tuning& tu) {
     if (f.N != 1 || f.K > kLeanK || !tu.spatial_lean || !tu.spatial_xcd || !tu.spatial_wave8) return false;
     if (f.unbiased) return !f.spatial_vis || bvh_lds_bytes(s) <= kLdsBudget;   // k_spatial1u[_vis]

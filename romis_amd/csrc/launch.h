@@ -18,10 +18,12 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg, const FeaturesDev& f,
 hipError_t launch_primary_ris(const SceneDev& s, const Region& rg, const CameraDev& cam, const FeaturesDev& f, uint32_t key,
                               float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,
                               float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss = nullptr,
-                              bool skip_res = false);
+                              uint32_t skip_res = 0u);   // bit 0: background reservoirs, bit 1: background G-buffer
 bool primary_ris_fits(const SceneDev& s);
 // the N = 1 spatial pass reads background tiles through MissTiles for this scene / features / knobs (SoA planes)
 bool spatial_reads_flags(const SceneDev& s, const FeaturesDev& f, const Tuning& tu);
+// final shading writes background tiles from MissTiles without reading them (k_final_n1_sorted)
+bool final_reads_flags(const SceneDev& s, const FeaturesDev& f, const Tuning& tu);
 hipError_t launch_temporal(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
                            const float4* n_t, const float4* p_mat, const float4* ca, const float4* cb,
                            const float4* pa, const float4* pb, float4* oa, float4* ob, float2* odbg,

@@ -1354,9 +1354,13 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     const bool skip_res = tmiss && passes > 0 && t.gwidth == t.width && t.gheight == t.height &&
                           spatial_reads_flags(s, f, c->tuning) &&
                           (size_t)t.gwidth * t.gheight * 16u <= 0xFFFFFFFFull;
+    // a single unbiased pass (k_spatial1u) also substitutes a background pixel's G-buffer records (own and the Z loop's
+    // neighbours); final shading reads none of them (its tiles are the RIS tiles here): nor are those stored
+    const uint32_t skip_mode =
+        skip_res ? (1u | ((f.unbiased && passes == 1u && final_reads_flags(s, f, c->tuning)) ? 2u : 0u)) : 0u;
     if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)
         TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),
-                                                          fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st, tmiss, skip_res));
+                                                          fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st, tmiss, skip_mode));
     } else {
         TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, fb.nt(0), pm, fb.nt2(), c->tuning, st));
         TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, ris_key, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), nullptr,

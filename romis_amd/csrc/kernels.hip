@@ -1587,12 +1587,14 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     float4 cpm = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ca = cpm, cb = cpm;
     float pd_cached = 0.0f;
     if (live) {
-        cpm = ld_at(p_mat, pofs);
         // a pixel of a background tile holds the known (0, W = 0), (0, M = mt.m) and pdf 0: RIS may not have stored
-        // them (its skip_res), so they are not read (a block-uniform branch: only tiles that straddle RIS tiles)
+        // them (its skip_res), so they are not read (a block-uniform branch: only tiles that straddle RIS tiles); nor,
+        // with mt.gbuf, its G-buffer records: the miss material and a P that is not NaN is all the shortcut uses
         if (mixed && tile_flag_at(mt, rg, x, y) == 0u) {
+            cpm = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(s.num_materials - 1u));
             cb.w = __uint_as_float(mt.m);
         } else {
+            cpm = ld_at(p_mat, pofs);
             ca = ld_at(ia, pofs);
             cb = ld_at(ib, pofs);
             if (rp_in) pd_cached = ld_at(rp_in, pofs >> 2);
@@ -1619,6 +1621,22 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     // DMA before that wave's ds_reads, and a workgroup-scope fence need not drain vmcnt on gfx950, so the wait
     // is explicit (scripts/kernel_isa.sh k_spatial1_ntl: s_waitcnt vmcnt(0) directly before s_barrier).
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (mt.gbuf) {
+        // RIS stored no G-buffer for background tiles: this thread's window entries there (its own LDS-DMA copies,
+        // landed after the wait above) become a miss's record, normal 0 and t = FLT_MAX -- what RIS would have stored
+        constexpr uint32_t kThreads = 256u * TH, kPer = (apron_max(TH) + kThreads - 1u) / kThreads;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++) {
+            const uint32_t i = threadIdx.x + kThreads * k;
+            if (i < n_apron) {
+                uint32_t r = __umulhi(i, 0xFFFFFFFFu / AW + 1u);   // i / AW for i < 2^16 (ntl_stage_window)
+                if (r * AW > i) r--;
+                const uint32_t c = i - r * AW;
+                if (tile_flag_at(mt, rg, ax0 + (int)c, ay0 + (int)r) == 0u)
+                    l_nt[i] = make_float4(0.0f, 0.0f, 0.0f, ROMIS_FLT_MAX);
+            }
+        }
+    }
     __syncthreads();
     if (!live) return;   // no barrier follows
     const float4 cn = l_nt[(uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0)];
@@ -2313,7 +2331,7 @@ extern "C" __global__ __launch_bounds__(256) void k_final_n1_sorted(SceneDev s, 
 extern "C" __global__ __launch_bounds__(256) void k_final_n2_sorted(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,
                                                                    float oz, const float4* n_t, const float4* p_mat,
                                                                    const float4* ra, const float4* rb, float* rgb) {
-    final_sorted_body<true, 2>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, nullptr, MissTiles{nullptr, 0u});
+    final_sorted_body<true, 2>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, nullptr, MissTiles{nullptr, 0u, 0u});
 }
 
 #define ROMIS_FINAL_KERNEL(NT, LDS, NAME)                                                                              \
@@ -3337,7 +3355,7 @@ hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev&
         if (!tu.final_miss) sf.miss_shade_zero = 0u;   // final.miss = 0: no miss shortcut (A/B runs)
         if (f.N == 1)
             ROMIS_LAUNCH(k_final_n1_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, sf, rg, f, o[0], o[1], o[2], n_t,
-                         p_mat, ra, rb, rgb, vis_in, rg.map2d ? mt : MissTiles{nullptr, 0u});
+                         p_mat, ra, rb, rgb, vis_in, rg.map2d ? mt : MissTiles{nullptr, 0u, 0u});
         else
             ROMIS_LAUNCH(k_final_n2_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, sf, rg, f, o[0], o[1], o[2], n_t,
                          p_mat, ra, rb, rgb);

@@ -32,11 +32,11 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg, const FeaturesDev
                           const float4* n_t, const float4* p_mat, const float4* ia, const float4* ib, float4* oa,
                           float4* ob, float2* odbg, const float* rp_in, const float* rp_nb, float* rp_out,
                           bool* rp_written, const Tuning& tu, hipStream_t stream, uint8_t* vis_out = nullptr,
-                          bool* vis_written = nullptr, MissTiles mt = MissTiles{nullptr, 0u});
+                          bool* vis_written = nullptr, MissTiles mt = MissTiles{nullptr, 0u, 0u});
 hipError_t launch_final(const SceneDev& s, const Region& rg, const FeaturesDev& f, const float* origin,
                         const float4* n_t, const float4* p_mat, const float4* ra, const float4* rb, float* rgb,
                         const Tuning& tu, hipStream_t stream, const uint8_t* vis_in = nullptr,
-                        MissTiles mt = MissTiles{nullptr, 0u});
+                        MissTiles mt = MissTiles{nullptr, 0u, 0u});
 hipError_t launch_halo_pack(const Region& rg, const HaloSegs& hs, uint32_t N, const float4* ra, const float4* rb, float4* out,
                             hipStream_t stream);
 hipError_t launch_halo_unpack(const Region& rg, const HaloSegs& hs, uint32_t N, const float4* in, float4* ra, float4* rb,

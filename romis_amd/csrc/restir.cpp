@@ -1356,8 +1356,11 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                           (size_t)t.gwidth * t.gheight * 16u <= 0xFFFFFFFFull;
     // a single unbiased pass (k_spatial1u) also substitutes a background pixel's G-buffer records (own and the Z loop's
     // neighbours); final shading reads none of them (its tiles are the RIS tiles here): nor are those stored
-    const uint32_t skip_mode =
-        skip_res ? (1u | ((f.unbiased && passes == 1u && final_reads_flags(s, f, c->tuning)) ? 2u : 0u)) : 0u;
+    // Biased passes (every pass reads the flags) fix their window up instead (MissTiles::gbuf); knob miss.gbuf.
+    const uint32_t mg = c->tuning.miss_gbuf;
+    const bool gbuf_ok = mg && final_reads_flags(s, f, c->tuning) &&
+                         (f.unbiased ? passes == 1u : (mg == 1u || t.gwidth >= 2048u));
+    const uint32_t skip_mode = skip_res ? (1u | (gbuf_ok ? 2u : 0u)) : 0u;
     if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)
         TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),
                                                           fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st, tmiss, skip_mode));
@@ -1399,12 +1402,12 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                              pass + 1 == passes ? vis : nullptr, &vis_ok,
                              // a background pixel holds M = f.M after RIS and after every biased pass; an unbiased pass
                              // sums its neighbours' M, which only pass 0 knows
-                             MissTiles{tmiss, (!f.unbiased || pass == 0) ? f.M : 0u}));
+                             MissTiles{tmiss, (!f.unbiased || pass == 0) ? f.M : 0u, (skip_mode & 2u) ? 1u : 0u}));
         cur = nxt;
     }
     if (pipe) HIP_TRY(hipEventRecord(c->pipe.after_spatial[k], st));
     TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), fb.rgb().as<float>(),
-                                          c->tuning, st, vis_ok ? vis : nullptr, MissTiles{tmiss, 0u}));
+                                          c->tuning, st, vis_ok ? vis : nullptr, MissTiles{tmiss, 0u, 0u}));
     if (pipe) {
         HIP_TRY(hipEventRecord(c->pipe.after_final[k], st));
         c->pipe.has[k] = true;
@@ -2352,6 +2355,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.xcd_cols")) t.spatial_xcd_cols = v;
     else if (!std::strcmp(key, "ris.late")) t.ris_late = v;
     else if (!std::strcmp(key, "miss.tiles")) t.miss_tiles = v;
+    else if (!std::strcmp(key, "miss.gbuf")) t.miss_gbuf = v;
     else if (!std::strcmp(key, "final.miss")) t.final_miss = v;
     else if (!std::strcmp(key, "spatial.lds")) {
         if (v != 0u && v != 3u)

@@ -107,6 +107,7 @@ struct Region {
 struct MissTiles {
     const uint8_t* flags;
     uint32_t m;
+    uint32_t gbuf;   // 1: RIS did not store background tiles' G-buffer records either (a biased pass fixes its window up)
 };
 
 // Launch-shape knobs (restir_set_tuning); they never change results, only speed.
@@ -122,6 +123,9 @@ struct Tuning {
                                    // _grid RIS kernels, kernels.hip ris_light_form)
     uint32_t miss_tiles = 1;       // restir_render: background-tile flags (MissTiles) from RIS to the spatial passes
                                    // and final shading
+    uint32_t miss_gbuf = 2;        // RIS skips background tiles' G-buffer stores: 0 never, 1 whenever the passes and final
+                                   // shading allow, 2 (auto) the same but biased passes only from 2048 px wide (their
+                                   // window fix-up's per-entry flag loads outweigh the saved stores at 1080p)
     uint32_t ris_late = 1;         // fused primary + RIS, one tile per block: stage the light table only for tiles with
                                    // a pixel that runs the candidate loop (0: every tile, before the primary rays)
     uint32_t spatial_xcd = 1;      // XCD-banded tile order

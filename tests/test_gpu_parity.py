@@ -891,11 +891,15 @@ def test_frames_in_flight_match_serial_frames(gpu, oracle, temporal, passes, N):
         gpu.set_tuning("frames.inflight", 1)
 
 
-@pytest.mark.parametrize("name,passes,unbiased,vis,tiled", [
-    ("cornell_1024", 1, 0, 0, 0), ("cornell_1024", 2, 0, 0, 0), ("cornell_4096", 1, 1, 1, 0),
-    ("cornell_4096", 2, 1, 1, 0), ("cornell_4096", 1, 1, 0, 0), ("nightclub_128pt", 1, 0, 0, 0),
-    ("cornell_1024", 2, 0, 0, 1), ("cornell_4096", 2, 1, 1, 1)])
-def test_miss_tiles_match_full_reads(gpu, name, passes, unbiased, vis, tiled):
+@pytest.mark.parametrize("name,passes,unbiased,vis,tiled,tune", [
+    ("cornell_1024", 1, 0, 0, 0, {}), ("cornell_1024", 2, 0, 0, 0, {}), ("cornell_4096", 1, 1, 1, 0, {}),
+    ("cornell_4096", 2, 1, 1, 0, {}), ("cornell_4096", 1, 1, 0, 0, {}), ("nightclub_128pt", 1, 0, 0, 0, {}),
+    ("cornell_1024", 2, 0, 0, 1, {}), ("cornell_4096", 2, 1, 1, 1, {}),
+    # biased passes with the G-buffer stores skipped too (miss.gbuf = 1; the default does so only from 2048 px wide):
+    # the window fix-up, on 32 x 8 and on 32 x 16 tiles
+    ("cornell_1024", 1, 0, 0, 0, {"miss.gbuf": 1}), ("cornell_1024", 2, 0, 0, 0, {"miss.gbuf": 1}),
+    ("cornell_1024", 1, 0, 0, 0, {"miss.gbuf": 1, "spatial.th": 2}), ("nightclub_128pt", 1, 0, 0, 0, {"miss.gbuf": 1})])
+def test_miss_tiles_match_full_reads(gpu, name, passes, unbiased, vis, tiled, tune):
     """MissTiles (miss.tiles = 1, the default): RIS flags the 32 x 8 tiles whose pixels all missed the scene, and the
     spatial passes and final shading write those tiles' known results without reading them.  Frames at 640 x 360
     (the Cornell box fills the middle: most tiles, and most unbiased neighbourhoods, are background), whole and as a
@@ -917,10 +921,14 @@ def test_miss_tiles_match_full_reads(gpu, name, passes, unbiased, vis, tiled):
         return rgb, grid.download()
 
     try:
+        for k, v in tune.items():
+            gpu.set_tuning(k, v)
         off_rgb, off_grid = run(0)
         on_rgb, on_grid = run(1)
     finally:
         gpu.set_tuning("miss.tiles", 1)
+        gpu.set_tuning("miss.gbuf", 2)
+        gpu.set_tuning("spatial.th", 0)
     assert_bits(on_rgb, off_rgb, f"{name} rgb")
     for a, b in zip(off_grid, on_grid):
         assert np.array_equal(np.asarray(a).view(np.uint32), np.asarray(b).view(np.uint32)), f"{name} grid"

@@ -3268,7 +3268,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
         rg.xcd_rows = tu.spatial_xcd_rows == kXcdRowsAuto ? std::max(1u, std::min(8u, 8192u / std::max(rg.rw, 1u)))
                                                           : tu.spatial_xcd_rows;
-        rg.xcd_cols = tu.spatial_xcd_cols;
+        rg.xcd_cols = tu.spatial_xcd_cols == kXcdColsAuto ? 0u : tu.spatial_xcd_cols;
         if (rg.xcd_rows) grid = xcd_grid(rg, ntx, nty);
         auto k = f.spatial_vis ? (odbg ? k_spatial1u_vis_dbg : k_spatial1u_vis) : (odbg ? k_spatial1u_dbg : k_spatial1u);
         uint8_t* vo = f.spatial_vis ? vis_out : nullptr;   // the own-pixel shadow ray, for final shading (N = 1)
@@ -3284,7 +3284,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
         rg.xcd_rows = tu.spatial_xcd_rows == kXcdRowsAuto ? std::max(1u, std::min(8u, 8192u / std::max(rg.rw, 1u)))
                                                           : tu.spatial_xcd_rows;
-        rg.xcd_cols = tu.spatial_xcd_cols;
+        rg.xcd_cols = tu.spatial_xcd_cols == kXcdColsAuto ? 0u : tu.spatial_xcd_cols;
         if (rg.xcd_rows) grid = xcd_grid(rg, ntx, nty);
         ROMIS_LAUNCH(odbg ? k_spatial2_ntl_dbg : k_spatial2_ntl, dim3(grid), dim3(kBlock), kApronMax * 16u, stream, s, rg, f,
                      key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg);
@@ -3300,7 +3300,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
             // 4 tile rows at 1920 px, 2 at 3840 (kbench: 4K 239 -> 225 us with 2, 1080p best with 4; r2bb)
             rg.xcd_rows = std::max(1u, std::min(8u, 8192u / std::max(rg.rw, 1u)));
         }
-        rg.xcd_cols = tu.spatial_xcd_cols;
+        rg.xcd_cols = tu.spatial_xcd_cols == kXcdColsAuto ? 0u : tu.spatial_xcd_cols;
         if (rg.xcd_rows) grid = xcd_grid(rg, ntx, nty);
         // 32x16 tiles (k_spatial1_ntl_t2) where the auto XCD chunk is at most 2 tile rows (wide images): C4 222 ->
         // 203 us, C2 76.8 -> 79.0 (cfg_kbench, profiles/r3/r3k); spatial.th = 1 / 2 forces either
@@ -3319,6 +3319,14 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
                          apron_max(2) * 16u, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg,
                          rp_in, rp_out, mt);
         } else if (tu.spatial_lds == 3u && f.R <= kLdsSpatialR) {
+            if (tu.spatial_xcd_cols == kXcdColsAuto && rg.xcd_rows && ntx >= 24u) {
+                // 2-D chunks: 8 tile rows x a third of the tile row (an odd number of chunks per chunk row, so the
+                // round-robin XCDs cover every column).  C2: fetch 83 -> 66 B/px at the same time (profiles/r4/r4g,
+                // r4h): the window rows a chunk's consecutive tile rows share stay in the XCD's L2.
+                if (tu.spatial_xcd_rows == kXcdRowsAuto) rg.xcd_rows = 8u;
+                rg.xcd_cols = (ntx + 2u) / 3u;
+                grid = xcd_grid(rg, ntx, nty);
+            }
 #ifndef ROMIS_NTL_EXTRA_LDS
 #define ROMIS_NTL_EXTRA_LDS 0   // occupancy experiments (build variants): extra dynamic LDS per block
 #endif

@@ -112,6 +112,7 @@ struct MissTiles {
 
 // Launch-shape knobs (restir_set_tuning); they never change results, only speed.
 constexpr uint32_t kXcdRowsAuto = 255u;
+constexpr uint32_t kXcdColsAuto = 255u;
 struct Tuning {
     uint32_t primary_blocks = 0;   // grid cap (persistent blocks); 0 = one block per work item
     uint32_t primary_lds = 1;      // stage the BVH in LDS when it fits
@@ -133,8 +134,10 @@ struct Tuning {
                                    // (k_spatial1, gathers; also any R > 10)
     uint32_t spatial_xcd_rows = 255; // k_spatial1: XCD x takes every 8th chunk of this many tile rows (0: one band;
                                      // 255 = kXcdRowsAuto: as many as keep a chunk's records in one XCD's L2)
-    uint32_t spatial_xcd_cols = 0;   // chunk width in tiles (0: full rows); 2-D chunks keep the +-R window rows of
-                                     // consecutive tile rows in the XCD's L2 on wide images
+    uint32_t spatial_xcd_cols = 255; // chunk width in tiles (0: full rows); 2-D chunks keep the +-R window rows of
+                                     // consecutive tile rows in the XCD's L2.  255 = kXcdColsAuto: the N = 1 biased
+                                     // pass on 32 x 8 tiles takes 8 tile rows x a third of the tile row when the row
+                                     // has >= 24 tiles (C2: 1.20 -> 1.0x traffic, same time), full rows elsewhere
     uint32_t spatial_blocks = 0;
     uint32_t spatial_wave8 = 1;    // waves cover 8x8 pixel blocks instead of 32x2 rows (-2..4 %, kbench)
     uint32_t fuse_primary_ris = 1; // restir_render: k_primary_ris instead of k_primary + k_ris when the BVH fits LDS

@@ -21,7 +21,7 @@ import numpy as np  # noqa: E402
 from romis_amd import _abi, restir, scene  # noqa: E402
 
 DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 1, "ris.queue": 0, "ris.compact": 1,
-            "ris.late": 1, "miss.tiles": 1, "miss.gbuf": 2, "spatial.xcd": 1, "spatial.xcd_rows": 255, "spatial.xcd_cols": 0, "spatial.lds": 3, "spatial.blocks": 0, "spatial.wave8": 1, "spatial.lean": 1, "spatial.th": 0, "fuse.primary_ris": 1, "bvh.max_leaf": 2, "final.blocks": 0, "final.lds": 1, "final.2d": 1,
+            "ris.late": 1, "miss.tiles": 1, "miss.gbuf": 2, "spatial.xcd": 1, "spatial.xcd_rows": 255, "spatial.xcd_cols": 255, "spatial.lds": 3, "spatial.blocks": 0, "spatial.wave8": 1, "spatial.lean": 1, "spatial.th": 0, "fuse.primary_ris": 1, "bvh.max_leaf": 2, "final.blocks": 0, "final.lds": 1, "final.2d": 1,
             "final.sort": 1, "final.miss": 1, "layout.records": 0}
 
 VARIANTS = {

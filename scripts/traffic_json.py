@@ -39,7 +39,8 @@ def main():
         W, H = cf.get("tile") or cf["image"]
         px = W * H
         times = json.load(open(os.path.join(src, f"{cfgname}_times.json")))["us_per_launch"]
-        orders = [("chunks", 255), ("bands", 0), ("tiles0", 255)] + ([("chunks_th1", 255)] if cfgname == "c4" else [])
+        orders = [("chunks", 255), ("rows", 255), ("bands", 0), ("tiles0", 255)] + \
+            ([("chunks_th1", 255)] if cfgname == "c4" else [])
         for order, rows in orders:
             f = os.path.join(src, f"{cfgname}_{order}_FETCH_SIZE", "run_counter_collection.csv")
             w = os.path.join(src, f"{cfgname}_{order}_WRITE_SIZE", "run_counter_collection.csv")

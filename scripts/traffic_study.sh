@@ -11,7 +11,8 @@ mkdir -p "$OUT"
 cd "$REPO" || exit 1
 export TMPDIR=/tmp
 for CFG in c2 c4; do
-    VARS=("chunks:spatial.xcd_rows=255" "bands:spatial.xcd_rows=0" "tiles0:spatial.xcd_rows=255,miss.tiles=0")
+    VARS=("chunks:spatial.xcd_rows=255" "rows:spatial.xcd_rows=255,spatial.xcd_cols=0" "bands:spatial.xcd_rows=0"
+          "tiles0:spatial.xcd_rows=255,miss.tiles=0")
     # C4: the default 32x16 tiles (k_spatial1_ntl_t2) against 32x8 ones
     [ $CFG = c4 ] && VARS+=("chunks_th1:spatial.xcd_rows=255,spatial.th=1")
     for V in "${VARS[@]}"; do

@@ -216,7 +216,7 @@ SPATIAL_VARIANTS = {"gather": {"spatial.lean": 1, "spatial.lds": 0},
                     "ntl_t2_2d": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 2, "spatial.xcd_rows": 1,
                                   "spatial.xcd_cols": 2},
                     "general": {"spatial.lean": 0}}
-SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 255, "spatial.xcd_cols": 0, "spatial.th": 0}
+SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 255, "spatial.xcd_cols": 255, "spatial.th": 0}
 
 
 # every (scene, N, combine mode) through the default knobs ("gather" selects the lean gather kernel for N = 1 biased

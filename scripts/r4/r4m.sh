@@ -23,3 +23,6 @@ for rep in 1 2 3; do
         python3 -c "import json; d=json.load(open('$OUT/b_${name}_$rep.json')); print('$name', d['ms_per_step'], d['value'], d['roofline']['avg_launch_us'])"
     done
 done
+# RIS at 7 waves per SIMD (72 VGPRs, 20 B of spills) against the shipped 6
+bash scripts/ab_libs_cfg.sh r4m/w7 c2 "--rounds 5 --frames 10" ris_w7 || exit 24
+bash scripts/ab_libs_cfg.sh r4m/w7 c4 "--rounds 3 --frames 8" ris_w7 || exit 25

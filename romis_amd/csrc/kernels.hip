@@ -956,7 +956,7 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
 #define ROMIS_RIS_WPE 5
 #endif
 #ifndef ROMIS_RIS1_WPE
-#define ROMIS_RIS1_WPE 6
+#define ROMIS_RIS1_WPE 7   // round 4: 7 (72 VGPRs, 20-24 B of spills) beats 6 at C2 by 2.8 % (profiles/r4/r4n)
 #endif
 #define ROMIS_RIS_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_RIS_WPE)))
 #define ROMIS_RIS1_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_RIS1_WPE)))

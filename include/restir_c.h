@@ -491,7 +491,13 @@ restir_status restir_enable_timing(restir_ctx* ctx, int enable);
  * triangles per BVH leaf for the next restir_set_scene (default 2).  "layout.records": restir_render's buffers as
  * per-pixel records [n_t, res_a, res_b] (1) or SoA planes (0, default).  "ris.compact": initial RIS (N = 1, 2) reads
  * a compact light table when the scene allows one -- point lights only, a light grid, one-colour parallelograms --
- * instead of the 7-float4 records (default 1; restir_set_scene detects the form bit for bit). */
+ * instead of the 7-float4 records (default 1; restir_set_scene detects the form bit for bit).  Round 4:
+ * "spatial.xcd_rows|xcd_cols" (the spatial pass's XCD chunk shape; 255 = automatic), "spatial.th" (1: 32x8, 2: 32x16
+ * tiles, 0: by width), "spatial.lds" (3: the n_t window in LDS, 0: gathers), "ris.late" (stage the light table after
+ * the primary rays, only for tiles that need it), "final.miss" (final shading reads only p_mat and (pos, W) for a
+ * primary-ray miss), "miss.tiles" (background-tile flags from RIS to the spatial passes and final shading, N = 1 without
+ * temporal reuse), "miss.gbuf" (0 / 1 / 2 = auto: RIS also skips background tiles' G-buffer stores), "frames.inflight"
+ * (1 / 2 frame slots), "timing.every" / "timing.fence" (event sampling).  All default on where measured faster. */
 restir_status restir_set_tuning(restir_ctx* ctx, const char* key, int value);
 restir_status restir_timings(restir_ctx* ctx, double* ms /*[RESTIR_K_COUNT]*/, uint64_t* launches /*[RESTIR_K_COUNT]*/);
 restir_status restir_reset_timings(restir_ctx* ctx);

@@ -1621,7 +1621,7 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     // DMA before that wave's ds_reads, and a workgroup-scope fence need not drain vmcnt on gfx950, so the wait
     // is explicit (scripts/kernel_isa.sh k_spatial1_ntl: s_waitcnt vmcnt(0) directly before s_barrier).
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (mt.gbuf) {
+    if (mt.m && mt.gbuf) {
         // RIS stored no G-buffer for background tiles: this thread's window entries there (its own LDS-DMA copies,
         // landed after the wait above) become a miss's record, normal 0 and t = FLT_MAX -- what RIS would have stored
         constexpr uint32_t kThreads = 256u * TH, kPer = (apron_max(TH) + kThreads - 1u) / kThreads;
@@ -3192,11 +3192,15 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f
 
 hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const CameraDev& cam, const FeaturesDev& f, uint32_t key,
                               float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,
-                              float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss, uint32_t skip_res) {
+                              float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss, uint32_t skip_res,
+                              bool* tmiss_written) {
+    if (tmiss_written) *tmiss_written = false;
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, tu.primary_2d);
-    // MissTiles flags: one 32 x 8 tile per block, N = 1 (the caller allocates one byte per tile)
+    // MissTiles flags: one 32 x 8 tile per block, N = 1 (the caller allocates one byte per tile and passes them on
+    // only when *tmiss_written)
     if (!rg.map2d || tu.ris_blocks || f.N != 1) tmiss = nullptr;
+    if (tmiss_written) *tmiss_written = tmiss != nullptr;
     const size_t bvh = bvh_lds_bytes(s);
     if (bvh > kLdsBudget) return hipErrorInvalidValue;   // caller checks primary_ris_fits()
     const int lt = ris_light_form(s, f, tu);
@@ -3251,7 +3255,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
                           bool* rp_written, const Tuning& tu, hipStream_t stream, uint8_t* vis_out, bool* vis_written,
                           MissTiles mt) {
     if (rp_written) *rp_written = false;
-    if (!mt.flags) mt.m = 0u;
+    if (!mt.flags) mt.m = mt.gbuf = 0u;
     if (vis_written) *vis_written = false;
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     Region rg = with_map(rg0, tu.spatial_xcd);   // XCD-banded order works on 2D tiles

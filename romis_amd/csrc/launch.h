@@ -18,7 +18,8 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg, const FeaturesDev& f,
 hipError_t launch_primary_ris(const SceneDev& s, const Region& rg, const CameraDev& cam, const FeaturesDev& f, uint32_t key,
                               float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,
                               float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss = nullptr,
-                              uint32_t skip_res = 0u);   // bit 0: background reservoirs, bit 1: background G-buffer
+                              uint32_t skip_res = 0u,    // bit 0: background reservoirs, bit 1: background G-buffer
+                              bool* tmiss_written = nullptr);   // the flags were written (else pass none on)
 bool primary_ris_fits(const SceneDev& s);
 // the N = 1 spatial pass reads background tiles through MissTiles for this scene / features / knobs (SoA planes)
 bool spatial_reads_flags(const SceneDev& s, const FeaturesDev& f, const Tuning& tu);

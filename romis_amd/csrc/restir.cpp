@@ -1360,10 +1360,16 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     const uint32_t mg = c->tuning.miss_gbuf;
     const bool gbuf_ok = mg && final_reads_flags(s, f, c->tuning) &&
                          (f.unbiased ? passes == 1u : (mg == 1u || t.gwidth >= 2048u));
-    const uint32_t skip_mode = skip_res ? (1u | (gbuf_ok ? 2u : 0u)) : 0u;
+    uint32_t skip_mode = skip_res ? (1u | (gbuf_ok ? 2u : 0u)) : 0u;
     if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)
+        bool written = false;
         TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),
-                                                          fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st, tmiss, skip_mode));
+                                                          fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st, tmiss, skip_mode,
+                                                          &written));
+        if (!written) {   // (then RIS skipped nothing either: its skips need the flags)
+            tmiss = nullptr;
+            skip_mode = 0u;
+        }
     } else {
         TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, fb.nt(0), pm, fb.nt2(), c->tuning, st));
         TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, ris_key, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), nullptr,

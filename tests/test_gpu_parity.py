@@ -898,7 +898,9 @@ def test_frames_in_flight_match_serial_frames(gpu, oracle, temporal, passes, N):
     # biased passes with the G-buffer stores skipped too (miss.gbuf = 1; the default does so only from 2048 px wide):
     # the window fix-up, on 32 x 8 and on 32 x 16 tiles
     ("cornell_1024", 1, 0, 0, 0, {"miss.gbuf": 1}), ("cornell_1024", 2, 0, 0, 0, {"miss.gbuf": 1}),
-    ("cornell_1024", 1, 0, 0, 0, {"miss.gbuf": 1, "spatial.th": 2}), ("nightclub_128pt", 1, 0, 0, 0, {"miss.gbuf": 1})])
+    ("cornell_1024", 1, 0, 0, 0, {"miss.gbuf": 1, "spatial.th": 2}), ("nightclub_128pt", 1, 0, 0, 0, {"miss.gbuf": 1}),
+    # a persistent RIS grid writes no flags: restir_render then passes none on (and RIS skips no stores)
+    ("cornell_1024", 1, 0, 0, 0, {"ris.blocks": 64, "miss.gbuf": 1}), ("cornell_4096", 1, 1, 1, 0, {"ris.blocks": 64})])
 def test_miss_tiles_match_full_reads(gpu, name, passes, unbiased, vis, tiled, tune):
     """MissTiles (miss.tiles = 1, the default): RIS flags the 32 x 8 tiles whose pixels all missed the scene, and the
     spatial passes and final shading write those tiles' known results without reading them.  Frames at 640 x 360
@@ -929,6 +931,7 @@ def test_miss_tiles_match_full_reads(gpu, name, passes, unbiased, vis, tiled, tu
         gpu.set_tuning("miss.tiles", 1)
         gpu.set_tuning("miss.gbuf", 2)
         gpu.set_tuning("spatial.th", 0)
+        gpu.set_tuning("ris.blocks", 0)
     assert_bits(on_rgb, off_rgb, f"{name} rgb")
     for a, b in zip(off_grid, on_grid):
         assert np.array_equal(np.asarray(a).view(np.uint32), np.asarray(b).view(np.uint32)), f"{name} grid"

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 4 HEAD check: smoke and the driver's own bench command at the committed sources (traffic / VALU records match).
+set -o pipefail
+REPO=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$REPO" || exit 1
+export TMPDIR=/tmp
+OUT=gpurun_out/r4_head
+mkdir -p $OUT
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 21; }
+cat $OUT/smoke.log
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 22; }
+cat $OUT/bench.json

@@ -1770,13 +1770,34 @@ __device__ __forceinline__ void spatialn_ntl_body(const SceneDev& s, const Regio
                                                   v3 origin, const float4* __restrict__ n_t,
                                                   const float4* __restrict__ p_mat, const float4* __restrict__ ia,
                                                   const float4* __restrict__ ib, float4* __restrict__ oa,
-                                                  float4* __restrict__ ob, float2* __restrict__ odbg) {
+                                                  float4* __restrict__ ob, float2* __restrict__ odbg, MissTiles mt) {
     const GlTabs tb = gl_stage_tables<false>();   // made visible by the window's barrier below
     float4* const l_nt = g_lds;
     uint32_t tile;
     if (!xcd_tile(rg, num_tiles(rg), blockIdx.x, tile)) return;   // block-uniform
     const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
     const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTileH);
+    if (mt.m) {
+        // a tile of background pixels: after RIS and after every biased pass each holds sub-reservoir 0 = (0, W = 0),
+        // (0, M = mt.m) and the others (0, W = 0), (0, M = 0) -- the miss shortcut's result below (M_0 = the sum of
+        // the own Ms), written without reading the tile or its window
+        const int x1 = min(tx0 + (int)kTileW, (int)(rg.rx0 + rg.rw)) - 1, y1 = min(ty0 + (int)kTileH, (int)(rg.ry0 + rg.rh)) - 1;
+        if (tiles_known_miss(mt, rg, tx0, x1, ty0, y1)) {
+            const uint32_t mw = threadIdx.x >> 6, ml = threadIdx.x & 63u;
+            const int mx = tx0 + (int)(mw * 8u + (ml & 7u)), my = ty0 + (int)(ml >> 3);
+            if (mx <= x1 && my <= y1) {
+                const uint32_t mo = ((uint32_t)(my - (int)rg.vy0) * rg.vw + (uint32_t)(mx - (int)rg.vx0)) << 4;
+                const uint32_t jo = rg.js << 4;
+#pragma unroll
+                for (int j = 0; j < NT; j++) {
+                    st_at(oa, mo + (uint32_t)j * jo, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+                    st_at(ob, mo + (uint32_t)j * jo, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(j == 0 ? mt.m : 0u)));
+                    if (DBG) st_at(odbg, (mo + (uint32_t)j * jo) >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
+                }
+            }
+            return;   // block-uniform, before the window's barrier
+        }
+    }
     const int xlo = max(0, (int)rg.vx0), xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1;
     const int ylo = max(0, (int)rg.vy0), yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1;
     const int R = (int)f.R;
@@ -1891,8 +1912,8 @@ __device__ __forceinline__ void spatialn_ntl_body(const SceneDev& s, const Regio
 #define ROMIS_SPATIALN_NTL_KERNEL(DBG, NT, NAME)                                                                      \
     extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL2_NTL_WPE))) void     \
     NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
-         const float4* p_mat, const float4* ia, const float4* ib, float4* oa, float4* ob, float2* odbg) {             \
-        spatialn_ntl_body<DBG, NT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg);                   \
+         const float4* p_mat, const float4* ia, const float4* ib, float4* oa, float4* ob, float2* odbg, MissTiles mt) { \
+        spatialn_ntl_body<DBG, NT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, mt);               \
     }
 ROMIS_SPATIALN_NTL_KERNEL(false, 2, k_spatial2_ntl)
 ROMIS_SPATIALN_NTL_KERNEL(true, 2, k_spatial2_ntl_dbg)
@@ -2191,7 +2212,7 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
                                                   MissTiles mt) {
     // NT shadow rays per pixel (one per sub-reservoir): ray j * 256 + t is pixel t's sub-reservoir j
     constexpr uint32_t kRays = 256u * NT;
-    if (NT == 1 && mt.flags) {
+    if (mt.flags) {
         // a tile of background pixels (MissTiles): after RIS and any biased / unbiased passes each holds W = 0 and the
         // initial (0, 0) sample, which a miss pixel shades to +-0 (kd = ks = 0; a non-finite dotNL or power is cleaned
         // up; the distance |P| is not NaN): the colour is +0 -- tone mapped as below, without reading anything
@@ -2330,8 +2351,8 @@ extern "C" __global__ __launch_bounds__(256) void k_final_n1_sorted(SceneDev s, 
 }
 extern "C" __global__ __launch_bounds__(256) void k_final_n2_sorted(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,
                                                                    float oz, const float4* n_t, const float4* p_mat,
-                                                                   const float4* ra, const float4* rb, float* rgb) {
-    final_sorted_body<true, 2>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, nullptr, MissTiles{nullptr, 0u, 0u});
+                                                                   const float4* ra, const float4* rb, float* rgb, MissTiles mt) {
+    final_sorted_body<true, 2>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, nullptr, mt);
 }
 
 #define ROMIS_FINAL_KERNEL(NT, LDS, NAME)                                                                              \
@@ -3197,9 +3218,9 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
     if (tmiss_written) *tmiss_written = false;
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, tu.primary_2d);
-    // MissTiles flags: one 32 x 8 tile per block, N = 1 (the caller allocates one byte per tile and passes them on
+    // MissTiles flags: one 32 x 8 tile per block, N <= 2 (the caller allocates one byte per tile and passes them on
     // only when *tmiss_written)
-    if (!rg.map2d || tu.ris_blocks || f.N != 1) tmiss = nullptr;
+    if (!rg.map2d || tu.ris_blocks || f.N > 2) tmiss = nullptr;
     if (tmiss_written) *tmiss_written = tmiss != nullptr;
     const size_t bvh = bvh_lds_bytes(s);
     if (bvh > kLdsBudget) return hipErrorInvalidValue;   // caller checks primary_ris_fits()
@@ -3291,7 +3312,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         rg.xcd_cols = tu.spatial_xcd_cols == kXcdColsAuto ? 0u : tu.spatial_xcd_cols;
         if (rg.xcd_rows) grid = xcd_grid(rg, ntx, nty);
         ROMIS_LAUNCH(odbg ? k_spatial2_ntl_dbg : k_spatial2_ntl, dim3(grid), dim3(kBlock), kApronMax * 16u, stream, s, rg, f,
-                     key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg);
+                     key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, mt);
         return hipGetLastError();
     }
     if (lean && !f.unbiased) {
@@ -3370,7 +3391,7 @@ hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev&
                          p_mat, ra, rb, rgb, vis_in, rg.map2d ? mt : MissTiles{nullptr, 0u, 0u});
         else
             ROMIS_LAUNCH(k_final_n2_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, sf, rg, f, o[0], o[1], o[2], n_t,
-                         p_mat, ra, rb, rgb);
+                         p_mat, ra, rb, rgb, rg.map2d ? mt : MissTiles{nullptr, 0u, 0u});
         return hipGetLastError();
     }
     ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.final_blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,

@@ -1338,11 +1338,11 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     // frames in flight: this frame's primary rays and RIS start once the other slot's spatial passes are done
     if (wait_other) HIP_TRY(hipStreamWaitEvent(st, c->pipe.after_spatial[k ^ 1], 0));
     const uint32_t ris_key = restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, 0);
-    // background tiles (MissTiles): N = 1, no temporal reuse (its output is not the RIS result), the fused kernel with
+    // background tiles (MissTiles): N <= 2, no temporal reuse (its output is not the RIS result), the fused kernel with
     // one 32 x 8 tile per block; the spatial shortcuts also need bounded normals (their miss tests)
     uint8_t* tmiss = nullptr;
     const bool fused = c->tuning.fuse_primary_ris && primary_ris_fits(s);
-    if (c->tuning.miss_tiles && fused && N == 1 && !temporal && c->tuning.primary_2d && !c->tuning.ris_blocks &&
+    if (c->tuning.miss_tiles && fused && N <= 2 && !temporal && c->tuning.primary_2d && !c->tuning.ris_blocks &&
         s.normals_bounded && !fb.records) {
         const size_t tiles = (size_t)((t.gwidth + 31u) / 32u) * ((t.gheight + 7u) / 8u);
         ST_TRY(fb.tmiss().ensure(tiles));

@@ -99,9 +99,10 @@ struct Region {
     uint32_t xcd_cols;   // chunk width in tiles (xcd_tile); 0 = the whole row of tiles
 };
 
-// Background tiles (restir_render, N = 1, no temporal reuse): the fused primary + RIS kernel writes one byte per
+// Background tiles (restir_render, N <= 2, no temporal reuse): the fused primary + RIS kernel writes one byte per
 // 32 x 8 tile of its region (the view), 0 when every pixel of the tile is a primary-ray miss whose RIS reservoir is
-// known -- the miss material, P not NaN, finite lights, L != 0: (0, 0, 0, W = 0), (0, 0, 0, M = f.M), pdf 0 -- and
+// known -- the miss material, P not NaN, finite lights, L != 0: (0, 0, 0, W = 0), (0, 0, 0, M = f.M) in sub-reservoir
+// 0 and M = 0 in sub-reservoir 1, pdf 0 -- and
 // 1 otherwise.  The spatial passes and final shading then write such tiles' known results without reading them.
 // m: the M every such pixel holds at the pass's input (0: flags unused by this launch).
 struct MissTiles {

@@ -900,7 +900,10 @@ def test_frames_in_flight_match_serial_frames(gpu, oracle, temporal, passes, N):
     ("cornell_1024", 1, 0, 0, 0, {"miss.gbuf": 1}), ("cornell_1024", 2, 0, 0, 0, {"miss.gbuf": 1}),
     ("cornell_1024", 1, 0, 0, 0, {"miss.gbuf": 1, "spatial.th": 2}), ("nightclub_128pt", 1, 0, 0, 0, {"miss.gbuf": 1}),
     # a persistent RIS grid writes no flags: restir_render then passes none on (and RIS skips no stores)
-    ("cornell_1024", 1, 0, 0, 0, {"ris.blocks": 64, "miss.gbuf": 1}), ("cornell_4096", 1, 1, 1, 0, {"ris.blocks": 64})])
+    ("cornell_1024", 1, 0, 0, 0, {"ris.blocks": 64, "miss.gbuf": 1}), ("cornell_4096", 1, 1, 1, 0, {"ris.blocks": 64}),
+    # N = 2 (the reference default): k_spatial2_ntl and k_final_n2_sorted read the flags too
+    ("cornell_1024", 1, 0, 0, 0, {"N": 2}), ("cornell_1024", 2, 0, 0, 0, {"N": 2}), ("nightclub_128pt", 1, 0, 0, 0, {"N": 2}),
+    ("cornell_1024", 2, 0, 0, 1, {"N": 2}), ("cornell_4096", 1, 1, 1, 0, {"N": 2})])
 def test_miss_tiles_match_full_reads(gpu, name, passes, unbiased, vis, tiled, tune):
     """MissTiles (miss.tiles = 1, the default): RIS flags the 32 x 8 tiles whose pixels all missed the scene, and the
     spatial passes and final shading write those tiles' known results without reading them.  Frames at 640 x 360
@@ -908,11 +911,13 @@ def test_miss_tiles_match_full_reads(gpu, name, passes, unbiased, vis, tiled, tu
     ghost-zoned screen tile (2 x 2 plan, rank 3: the RIS, spatial and final regions start at different offsets), must
     equal the frames rendered with the flags off bit for bit -- RGB and the returned grid."""
     from romis_amd import restir
+    tune = dict(tune)
+    N = tune.pop("N", 1)
     w, h = 640, 360
     s = get_scene(name)
     gpu.set_scene(s)
     cam = scene.camera_for(name, w, h)
-    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=passes, unbiased_combination=unbiased,
+    f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=passes, unbiased_combination=unbiased,
                               temporal_reuse=0, spatial_reuse_visibility_check=vis)
     tile = restir.tile_plan(w, h, 2, 2, 3, passes * f.spatial_resample_radius) if tiled else None
 

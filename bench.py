@@ -429,7 +429,16 @@ def halo_check(torch, r, rank, world, local, cf, f, cam, GW, GH, tx, ty, passes,
     r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
     ghost_tile = restir.tile_plan(GW, GH, tx, ty, rank, passes * args.r)
     rgb_ghost, _ = r.render_restir(None, cam, GW, GH, fc, tile=ghost_tile, want_grid=False)
-    bad = distributed.tile_mismatches(rgb_halo, rgb_ghost)
+    bad = distributed.tile_mismatches(rgb_halo, rgb_ghost)   # summed over ranks: every rank decides alike
+    if bad and transport == "native":
+        # the library's own RCCL transport first runs with two or more GPUs here: its mismatch is recorded and the
+        # protocol checked again over the torch transport, which carries the same pack / unpack kernels
+        rec["native_check"] = f"{bad} mismatching values"
+        rec["transport"] = transport = "torch"
+        hfc = distributed.HaloFrames(r, GW, GH, (tx, ty), rank, fc, transport=transport)
+        r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
+        rgb_halo, _ = hfc.render(None, cam, want_rgb=True, want_grid=False)
+        bad = distributed.tile_mismatches(rgb_halo, rgb_ghost)
     rec["check"] = "bit-exact" if bad == 0 else f"{bad} mismatching values"
     if bad:
         if rank == 0:

@@ -419,6 +419,23 @@ __device__ __forceinline__ GlTabs gl_stage_tables() {
     t.exp2 = s_gl_exp2;
     return t;
 }
+// The same copy by one LDS-DMA instruction of wave 0 (lanes 0-15 the log2 table, 16-31 the exp2 table, 16 B each):
+// no VGPR round trip and no wait of its own -- the register-staged form above waits for its loads right where it is
+// issued, before the block's own loads go out.  The caller's s_waitcnt vmcnt(0) + barrier make it visible.
+__device__ __forceinline__ GlTabs gl_stage_tables_dma() {
+    __shared__ __attribute__((aligned(16))) unsigned long long s_gl_tab[64];
+    if (threadIdx.x < 32u) {
+        const unsigned long long* src = threadIdx.x < 16u
+                                            ? reinterpret_cast<const unsigned long long*>(kGlLog2Tab) + 2u * threadIdx.x
+                                            : kGlExp2Tab + 2u * (threadIdx.x - 16u);
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)s_gl_tab, 16, 0, 0);
+    }
+    GlTabs t;
+    t.log2 = reinterpret_cast<const double*>(s_gl_tab);
+    t.exp2 = s_gl_tab + 32;
+    return t;
+}
 
 // ---------------------------------------------------------------------------------------------------------
 // Reservoir state (reservoir.h:28-73), one sub-reservoir
@@ -703,8 +720,10 @@ template <int NT, int LT = kLtGeneral>
 __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                           const float4* lights, const Bvh& bvh, float4 nt, float4 pm, uint32_t x,
                                           uint32_t y, size_t p, float4* __restrict__ ra, float4* __restrict__ rb,
-                                          float2* __restrict__ rdbg, float* __restrict__ rp, const GlTabs& tb) {
+                                          float2* __restrict__ rdbg, float* __restrict__ rp, const GlTabs& tb,
+                                          float* __restrict__ hw = nullptr, uint32_t* __restrict__ hm = nullptr) {
     const uint32_t L = s.num_lights;
+    uint32_t hidx = L;   // the held sample's light index for the handle planes (k_spatial1h; L = the zero sample)
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
     const float invL = 1.0f / (float)L;
@@ -817,6 +836,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 if (best != 0xFFFFFFFFu) {
                     sample(best, r[0].pos, r[0].col);
                     r[0].has_pd = true;
+                    if (LT == kLtPoint) hidx = uniform_index(draw(ps, 4u * best), L);
                 }
             } else {
                 for (uint32_t c = 0; c < c_end; c++) {
@@ -837,6 +857,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
             rp[p] = target_pdf(s, f, make_px(s, nt, pm, origin, p), r[0].pos, r[0].col, tb);   // no lights: the initial sample
         }
         for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, ridx(rg, j, p), j * npx + p);
+        if (NT == 1 && LT == kLtPoint && hw) { hw[p] = r[0].W; hm[p] = r[0].M | (hidx << 24); }
     }
 }
 
@@ -889,7 +910,7 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
                                                  float4* __restrict__ p_mat, float4* __restrict__ n_t2,
                                                  float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
                                                  float* __restrict__ rp, uint32_t late_ok, uint8_t* __restrict__ tmiss,
-                                                 uint32_t skip_res) {
+                                                 uint32_t skip_res, float* __restrict__ hw, uint32_t* __restrict__ hm) {
     const uint32_t bvh_f4 = 2u * s.num_nodes + 3u * s.num_tris;
     const float4* lights = global_lights<LT>(s);
     const uint32_t items = work_items(rg);
@@ -933,7 +954,7 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         // pdfs are not stored -- the first spatial pass substitutes them from the flag; bit 1 (above), nor its G-buffer
         // records (a single unbiased pass, which substitutes those too)
         if (live && (any || !tmiss || !(skip_res & 1u)))
-            ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb);
+            ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb, hw, hm);
         return;
     }
     for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {
@@ -942,7 +963,7 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         if (!work_pixel(rg, item, x, y, p)) continue;
         float4 nt, pm;
         primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, nt, pm);
-        ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb);
+        ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb, hw, hm);
     }
 }
 
@@ -992,8 +1013,10 @@ ROMIS_RIS_KERNEL_LT(2, false, kLtPgram, k_ris_n2_pg, ROMIS_RIS_ATTR)
     extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, CameraDev cam, FeaturesDev f,   \
                                                           uint32_t key, float4* n_t, float4* p_mat, float4* n_t2,      \
                                                           float4* ra, float4* rb, float2* rdbg, float* rp,             \
-                                                          uint32_t late_ok, uint8_t* tmiss, uint32_t skip_res) {       \
-        primary_ris_body<NT, LDS, LT>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp, late_ok, tmiss, skip_res); \
+                                                          uint32_t late_ok, uint8_t* tmiss, uint32_t skip_res,         \
+                                                          float* hw, uint32_t* hm) {                                   \
+        primary_ris_body<NT, LDS, LT>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp, late_ok, tmiss, skip_res,   \
+                                      hw, hm);                                                                         \
     }
 #define ROMIS_PRIMARY_RIS_KERNEL(NT, LDS, NAME, ATTR) ROMIS_PRIMARY_RIS_KERNEL_LT(NT, LDS, kLtGeneral, NAME, ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(1, true, k_primary_ris_n1_lds, ROMIS_RIS1_ATTR)
@@ -1421,6 +1444,12 @@ __device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& 
     if (rp_out) st_at(rp_out, pofs >> 2, p);
 }
 
+#ifndef ROMIS_TAB_DMA
+#define ROMIS_TAB_DMA 1   // the biased passes stage powf's tables by LDS-DMA behind their own loads (gl_stage_tables_dma)
+#endif
+#ifndef ROMIS_FLAG_SMEM
+#define ROMIS_FLAG_SMEM 1   // a block's single background-tile flag through the scalar cache (tiles_known_miss)
+#endif
 // Tile of block b (XCD b % 8, block b runs on XCD b % 8): XCD x owns every 8th chunk of rg.xcd_rows tile
 // rows (chunks x, x + 8, x + 16, ...), walked row-major, so its L2 holds the chunk's G-buffer and reservoirs
 // while the gathers reach 10 px across tile borders; interleaving short chunks spreads cheap (background)
@@ -1466,6 +1495,15 @@ __device__ __forceinline__ bool tiles_known_miss(const MissTiles& mt, const Regi
     const uint32_t ntxv = (rg.vw + kTileW - 1u) / kTileW;
     const uint32_t cx0 = (uint32_t)(x0 - (int)rg.vx0) / kTileW, cx1 = (uint32_t)(x1 - (int)rg.vx0) / kTileW;
     const uint32_t cy0 = (uint32_t)(y0 - (int)rg.vy0) / kTileH, cy1 = (uint32_t)(y1 - (int)rg.vy0) / kTileH;
+    if (ROMIS_FLAG_SMEM && cx0 == cx1 && cy0 == cy1) {
+        // one RIS tile (the biased pass's 32 x 8 tiles on the RIS grid): its flag's word by a scalar load -- the address
+        // is block-uniform and the flags were written by an earlier kernel (the launcher rounds the buffer to words)
+        const uint32_t c = cy0 * ntxv + cx0;
+        const auto* w = (const __attribute__((address_space(4))) uint32_t*)(mt.flags + (c & ~3u));
+        const uint32_t v = (*w >> (8u * (c & 3u))) & 0xFFu;
+        if (some_known) *some_known = v == 0u;
+        return v == 0u;
+    }
     uint32_t any = 0u, all = 1u;
     for (uint32_t cy = cy0; cy <= cy1; cy++)
         for (uint32_t cx = cx0; cx <= cx1; cx++) {
@@ -1547,7 +1585,9 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
                                                   float4* __restrict__ ob, float2* __restrict__ odbg,
                                                   const float* __restrict__ rp_in, float* __restrict__ rp_out,
                                                   MissTiles mt) {
+#if !ROMIS_TAB_DMA
     const GlTabs tb = gl_stage_tables<false>();   // made visible by the window's barrier below
+#endif
     float4* const l_nt = g_lds;
     uint32_t tile;
     constexpr uint32_t kTH = kTileH * TH;   // tile rows
@@ -1601,6 +1641,9 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
         }
     }
     ntl_stage_window<TH>(rg, n_t, l_nt, ax0, ay0, AW, n_apron);
+#if ROMIS_TAB_DMA
+    const GlTabs tb = gl_stage_tables_dma();   // behind the block's own loads; made visible by the window's barrier
+#endif
     // neighbour draws while the loads are in flight
     const uint32_t K = f.K;   // <= kLeanK (host check)
     const uint32_t ps = pix_state(key, (uint32_t)y * rg.W + (uint32_t)x);
@@ -1723,6 +1766,242 @@ ROMIS_SPATIAL1_NTL_KERNEL(true, k_spatial1_ntl_dbg)
     }
 ROMIS_SPATIAL1_T2_KERNEL(false, k_spatial1_ntl_t2)
 ROMIS_SPATIAL1_T2_KERNEL(true, k_spatial1_ntl_t2_dbg)
+
+// ---------------------------------------------------------------------------------------------------------
+// k_spatial1h[_t2]: the N = 1 biased pass over sample handles (round 5).  In a point-light scene
+// (SceneDev::light_types == points) a reservoir's sample is a light's (position, colour) from the light table, or
+// the initial (0, 0) sample; the producer (k_primary_ris_n1*_pt, or this pass for the next) also writes the handle
+// planes Handles::w = W and Handles::m = M | light index << 24 (index L = the zero sample), 4 + 4 B per pixel.  The
+// block LDS-DMAs both planes over the tile's +-R window beside the n_t window, and the light table (positions, then
+// colours, entry L zero), so an accepted neighbour's input is three ds_reads -- no global gather in the combine, and
+// the pixel's own reservoir is read from the window too.  The arithmetic, RNG slots and update order are
+// spatial1_ntl_body's (render_utils.cpp:102-133, reservoir.cpp:40-66): the same (position, colour, W, M) values, in
+// the same operations.  The host launches it only when every M the passes can produce fits 24 bits and L <= 254.
+struct HandlesIn { const float* w; const uint32_t* m; };
+constexpr uint32_t kHandleM = 0x00FFFFFFu;
+
+// The combine state over handles: Comb1 with the held sample's light index instead of its (position, colour).
+struct Comb1h {
+    float wsum, chosen, pd;
+    uint32_t macc, li;
+    bool has_pd;
+    uint32_t h;
+    __device__ __forceinline__ void take(float pd_in, float W, uint32_t M, uint32_t l) {
+        const float w = (pd_in * W) * (float)M;          // reservoir.cpp:50
+        macc += M;
+        wsum += w;
+        const float u = rand01(mix32(h));
+        h += 0x9E3779B9u;
+        if (u < (w / wsum)) { li = l; chosen = w; pd = pd_in; has_pd = true; }
+    }
+};
+
+// LDS of a handle block: the n_t window, the two handle windows, then the light table (2 (L + 1) float4)
+__host__ __device__ constexpr uint32_t h_lds_f4(uint32_t TH) { return apron_max(TH) + apron_max(TH) / 2u; }
+
+template <uint32_t TH>
+__device__ __forceinline__ void h_stage(const SceneDev& s, const Region& rg, const float4* __restrict__ n_t, HandlesIn hi,
+                                        float4* l_nt, float* l_w, uint32_t* l_m, float4* l_lt, int ax0, int ay0, uint32_t AW,
+                                        uint32_t n_apron) {
+    constexpr uint32_t kThreads = 256u * TH, kPer = (apron_max(TH) + kThreads - 1u) / kThreads;
+    const uint32_t magic = 0xFFFFFFFFu / AW + 1u;
+    const uint32_t w64 = (threadIdx.x >> 6) << 6;
+    const uint32_t base = (uint32_t)(ay0 - (int)rg.vy0) * rg.vw + (uint32_t)(ax0 - (int)rg.vx0);
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+        const uint32_t i = threadIdx.x + kThreads * k;
+        if (i < n_apron) {
+            uint32_t r = __umulhi(i, magic);   // i / AW for i < 2^16
+            if (r * AW > i) r--;
+            const uint32_t o = base + r * rg.vw + (i - r * AW);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(n_t + o),
+                                             (__attribute__((address_space(3))) void*)(l_nt + kThreads * k + w64), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(hi.w + o),
+                                             (__attribute__((address_space(3))) void*)(l_w + kThreads * k + w64), 4, 0, 0);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(hi.m + o),
+                                             (__attribute__((address_space(3))) void*)(l_m + kThreads * k + w64), 4, 0, 0);
+        }
+    }
+    // light table: entries d = 0 .. L positions, L + 1 .. 2L + 1 colours (light_c2 rows 0 and 1); d = L and 2L + 1 are
+    // the zero sample's, stored by two threads
+    const uint32_t L = s.num_lights, nd = 2u * L + 2u;
+    for (uint32_t d0 = 0; d0 < nd; d0 += kThreads) {
+        const uint32_t d = d0 + threadIdx.x;
+        if (d < nd && d != L && d != 2u * L + 1u) {
+            const float4* src = d < L ? s.light_c2 + 2u * d : s.light_c2 + 2u * (d - L - 1u) + 1u;
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(l_lt + d0 + w64), 16, 0, 0);
+        }
+    }
+    if (threadIdx.x < 2u) l_lt[threadIdx.x ? 2u * L + 1u : L] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
+template <bool DBG, uint32_t TH = 1>
+__device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
+                                               v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                               HandlesIn hi, float4* __restrict__ oa, float4* __restrict__ ob,
+                                               float2* __restrict__ odbg, const float* __restrict__ rp_in,
+                                               float* __restrict__ rp_out, float* __restrict__ how,
+                                               uint32_t* __restrict__ hom, MissTiles mt) {
+    constexpr uint32_t kTH = kTileH * TH;
+    float4* const l_nt = g_lds;
+    float* const l_w = reinterpret_cast<float*>(g_lds + apron_max(TH));
+    uint32_t* const l_m = reinterpret_cast<uint32_t*>(l_w + apron_max(TH));
+    float4* const l_lt = g_lds + h_lds_f4(TH);
+    const uint32_t L = s.num_lights;
+    uint32_t tile;
+    const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
+    if (!xcd_tile(rg, ntx * ((rg.rh + kTH - 1) / kTH), blockIdx.x, tile)) return;   // block-uniform
+    const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTH);
+    bool mixed = false;
+    if (mt.m) {   // background tiles: spatial1_ntl_body
+        const int x1 = min(tx0 + (int)kTileW, (int)(rg.rx0 + rg.rw)) - 1, y1 = min(ty0 + (int)kTH, (int)(rg.ry0 + rg.rh)) - 1;
+        if (tiles_known_miss(mt, rg, tx0, x1, ty0, y1, &mixed)) {
+            const uint32_t mw = threadIdx.x >> 6, ml = threadIdx.x & 63u;
+            const int mx = tx0 + (int)((mw & 3u) * 8u + (ml & 7u)), my = ty0 + (int)((mw >> 2) * 8u + (ml >> 3));
+            if (mx <= x1 && my <= y1) {
+                const uint32_t mp = (uint32_t)(my - (int)rg.vy0) * rg.vw + (uint32_t)(mx - (int)rg.vx0);
+                st_at(oa, mp << 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+                st_at(ob, mp << 4, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(mt.m)));
+                if (DBG) st_at(odbg, mp << 3, make_float2(ROMIS_FLT_MIN, 0.0f));
+                if (rp_out) rp_out[mp] = 0.0f;
+                if (how) { how[mp] = 0.0f; hom[mp] = mt.m | (L << 24); }
+            }
+            return;
+        }
+    }
+    const int xlo = max(0, (int)rg.vx0), xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1;
+    const int ylo = max(0, (int)rg.vy0), yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1;
+    const int R = (int)f.R;
+    const int ax0 = max(tx0 - R, xlo), ax1 = min(tx0 + (int)kTileW - 1 + R, xhi);
+    const int ay0 = max(ty0 - R, ylo), ay1 = min(ty0 + (int)kTH - 1 + R, yhi);
+    const uint32_t AW = (uint32_t)(ax1 - ax0 + 1), n_apron = AW * (uint32_t)(ay1 - ay0 + 1);
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    const int x = tx0 + (int)((w & 3u) * 8u + (l & 7u)), y = ty0 + (int)((w >> 2) * 8u + (l >> 3));
+    const bool live = x < (int)(rg.rx0 + rg.rw) && y < (int)(rg.ry0 + rg.rh);
+    const uint32_t pix = (uint32_t)(y - (int)rg.vy0) * rg.vw + (uint32_t)(x - (int)rg.vx0);
+    float4 cpm = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float pd_cached = 0.0f;
+    const bool own_bg = live && mixed && tile_flag_at(mt, rg, x, y) == 0u;   // a background RIS tile: known, unread
+    if (live) {
+        if (own_bg) {
+            cpm = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(s.num_materials - 1u));
+        } else {
+            cpm = p_mat[pix];
+            if (rp_in) pd_cached = rp_in[pix];
+        }
+    }
+    h_stage<TH>(s, rg, n_t, hi, l_nt, l_w, l_m, l_lt, ax0, ay0, AW, n_apron);
+    const GlTabs tb = gl_stage_tables_dma();
+    const uint32_t K = f.K;   // <= kLeanK (host check)
+    const uint32_t ps = pix_state(key, (uint32_t)y * rg.W + (uint32_t)x);
+    const uint32_t span = 2u * f.R + 1u;
+    uint32_t qi[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        qi[n] = 0u;
+        if (n < K) {
+            const int nx = min(max(x - R + (int)__umulhi(draw(ps, 2u * n), span), xlo), xhi);
+            const int ny = min(max(y - R + (int)__umulhi(draw(ps, 2u * n + 1u), span), ylo), yhi);
+            qi[n] = (uint32_t)(ny - ay0) * AW + (uint32_t)(nx - ax0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's DMA before the barrier (spatial1_ntl_body)
+    if (mt.m && mt.gbuf) {   // background G-buffer records: spatial1_ntl_body's window fix-up
+        constexpr uint32_t kThreads = 256u * TH, kPer = (apron_max(TH) + kThreads - 1u) / kThreads;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++) {
+            const uint32_t i = threadIdx.x + kThreads * k;
+            if (i < n_apron) {
+                uint32_t r = __umulhi(i, 0xFFFFFFFFu / AW + 1u);
+                if (r * AW > i) r--;
+                const uint32_t c = i - r * AW;
+                if (tile_flag_at(mt, rg, ax0 + (int)c, ay0 + (int)r) == 0u) l_nt[i] = make_float4(0.0f, 0.0f, 0.0f, ROMIS_FLT_MAX);
+            }
+        }
+    }
+    __syncthreads();
+    if (!live) return;   // no barrier follows
+    const uint32_t own = (uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0);
+    const float4 cn = l_nt[own];
+    const float cw = own_bg ? 0.0f : l_w[own];
+    const uint32_t cm = own_bg ? (mt.m | (L << 24)) : l_m[own];
+    const uint32_t cli = cm >> 24;
+    const v3 cpos = xyz(l_lt[cli]), ccol = xyz(l_lt[L + 1u + cli]);
+    const Px cur = make_px(s, cn, cpm, origin, pix);
+    if (cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z) &&
+        __builtin_isfinite(cw) && __builtin_isfinite(ccol.x + ccol.y + ccol.z)) {
+        st_at(oa, pix << 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+        st_at(ob, pix << 4, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(cm & kHandleM)));
+        if (DBG) st_at(odbg, pix << 3, make_float2(ROMIS_FLT_MIN, 0.0f));
+        if (rp_out) rp_out[pix] = 0.0f;
+        if (how) { how[pix] = 0.0f; hom[pix] = (cm & kHandleM) | (L << 24); }
+        return;
+    }
+    const double rt = rcp_d(cur.t);
+    const bool rt_all = __all(div_fast_ok(cur.t));
+    bool ok[kLeanK];
+    uint32_t qm[kLeanK];
+    float qw[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        ok[n] = false;
+        qm[n] = 0u;
+        qw[n] = 0.0f;
+        if (n < K) {
+            const float4 g = l_nt[qi[n]];
+            qm[n] = l_m[qi[n]];
+            qw[n] = l_w[qi[n]];
+            const float nd = vdot(xyz(g), cur.N);
+            float q = div_by_rcp_d(g.w, rt);
+            if (__builtin_expect(!rt_all, 0)) {
+                if (!div_fast_ok(cur.t)) q = g.w / cur.t;
+            }
+            ok[n] = !(nd < 0.90630778703f) && !(fabsf(1.0f - q) > 0.1f);
+        }
+    }
+    const float pd_cur = rp_in ? pd_cached : target_pdf(s, f, cur, cpos, ccol, tb);
+    Comb1h cmb;
+    cmb.wsum = ROMIS_FLT_MIN; cmb.chosen = 0.0f; cmb.pd = 0.0f; cmb.macc = 0u; cmb.li = L; cmb.has_pd = false;
+    cmb.h = ps + 2u * K * 0x9E3779B9u;
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        if (ok[n]) {
+            const uint32_t li = qm[n] >> 24;
+            cmb.take(target_pdf(s, f, cur, xyz(l_lt[li]), xyz(l_lt[L + 1u + li]), tb), qw[n], qm[n] & kHandleM, li);
+        }
+    }
+    cmb.take(pd_cur, cw, cm & kHandleM, cli);
+    const v3 pos = xyz(l_lt[cmb.li]), col = xyz(l_lt[L + 1u + cmb.li]);
+    float p = cmb.pd;
+    if (!cmb.has_pd) p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, pos, col, tb);
+    const float W = contribution_weight(p, cmb.macc, cmb.wsum);
+    st_at(oa, pix << 4, make_float4(pos.x, pos.y, pos.z, W));
+    st_at(ob, pix << 4, make_float4(col.x, col.y, col.z, __uint_as_float(cmb.macc)));
+    if (DBG) st_at(odbg, pix << 3, make_float2(cmb.wsum, cmb.chosen));
+    if (rp_out) rp_out[pix] = p;
+    if (how) { how[pix] = W; hom[pix] = cmb.macc | (cmb.li << 24); }
+}
+
+#ifndef ROMIS_SPATIAL1H_WPE
+#define ROMIS_SPATIAL1H_WPE 5
+#endif
+#define ROMIS_SPATIAL1H_KERNEL(DBG, TH, NAME)                                                                          \
+    extern "C" __global__ __launch_bounds__(256 * TH)                                                                 \
+    __attribute__((amdgpu_waves_per_eu(TH >= 3 ? 8 : ROMIS_SPATIAL1H_WPE))) void                                      \
+    NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
+         const float4* p_mat, HandlesIn hi, float4* oa, float4* ob, float2* odbg, const float* rp_in, float* rp_out,  \
+         float* how, uint32_t* hom, MissTiles mt) {                                                                   \
+        spatial1h_body<DBG, TH>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, hi, oa, ob, odbg, rp_in, rp_out, how, hom, mt); \
+    }
+ROMIS_SPATIAL1H_KERNEL(false, 1, k_spatial1h)
+ROMIS_SPATIAL1H_KERNEL(true, 1, k_spatial1h_dbg)
+ROMIS_SPATIAL1H_KERNEL(false, 2, k_spatial1h_t2)
+ROMIS_SPATIAL1H_KERNEL(true, 2, k_spatial1h_t2_dbg)
+ROMIS_SPATIAL1H_KERNEL(false, 3, k_spatial1h_t3)
+ROMIS_SPATIAL1H_KERNEL(true, 3, k_spatial1h_t3_dbg)
+ROMIS_SPATIAL1H_KERNEL(false, 4, k_spatial1h_t4)
+ROMIS_SPATIAL1H_KERNEL(true, 4, k_spatial1h_t4_dbg)
 
 // k_spatial2_ntl: the biased pass for N = 2 sub-reservoirs (the reference's default, common.h:105), laid out like
 // k_spatial1_ntl (32x8 tiles in the XCD chunk order, the n_t window in LDS by LDS-DMA, one shared depth
@@ -3214,7 +3493,7 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f
 hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const CameraDev& cam, const FeaturesDev& f, uint32_t key,
                               float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,
                               float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss, uint32_t skip_res,
-                              bool* tmiss_written) {
+                              bool* tmiss_written, Handles h) {
     if (tmiss_written) *tmiss_written = false;
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, tu.primary_2d);
@@ -3238,11 +3517,21 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
                         : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
     ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.ris_blocks), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
                  cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr, tu.ris_late, tmiss,
-                 tmiss ? skip_res : 0u);
+                 tmiss ? skip_res : 0u, lt == kLtPoint && f.N == 1 ? h.w : nullptr, lt == kLtPoint && f.N == 1 ? h.m : nullptr);
     return hipGetLastError();
 }
 
 bool primary_ris_fits(const SceneDev& s) { return bvh_lds_bytes(s) <= kLdsBudget; }
+
+bool spatial_handles_ok(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes) {
+    if (!tu.spatial_handles || passes == 0 || f.N != 1 || f.unbiased || f.K > kLeanK || f.R > kLdsSpatialR) return false;
+    if (!tu.spatial_lean || !tu.spatial_xcd || !tu.spatial_wave8 || tu.spatial_lds != 3u || !tu.ris_compact) return false;
+    if (s.light_types != 1u || s.num_lights == 0 || s.num_lights > 254u) return false;   // point lights; index L = zero
+    // every M: RIS M, then each biased pass sums at most K + 1 inputs
+    uint64_t m = f.M;
+    for (uint32_t p = 0; p < passes && m <= kHandleM; p++) m *= (uint64_t)(f.K + 1u);
+    return m <= kHandleM;
+}
 
 // launch_spatial's N = 1 pass reads background tiles through MissTiles (k_spatial1_ntl / _t2 biased, k_spatial1u[_vis]
 // unbiased) for these features and knobs, SoA planes -- the condition for RIS's skip_res
@@ -3274,7 +3563,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
                           const float4* n_t, const float4* p_mat, const float4* ia, const float4* ib, float4* oa,
                           float4* ob, float2* odbg, const float* rp_in, const float* rp_nb, float* rp_out,
                           bool* rp_written, const Tuning& tu, hipStream_t stream, uint8_t* vis_out, bool* vis_written,
-                          MissTiles mt) {
+                          MissTiles mt, Handles hin, Handles hout) {
     if (rp_written) *rp_written = false;
     if (!mt.flags) mt.m = mt.gbuf = 0u;
     if (vis_written) *vis_written = false;
@@ -3330,7 +3619,31 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         // 32x16 tiles (k_spatial1_ntl_t2) where the auto XCD chunk is at most 2 tile rows (wide images): C4 222 ->
         // 203 us, C2 76.8 -> 79.0 (cfg_kbench, profiles/r3/r3k); spatial.th = 1 / 2 forces either
         const uint32_t th = tu.spatial_th ? tu.spatial_th : (8192u / std::max(rg.rw, 1u) <= 2u ? 2u : 1u);
-        if (tu.spatial_lds == 3u && f.R <= kLdsSpatialR && th == 2u) {
+        if (hin.w && tu.spatial_lds == 3u && f.R <= kLdsSpatialR) {
+            // sample handles (k_spatial1h[_tN]): 32 x 8 TH tiles, TH = spatial.th (auto: 2); the XCD chunks hold
+            // xcd_rows tile rows (the automatic count divided by TH)
+            const uint32_t hth = tu.spatial_th ? tu.spatial_th : 2u;
+            if (hth > 1u) {
+                const uint32_t ntyh = (rg.rh + hth * kTileH - 1) / (hth * kTileH);
+                if (rg.xcd_rows) {
+                    if (tu.spatial_xcd_rows == kXcdRowsAuto) rg.xcd_rows = std::max(1u, rg.xcd_rows / hth);
+                    grid = xcd_grid(rg, ntx, ntyh);
+                } else {
+                    grid = ntx * ntyh;
+                }
+            } else if (tu.spatial_xcd_cols == kXcdColsAuto && rg.xcd_rows && ntx >= 24u) {
+                if (tu.spatial_xcd_rows == kXcdRowsAuto) rg.xcd_rows = 8u;
+                rg.xcd_cols = (ntx + 2u) / 3u;
+                grid = xcd_grid(rg, ntx, nty);
+            }
+            const size_t lds = (size_t)h_lds_f4(hth) * 16u + (size_t)(2u * s.num_lights + 2u) * 16u;
+            const HandlesIn hi{hin.w, hin.m};
+            auto k = hth == 4u ? (odbg ? k_spatial1h_t4_dbg : k_spatial1h_t4)
+                   : hth == 3u ? (odbg ? k_spatial1h_t3_dbg : k_spatial1h_t3)
+                   : hth == 2u ? (odbg ? k_spatial1h_t2_dbg : k_spatial1h_t2) : (odbg ? k_spatial1h_dbg : k_spatial1h);
+            ROMIS_LAUNCH(k, dim3(grid), dim3(hth * kBlock), lds, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, hi, oa,
+                         ob, odbg, rp_in, rp_out, hout.w, hout.m, mt);
+        } else if (tu.spatial_lds == 3u && f.R <= kLdsSpatialR && th >= 2u) {
             // 32x16 tiles: the chunks hold half as many (twice as tall) tile rows
             const uint32_t nty2 = (rg.rh + 2u * kTileH - 1) / (2u * kTileH);
             if (rg.xcd_rows) {

@@ -220,6 +220,7 @@ struct restir_ctx {
     DevBuf rp[2];                                   // their target-pdf cache planes (N = 1, planes layout)
     DevBuf vis;                                     // unbiased + visibility pass -> final shading: own-pixel ray
     DevBuf tmiss;                                   // RIS -> spatial passes / final shading: background tiles (MissTiles)
+    DevBuf hnd[2];                                  // sample handles of rec[i] (N = 1 point lights, k_spatial1h)
     int cur = 0;
     uint32_t rgb_w = 0, rgb_h = 0;
     // Frames in flight (tuning frames.inflight = 2): restir_render alternates two frame slots -- slot 0 is the buffers
@@ -229,7 +230,7 @@ struct restir_ctx {
     // spatial pass never shares the GPU with another kernel (its timed duration stays the pass alone).
     struct Slot1 {
         hipStream_t stream = nullptr;
-        DevBuf n_t, p_mat, rec[2], rp[2], rgb, uv, vis, tmiss;
+        DevBuf n_t, p_mat, rec[2], rp[2], rgb, uv, vis, tmiss, hnd[2];
     } slot1;
     struct {
         hipEvent_t after_spatial[2] = {nullptr, nullptr}, after_final[2] = {nullptr, nullptr}, joined = nullptr;
@@ -718,6 +719,12 @@ struct FrameBufs {
     DevBuf& uv() const { return slot ? c->slot1.uv : c->uv; }
     DevBuf& vis() const { return slot ? c->slot1.vis : c->vis; }
     DevBuf& tmiss() const { return slot ? c->slot1.tmiss : c->tmiss; }
+    DevBuf* hnd_() const { return slot ? c->slot1.hnd : c->hnd; }
+    // the sample-handle planes of rec[i]: W then M | index << 24, one 4-byte plane each (ensure_handles)
+    Handles h(int i) const {
+        float* w = hnd_()[i].as<float>();
+        return w ? Handles{w, reinterpret_cast<uint32_t*>(w + npx)} : Handles{nullptr, nullptr};
+    }
     float4* nt(int i) const { return records ? rec_()[i].as<float4>() : n_t_().as<float4>(); }
     float4* ra(int i) const { return rec_()[i].as<float4>() + (records ? 1 : 0); }
     float4* rb(int i) const { return rec_()[i].as<float4>() + (records ? 2 : npx * N); }
@@ -828,7 +835,7 @@ void restir_destroy(restir_ctx* c) {
         if (c->slot1.stream) (void)hipStreamSynchronize(c->slot1.stream);
         for (DevBuf* b : {&c->slot1.n_t, &c->slot1.p_mat, &c->slot1.rec[0], &c->slot1.rec[1], &c->slot1.rp[0],
                           &c->slot1.rp[1], &c->slot1.rgb, &c->slot1.uv, &c->slot1.vis, &c->vis,
-                          &c->slot1.tmiss, &c->tmiss})
+                          &c->slot1.tmiss, &c->tmiss, &c->hnd[0], &c->hnd[1], &c->slot1.hnd[0], &c->slot1.hnd[1]})
             b->release();
         for (hipEvent_t* e : {&c->pipe.after_spatial[0], &c->pipe.after_spatial[1], &c->pipe.after_final[0],
                               &c->pipe.after_final[1], &c->pipe.joined})
@@ -1345,7 +1352,7 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     if (c->tuning.miss_tiles && fused && N <= 2 && !temporal && c->tuning.primary_2d && !c->tuning.ris_blocks &&
         s.normals_bounded && !fb.records) {
         const size_t tiles = (size_t)((t.gwidth + 31u) / 32u) * ((t.gheight + 7u) / 8u);
-        ST_TRY(fb.tmiss().ensure(tiles));
+        ST_TRY(fb.tmiss().ensure((tiles + 3u) & ~(size_t)3u));   // whole words: the spatial pass reads its flag's word
         tmiss = fb.tmiss().as<uint8_t>();
     }
     // the first spatial pass substitutes a background tile's known reservoirs (k_spatial1_ntl / _t2, k_spatial1u); the
@@ -1361,11 +1368,17 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     const bool gbuf_ok = mg && final_reads_flags(s, f, c->tuning) &&
                          (f.unbiased ? passes == 1u : (mg == 1u || t.gwidth >= 2048u));
     uint32_t skip_mode = skip_res ? (1u | (gbuf_ok ? 2u : 0u)) : 0u;
+    // sample handles (k_spatial1h): N = 1 biased passes over a point-light scene, written by the fused RIS kernel and by
+    // every pass but the last; 4 + 4 B per pixel and 16 B of slack (the planes are read a word at a time)
+    const bool handles = fused && !temporal && !fb.records && spatial_handles_ok(s, f, c->tuning, passes) &&
+                         (size_t)t.gwidth * t.gheight * 16u <= 0xFFFFFFFFull;
+    if (handles)
+        for (int i = 0; i < 2; i++) ST_TRY(fb.hnd_()[i].ensure((size_t)t.gwidth * t.gheight * 8u + 16u));
     if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)
         bool written = false;
         TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),
                                                           fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st, tmiss, skip_mode,
-                                                          &written));
+                                                          &written, handles ? fb.h(cur) : Handles{nullptr, nullptr}));
         if (!written) {   // (then RIS skipped nothing either: its skips need the flags)
             tmiss = nullptr;
             skip_mode = 0u;
@@ -1408,7 +1421,9 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                              pass + 1 == passes ? vis : nullptr, &vis_ok,
                              // a background pixel holds M = f.M after RIS and after every biased pass; an unbiased pass
                              // sums its neighbours' M, which only pass 0 knows
-                             MissTiles{tmiss, (!f.unbiased || pass == 0) ? f.M : 0u, (skip_mode & 2u) ? 1u : 0u}));
+                             MissTiles{tmiss, (!f.unbiased || pass == 0) ? f.M : 0u, (skip_mode & 2u) ? 1u : 0u},
+                             handles ? fb.h(cur) : Handles{nullptr, nullptr},
+                             handles && pass + 1 < passes ? fb.h(nxt) : Handles{nullptr, nullptr}));
         cur = nxt;
     }
     if (pipe) HIP_TRY(hipEventRecord(c->pipe.after_spatial[k], st));
@@ -2371,7 +2386,8 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     }
     else if (!std::strcmp(key, "spatial.wave8")) t.spatial_wave8 = v;
     else if (!std::strcmp(key, "spatial.lean")) t.spatial_lean = v;
-    else if (!std::strcmp(key, "spatial.th")) { if (v > 2) return fail(RESTIR_ERR_INVALID, "spatial.th: 0 (auto), 1 or 2"); t.spatial_th = v; }
+    else if (!std::strcmp(key, "spatial.th")) { if (v > 4) return fail(RESTIR_ERR_INVALID, "spatial.th: 0 (auto), 1 .. 4"); t.spatial_th = v; }
+    else if (!std::strcmp(key, "spatial.handles")) t.spatial_handles = v;
     else if (!std::strcmp(key, "fuse.primary_ris")) t.fuse_primary_ris = v;
     else if (!std::strcmp(key, "frames.inflight")) {
         if (v < 1u || v > 2u) return fail(RESTIR_ERR_INVALID, "frames.inflight: 1 or 2");

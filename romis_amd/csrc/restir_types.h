@@ -111,6 +111,13 @@ struct MissTiles {
     uint32_t gbuf;   // 1: RIS did not store background tiles' G-buffer records either (a biased pass fixes its window up)
 };
 
+// Sample handles (N = 1, point-light scenes, kernels.hip k_spatial1h): per view pixel the held sample's W (w) and
+// M | light index << 24 (m; index L = the initial zero sample), written beside the reservoir planes by the producer.
+struct Handles {
+    float* w;
+    uint32_t* m;
+};
+
 // Launch-shape knobs (restir_set_tuning); they never change results, only speed.
 constexpr uint32_t kXcdRowsAuto = 255u;
 constexpr uint32_t kXcdColsAuto = 255u;
@@ -144,6 +151,7 @@ struct Tuning {
     uint32_t fuse_primary_ris = 1; // restir_render: k_primary_ris instead of k_primary + k_ris when the BVH fits LDS
     uint32_t spatial_lean = 1;     // N = 1 biased passes through k_spatial1 (0: the general kernel)
     uint32_t spatial_th = 0;       // N = 1 biased ntl pass: tile height in 8-row units (1: 32x8, 2: 32x16 k_spatial1_ntl_t2; 0: by width)
+    uint32_t spatial_handles = 1;  // restir_render, N = 1 biased, point lights: the passes read sample handles (k_spatial1h)
     uint32_t timing_mask = 0xFFFFFFFFu;   // kernels (bit = RESTIR_K_*) bracketed by HIP events when timing is on
     uint32_t inflight = 1;         // restir_render frame slots: 2 overlaps frame f's final shading with frame f + 1's
                                    // primary rays + RIS (restir_ctx::Slot1; every spatial pass still runs alone)

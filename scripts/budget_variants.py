@@ -101,10 +101,23 @@ VARIANTS = {
                       "v3 R = vsub(vscale(px.N, 2.0f * r.dotNL), L);")],
     "risg_no_len": [(r"return vlength\(shade_ref\(s, f, px, lpos, lcol, tb\)\);",
                      "const v3 sh_ = shade_ref(s, f, px, lpos, lcol, tb); return sh_.x + sh_.y + sh_.z;")],
+    # round 5: every block reads the SAME tile's records and window (the image's middle tile: geometry, L2-resident after
+    # the first blocks) and stores to its own tile -- the pass's compute with its load phase reduced to L2 hits.  If this
+    # runs far below the shipped time, the pass's time is load phase + compute in series, not either alone.
+    "l2res": [(r"    const int tx0 = \(int\)\(rg\.rx0 \+ \(tile % ntx\) \* kTileW\), ty0 = \(int\)\(rg\.ry0 \+ \(tile / ntx\) \* kTH\);",
+               "    const int stx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), sty0 = (int)(rg.ry0 + (tile / ntx) * kTH);\n"
+               "    const uint32_t ftile = ((rg.rh + kTH - 1) / kTH) / 2u * ntx + ntx / 2u;\n"
+               "    const int tx0 = (int)(rg.rx0 + (ftile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (ftile / ntx) * kTH);"),
+              (r"(    const uint32_t pofs = \(\(uint32_t\)\(y - \(int\)rg\.vy0\) \* rg\.vw \+ \(uint32_t\)\(x - \(int\)rg\.vx0\)\) << 4;)",
+               "\\1\n    const uint32_t pofs_s = pofs + ((((uint32_t)(sty0 - ty0)) * rg.vw + (uint32_t)(stx0 - tx0)) << 4);"),
+              (r"st_at\((oa|ob|odbg|rp_out), pofs", r"st_at(\1, pofs_s")],
     # the whole combine (takes) -> sums
     "no_take": [(r"cmb\.take\(target_pdf(?:_lean)?\(s, f, cur, p, c, tb\), na\[n\]\.w, __float_as_uint\(nb\[n\]\.w\), p, c\);",
                  "cmb.wsum += target_pdf(s, f, cur, p, c, tb) * na[n].w; cmb.macc += __float_as_uint(nb[n].w);")],
 }
+
+VARIANTS["l2res_no_phat"] = VARIANTS["l2res"] + VARIANTS["no_phat"]
+VARIANTS["l2res_no_gather"] = VARIANTS["l2res"] + VARIANTS["no_gather"]
 
 
 def main():

@@ -21,11 +21,16 @@ import numpy as np  # noqa: E402
 from romis_amd import _abi, restir, scene  # noqa: E402
 
 DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 1, "ris.queue": 0, "ris.compact": 1,
-            "ris.late": 1, "miss.tiles": 1, "miss.gbuf": 2, "spatial.xcd": 1, "spatial.xcd_rows": 255, "spatial.xcd_cols": 255, "spatial.lds": 3, "spatial.blocks": 0, "spatial.wave8": 1, "spatial.lean": 1, "spatial.th": 0, "fuse.primary_ris": 1, "bvh.max_leaf": 2, "final.blocks": 0, "final.lds": 1, "final.2d": 1,
+            "ris.late": 1, "miss.tiles": 1, "miss.gbuf": 2, "spatial.xcd": 1, "spatial.xcd_rows": 255, "spatial.xcd_cols": 255, "spatial.lds": 3, "spatial.blocks": 0, "spatial.wave8": 1, "spatial.lean": 1, "spatial.th": 0, "spatial.handles": 1, "fuse.primary_ris": 1, "bvh.max_leaf": 2, "final.blocks": 0, "final.lds": 1, "final.2d": 1,
             "final.sort": 1, "final.miss": 1, "layout.records": 0}
 
 VARIANTS = {
     "default": {},
+    "handles_off": {"spatial.handles": 0},
+    "handles_t1": {"spatial.th": 1},
+    "handles_t3": {"spatial.th": 3},
+    "handles_t4": {"spatial.th": 4},
+    "ntl_t2": {"spatial.handles": 0, "spatial.th": 2},
     "feat_no_tonemap": {"@enable_tone_mapping": 0},
     "primary_1d_global": {"primary.2d": 0, "primary.lds": 0},
     "primary_1d_lds": {"primary.2d": 0},

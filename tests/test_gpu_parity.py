@@ -417,6 +417,30 @@ def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased, M, 
     assert_grid(grid, res, name)
 
 
+@pytest.mark.parametrize("th", [1, 2, 3, 4])
+@pytest.mark.parametrize("w,h,passes,M", [(96, 64, 1, 32), (37, 23, 2, 32), (130, 70, 2, 1), (64, 1, 1, 16)])
+def test_spatial_handles_frames_match_oracle(gpu, oracle, th, w, h, passes, M):
+    """The biased passes over sample handles (k_spatial1h[_tN], round 5: W and M | light index planes staged in LDS
+    beside the n_t window, point lights) at every tile height, ragged sizes, 1 and 2 passes: RGB and the returned grid
+    bit-exact with the oracle (render_utils.cpp:87-140, reservoir.cpp:40-66)."""
+    name = "nightclub_128pt"
+    s = get_scene(name)
+    gpu.set_scene(s)
+    osc = oracle.OracleScene(s)
+    cam = scene.camera_for(name, w, h)
+    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=passes, temporal_reuse=0,
+                              initial_light_samples=M)
+    gpu.set_tuning("spatial.th", th)
+    try:
+        gpu.set_seed(SEED, 0)
+        rgb, grid = gpu.render_restir(None, cam, w, h, f)
+    finally:
+        gpu.set_tuning("spatial.th", 0)
+    want, res, _ = oracle.render_frame(osc, cam, f, w, h, SEED, 0)
+    assert_bits(rgb, want, f"th={th} {w}x{h} passes={passes}")
+    assert_grid(grid, res, f"th={th} {w}x{h} passes={passes}")
+
+
 @pytest.mark.parametrize("w,h,N,passes,M", [(1, 1, 1, 2, 32), (37, 23, 2, 2, 32), (33, 9, 1, 1, 1), (40, 24, 32, 1, 8),
                                           (64, 1, 3, 2, 16), (1, 50, 1, 1, 32)])
 def test_odd_sizes_and_extremes_match_oracle(gpu, oracle, w, h, N, passes, M):

@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)   # ~0.1 s timed at C2: past the first frames after the idle sync (slower clocks; 50 steps read 2 % low, profiles/r3/r3q)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c4f", "c5f"],
                     help="BASELINE.json config (c2 = configs[1], the headline)")
     ap.add_argument("--scene", default=None, help="override the config's scene")
     ap.add_argument("--mode", default="auto", choices=["auto", "ghost", "halo"],
@@ -144,7 +144,7 @@ def gemm_prewarm(torch, local, ms):
     t0 = time.perf_counter()
     while (time.perf_counter() - t0) * 1e3 < ms:
         for _ in range(4):
-            a = torch.mm(a, b) * 1e-3
+            a = torch.mm(a, b) * (1.0 / 64.0)   # 1/sqrt(4096): the entries keep their magnitude (no decay to zeros)
         torch.cuda.synchronize(dev)
     del a, b
 
@@ -158,7 +158,7 @@ def committed_traffic(cfg):
         from romis_amd import build
         with open(path) as fh:
             rec = json.load(fh)
-        keys = ("scene", "tile", "M", "N", "k", "r", "passes")
+        keys = ("scene", "tile", "M", "N", "k", "r", "passes", "camera")
         here = build.source_hash()
         # the top-level record (scripts/collect_profiles.py: the headline's --pmc passes), then the per-config
         # entries of the attribution study (scripts/traffic_json.py), each only at these exact kernel sources;
@@ -380,6 +380,15 @@ CONFIGS = {
     "c5": dict(scene="cornell_4096", image=(7680, 4320), M=64, passes=1, temporal=0, unbiased=1, vis=1,
                workload="C5: 8K Cornell box, 64x64 = 4096 ceiling parallelogram lights, M=64, k=5 x1 unbiased "
                         "+ spatial visibility reuse"),
+    # C4 / C5 with the camera looking into the box (scene.CORNELL_FRAMED): the TOML camera's frame is 87 % background,
+    # whose tiles the passes write without reading (MissTiles), so c4 / c5 do not measure the 4K / 8K pass on geometry
+    # -- these do (99.9 % of the pixels hit the box).  Same scenes, lights, M, k, passes and combine.
+    "c4f": dict(scene="cornell_1024", image=(3840, 2160), M=32, passes=1, temporal=0, unbiased=0, vis=0, camera="framed",
+                workload="C4 framed: 4K Cornell box, 32x32 = 1024 ceiling parallelogram lights, M=32, k=5 x1 biased, "
+                         "camera looking into the box (99.9 % geometry)"),
+    "c5f": dict(scene="cornell_4096", image=(7680, 4320), M=64, passes=1, temporal=0, unbiased=1, vis=1, camera="framed",
+                workload="C5 framed: 8K Cornell box, 64x64 = 4096 ceiling parallelogram lights, M=64, k=5 x1 unbiased "
+                         "+ spatial visibility reuse, camera looking into the box (99.9 % geometry)"),
 }
 
 
@@ -401,45 +410,71 @@ def spatial_px_per_launch(tile, passes, r):
     return tot / max(1, passes)
 
 
-def halo_check(torch, r, rank, world, local, cf, f, cam, GW, GH, tx, ty, passes, args, transport):
-    """N > 1: this rank's tile rendered through the reservoir halo exchange (HaloFrames: interior launched while
-    the border reservoirs move, border strips after) must equal, bit for bit, the same tile rendered with a ghost
-    zone (restir_render on tile + passes * r) -- exits 3 on any mismatch.  Then the halo-mode frame and the
-    exchange alone are timed.  Temporal reuse is off in the check (one frame from no predecessor), as in c2."""
-    import numpy as np
+def select_halo(torch, world, local, backend, transport, make, check):
+    """The halo transport the run times, chosen once and verified: make(transport) builds the HaloFrames
+    (it may raise RestirError: no RCCL, a failed attach), check(hf) counts the words where its tile differs from the
+    ghost-zone tile, summed over ranks (every rank sees the same count).  A construction failure on any rank moves
+    every rank to the torch transport together; a mismatch over the native transport (first run with two or more GPUs
+    on the driver's node) is recorded as native_check and the protocol re-checked over the torch transport, which
+    carries the same pack / unpack kernels.  Returns (hf, rec, mismatches): hf is the instance the caller must time --
+    rec["transport"] is always hf.transport -- and mismatches != 0 means even the fallback failed (exit 3)."""
+    from romis_amd import _abi
+    rec = {"transport": transport}
+    hf = None
+    try:
+        hf = make(transport)
+    except _abi.RestirError as e:
+        rec["native_error"] = str(e)[:200]
+    dev = torch.device("cuda", local) if backend == "nccl" else "cpu"
+    failed = torch.tensor([1 if hf is None else 0], dtype=torch.int32, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(failed, op=torch.distributed.ReduceOp.MAX)
+    if int(failed.item()) and transport != "torch":   # every rank falls back together
+        transport = "torch"
+        hf = make(transport)
+    bad = check(hf)
+    if bad and transport == "native":
+        rec["native_check"] = f"{bad} mismatching values"
+        transport = "torch"
+        hf = make(transport)
+        bad = check(hf)
+    rec["transport"] = hf.transport
+    return hf, rec, bad
+
+
+def halo_frames(torch, r, rank, world, local, f, cam, GW, GH, tx, ty, passes, args, transport, check_on):
+    """N > 1 with spatial passes: this rank's tile rendered through the reservoir halo exchange (HaloFrames: interior
+    launched while the border reservoirs move, border strips after) must equal, bit for bit, the same tile rendered
+    with a ghost zone (restir_render on tile + passes * r) -- exits 3 on any mismatch (check_on).  Then the halo-mode
+    frame and the exchange alone are timed.  Temporal reuse is off in the check (one frame from no predecessor).
+    Returns (hf, rec): the verified HaloFrames -- the halo-mode main loop (c4 / c5, --mode halo) times this instance,
+    so the run never times a transport other than the one it checked -- and the JSON record."""
     from romis_amd import _abi, distributed, restir
     fc = _abi.Features.from_buffer_copy(f)
     fc.temporal_reuse = 0
-    rec = {"transport": transport}
-    rgb_halo = None
-    try:
-        hfc = distributed.HaloFrames(r, GW, GH, (tx, ty), rank, fc, transport=transport)
+    ghost = {}
+
+    def make(tr):
+        return distributed.HaloFrames(r, GW, GH, (tx, ty), rank, f, transport=tr)
+
+    def check(hf):
+        if not check_on:
+            return 0
+        if "rgb" not in ghost:
+            r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
+            ghost_tile = restir.tile_plan(GW, GH, tx, ty, rank, passes * args.r)
+            ghost["rgb"], _ = r.render_restir(None, cam, GW, GH, fc, tile=ghost_tile, want_grid=False)
         r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
-        rgb_halo, _ = hfc.render(None, cam, want_rgb=True, want_grid=False)
-    except _abi.RestirError as e:    # RCCL unavailable: the torch transport carries the same protocol
-        rec["native_error"] = str(e)[:200]
-    failed = torch.tensor([1 if rgb_halo is None else 0], dtype=torch.int32,
-                          device=torch.device("cuda", local) if args.dist_backend == "nccl" else "cpu")
-    torch.distributed.all_reduce(failed, op=torch.distributed.ReduceOp.MAX)
-    if int(failed.item()):           # every rank falls back together
-        rec["transport"] = transport = "torch"
-        hfc = distributed.HaloFrames(r, GW, GH, (tx, ty), rank, fc, transport=transport)
-        r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
-        rgb_halo, _ = hfc.render(None, cam, want_rgb=True, want_grid=False)
-    r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
-    ghost_tile = restir.tile_plan(GW, GH, tx, ty, rank, passes * args.r)
-    rgb_ghost, _ = r.render_restir(None, cam, GW, GH, fc, tile=ghost_tile, want_grid=False)
-    bad = distributed.tile_mismatches(rgb_halo, rgb_ghost)   # summed over ranks: every rank decides alike
-    if bad and transport == "native":
-        # the library's own RCCL transport first runs with two or more GPUs here: its mismatch is recorded and the
-        # protocol checked again over the torch transport, which carries the same pack / unpack kernels
-        rec["native_check"] = f"{bad} mismatching values"
-        rec["transport"] = transport = "torch"
-        hfc = distributed.HaloFrames(r, GW, GH, (tx, ty), rank, fc, transport=transport)
-        r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
-        rgb_halo, _ = hfc.render(None, cam, want_rgb=True, want_grid=False)
-        bad = distributed.tile_mismatches(rgb_halo, rgb_ghost)
-    rec["check"] = "bit-exact" if bad == 0 else f"{bad} mismatching values"
+        f0 = hf.f
+        hf.f = fc
+        try:
+            rgb, _ = hf.render(None, cam, want_rgb=True, want_grid=False)
+        finally:
+            hf.f = f0
+        return distributed.tile_mismatches(rgb, ghost["rgb"])   # summed over ranks: every rank decides alike
+
+    hf, rec, bad = select_halo(torch, world, local, args.dist_backend, transport, make, check)
+    rec["check"] = ("bit-exact" if bad == 0 else f"{bad} mismatching values") if check_on else "off"
     if bad:
         if rank == 0:
             print(json.dumps({"error": "halo tile differs from the ghost-zone tile", "halo": rec}), flush=True)
@@ -448,21 +483,21 @@ def halo_check(torch, r, rank, world, local, cf, f, cam, GW, GH, tx, ty, passes,
     # halo-mode frames, timed like the main loop (max over ranks)
     k = max(5, min(args.steps, 20))
     for _ in range(2):
-        hfc.render(None, cam, want_rgb=False, want_grid=False)
+        hf.render(None, cam, want_rgb=False, want_grid=False)
     barrier_sync(torch, world, r)
     t0 = time.perf_counter()
     for _ in range(k):
-        hfc.render(None, cam, want_rgb=False, want_grid=False)
+        hf.render(None, cam, want_rgb=False, want_grid=False)
     barrier_sync(torch, world, r)
     dt = max_over_ranks(torch, world, time.perf_counter() - t0, local) / k
-    bytes_pp = max_over_ranks(torch, world, float(sum(s.bytes for s in hfc.send)), local)
+    bytes_pp = max_over_ranks(torch, world, float(sum(s.bytes for s in hf.send)), local)
     rec.update({"frame_ms": round(dt * 1e3, 4), "value": round(GW * GH * f.num_samples_in_reservoir / dt / 1e6, 3),
                 "bytes_per_pass": int(bytes_pp), "passes": passes,
-                "exchange_us_per_pass": round(distributed.exchange_probe(hfc.send, hfc.recv), 2),
+                "exchange_us_per_pass": round(distributed.exchange_probe(hf.send, hf.recv), 2),
                 "note": "value/frame_ms: the same frames with the reservoir halo exchanged over the process group "
                         "before each spatial pass instead of a ghost zone; exchange_us_per_pass: the pass's "
                         "segments moved alone (torch p2p, max over ranks), which the pass overlaps with its interior"})
-    return rec
+    return hf, rec
 
 
 def main():
@@ -486,7 +521,7 @@ def main():
     # scaling c2 recomputes a ghost zone instead (no data-path communication)
     halo = world > 1 and (args.mode == "halo" or (args.mode == "auto" and (cf["temporal"] or scaling == "strong")))
     sc = scene.bench_scene(cf["scene"])
-    cam = scene.camera_for(cf["scene"], GW, GH)
+    cam = scene.camera_for(cf["scene"], GW, GH, cf.get("camera"))
     passes = cf["passes"]
     f = _abi.default_features(initial_light_samples=cf["M"], num_samples_in_reservoir=args.N,
                               num_neighbours_to_sample=args.k, spatial_resample_radius=args.r,
@@ -507,14 +542,17 @@ def main():
     if transport == "auto":
         transport = "native" if args.dist_backend == "nccl" else "torch"
     hf = None
-    if halo:
-        from romis_amd import distributed
-        hf = distributed.HaloFrames(r, GW, GH, (tx, ty), rank, f, transport=transport)
-        tile = hf.tile
     halo_rec = None
-    if world > 1 and passes > 0 and args.halo_check != "off":
-        halo_rec = halo_check(torch, r, rank, world, local, cf, f, cam, GW, GH, tx, ty, passes, args, transport)
+    check_on = world > 1 and passes > 0 and args.halo_check != "off"
+    if halo or check_on:
+        # one HaloFrames per run, chosen and verified by halo_frames (select_halo); the halo-mode loop times it
+        hf_checked, halo_rec = halo_frames(torch, r, rank, world, local, f, cam, GW, GH, tx, ty, passes, args, transport,
+                                           check_on)
         r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
+        if halo:
+            hf = hf_checked
+            tile = hf.tile
+            halo_rec["timed"] = True   # the main loop's frames are this transport's
 
     def step():
         if hf is not None:   # RCCL halo exchange of the reservoirs before every spatial pass
@@ -574,6 +612,8 @@ def main():
            "tiles": [tx, ty], "M": cf["M"], "N": args.N, "k": args.k, "r": args.r, "passes": passes,
            "temporal": cf["temporal"], "unbiased": cf["unbiased"], "spatial_visibility": cf["vis"],
            "parallelism": f"screen tiles {tx}x{ty}, " + (f"RCCL reservoir halo {args.r}px" if halo else f"ghost {ghost}px")}
+    if cf.get("camera") == "framed":
+        cfg["camera"] = dict(scene.CORNELL_FRAMED, kind="framed (scene.CORNELL_FRAMED)")
 
     # roofline of the spatial pass: algorithmic bytes per pixel = read 32 (own G-buffer) + 32 N (own
     # reservoir), write 32 N; neighbour gathers are cache traffic, not counted
@@ -601,7 +641,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         rows = args.cpu_rows or min(GH, max(8, 1036800 // GW))   # ~1 Mpx of the workload, ~0.3 s on 16 cores
-        cpu = cpu_baseline(sc, lambda w, h: scene.camera_for(cf["scene"], w, h), f, rows, GW, GH)
+        cpu = cpu_baseline(sc, lambda w, h: scene.camera_for(cf["scene"], w, h, cf.get("camera")), f, rows, GW, GH)
         if args.cpu_stages:
             def feats(c):   # the config's frame at N, k, r of this run
                 return _abi.default_features(initial_light_samples=c["M"], num_samples_in_reservoir=args.N,

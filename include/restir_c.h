@@ -426,7 +426,8 @@ restir_status restir_halo_ops(uint32_t global_width, uint32_t global_height, uin
  * event, then on the context stream the interior launch, the wait for `moved`, the unpack and the border launches
  * -- and otherwise runs the pass with a zeroed receive buffer (the border strips then read zero reservoirs: not a
  * valid image).  restir_halo_log copies the log out in issue order and clears it; *count: in = capacity, out =
- * entries (RESTIR_ERR_INVALID, nothing cleared, when the capacity is short: *count = entries needed). */
+ * entries (RESTIR_ERR_INVALID, nothing cleared, when the capacity is short: *count = entries needed).  Attaching a
+ * communicator (restir_halo_attach_rccl / _attach_comm) ends record-only mode. */
 #define RESTIR_HALO_EV_PACK         0u
 #define RESTIR_HALO_EV_RECORD       1u   /* peer: 0 = `packed`, 1 = `moved` */
 #define RESTIR_HALO_EV_WAIT         2u   /* peer: the event waited for, as above */

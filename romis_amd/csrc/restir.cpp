@@ -2168,6 +2168,8 @@ static restir_status attach_comm_locked(restir_ctx* c, void* comm, bool owned) {
     RCCL_TRY(rccl_api().comm_user_rank(static_cast<ncclComm_t>(comm), &r));
     q.nranks = n;
     q.rank = r;
+    c->halo_record = false;   // a communicator ends record-only mode: its passes move real reservoirs
+    c->halo_log.clear();
     return RESTIR_OK;
 }
 

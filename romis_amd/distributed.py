@@ -48,6 +48,9 @@ class HaloFrames:
             # (zeroed receive buffers) -- the plumbing check of tests/test_gpu_halo.py, not a valid frame
             self.r.halo_record(True)
             return
+        # any other transport renders real frames: leave a record-only mode an earlier HaloFrames("record") set on this
+        # renderer (the native attach below also clears it in the library)
+        self.r.halo_record(False)
         if self.transport == "native":
             # one rank draws the communicator id, every rank receives it over the torch group; its last byte says
             # whether rank 0 could draw one, so that every rank fails together (never some ranks waiting inside a

@@ -49,7 +49,7 @@ def main():
         raise SystemExit(f"cfg_kbench: no default for {missing} in scripts/kbench.py DEFAULTS")
     r = restir.Renderer(0)
     r.set_scene(scene.bench_scene(cf["scene"]))
-    cam = scene.camera_for(cf["scene"], W, H)
+    cam = scene.camera_for(cf["scene"], W, H, cf.get("camera"))
     ref = None
     samples = {v: {} for v in variants}
     for _ in range(args.rounds):

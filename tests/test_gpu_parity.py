@@ -729,30 +729,55 @@ def test_textured_frames_match_oracle(gpu, oracle, texture):
     assert not np.array_equal(other, first)
 
 
+def geometry_bands(oracle, osc, cam, Wf, Hf, rows, n, min_hits=0.2):
+    """n row bands of `rows` rows spread over the rows whose oracle primary rays hit the scene: every band's pixels
+    are >= min_hits geometry (the oracle G-buffer of 64 candidate bands, not the GPU's)."""
+    cands = []
+    for y0 in np.linspace(0, Hf - rows, 64).astype(int):
+        _, p_mat = oracle.gbuffer(osc, cam, Wf, Hf, oracle.Rect(0, int(y0), Wf, rows))
+        if (p_mat[:, 3].view(np.uint32) != osc.miss_material).mean() >= min_hits:
+            cands.append(int(y0))
+    assert len(cands) >= n, f"only {len(cands)} bands hold >= {min_hits:.0%} geometry"
+    return [cands[i] for i in np.linspace(0, len(cands) - 1, n).astype(int)]
+
+
 # C4 (4K, 1024 parallelogram lights, k = 5 x1 biased) and C5 (8K, 4096 lights, M = 64, unbiased + spatial
-# visibility reuse) at their full sizes: the GPU frame's RGB on sampled row bands against the oracle rendering
-# those rows (with the ghost rows its spatial pass reads), bit for bit.
-@pytest.mark.parametrize("cfg", ["c4", "c5"])
+# visibility reuse) at their full sizes, with the TOML camera (c4, c5: 13 % geometry) and looking into the box (c4f,
+# c5f: 99.9 %): the GPU frame's RGB and returned grid (position, W, colour, M) on four row bands that each hold
+# >= 20 % geometry by the oracle's G-buffer, against the oracle rendering those rows (with the ghost rows its spatial
+# pass reads), bit for bit.
+@pytest.mark.parametrize("cfg", ["c4", "c5", "c4f", "c5f"])
 def test_full_size_frames_c4_c5_band_parity(gpu, oracle, cfg):
-    name, Wf, Hf, M, unb = {"c4": ("cornell_1024", 3840, 2160, 32, 0), "c5": ("cornell_4096", 7680, 4320, 64, 1)}[cfg]
+    name, Wf, Hf, M, unb = {"c4": ("cornell_1024", 3840, 2160, 32, 0), "c5": ("cornell_4096", 7680, 4320, 64, 1)}[cfg[:2]]
     s = get_scene(name)
     gpu.set_scene(s)
     gpu.set_seed(SEED, 0)
-    cam = scene.camera_for(name, Wf, Hf)
+    cam = scene.camera_for(name, Wf, Hf, "framed" if cfg.endswith("f") else None)
     f = _abi.default_features(initial_light_samples=M, num_samples_in_reservoir=1, spatial_resampling_passes=1,
                               temporal_reuse=0, unbiased_combination=unb, spatial_reuse_visibility_check=unb)
-    rgb, _ = gpu.render_restir(None, cam, Wf, Hf, f, want_grid=False)
+    rgb, grid = gpu.render_restir(None, cam, Wf, Hf, f)
     assert rgb.shape == (Hf, Wf, 3) and np.isfinite(rgb).all()
+    pos, col, w, m = grid.download()
+    del grid
     osc = oracle.OracleScene(s)
     g = f.spatial_resample_radius
-    for y0 in (0, Hf // 2 - 3, Hf - 4):
-        rows = 4
+    rows = 4
+    for y0 in geometry_bands(oracle, osc, cam, Wf, Hf, rows, 4):
         vy0 = max(0, y0 - g)
         view = oracle.Rect(0, vy0, Wf, min(Hf, y0 + rows + g) - vy0)
         rect = oracle.Rect(0, y0, Wf, rows)
-        want, _, _ = oracle.render_frame(osc, cam, f, Wf, Hf, view=view, rect=rect, threads=16)
+        want, res, _ = oracle.render_frame(osc, cam, f, Wf, Hf, SEED, 0, view=view, rect=rect, threads=16)
         r0 = Hf - (y0 + rows)          # RGB row 0 = top of the image
         assert_bits(rgb[r0:r0 + rows], want, f"{cfg} rows {y0}..{y0 + rows - 1}")
+        a, b = res
+        sl = slice((y0 - vy0) * Wf, (y0 - vy0 + rows) * Wf)
+        a = a[:, sl].reshape(1, rows, Wf, 4)
+        b = b[:, sl].reshape(1, rows, Wf, 4)
+        gs = slice(y0, y0 + rows)
+        assert_bits(pos[:, gs], np.ascontiguousarray(a[..., :3]), f"{cfg} grid position rows {y0}..")
+        assert_bits(w[:, gs], np.ascontiguousarray(a[..., 3]), f"{cfg} grid W rows {y0}..")
+        assert_bits(col[:, gs], np.ascontiguousarray(b[..., :3]), f"{cfg} grid colour rows {y0}..")
+        assert np.array_equal(m[:, gs], np.ascontiguousarray(b[..., 3]).view(np.uint32)), f"{cfg} grid M rows {y0}.."
 
 
 def test_full_size_c2_frame_band_parity(gpu, oracle):

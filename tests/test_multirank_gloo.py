@@ -326,3 +326,68 @@ def test_native_halo_operations_over_gloo(tmp_path, world, tiles, Wimg, Himg, R,
     for r in range(world):
         msg = open(tmp_path / f"rank{r}.txt").read()
         assert msg == "ok", f"rank {r}: {msg}"
+
+
+# ---- bench.py's halo transport choice ------------------------------------
+# select_halo builds the run's one HaloFrames, checks it against the ghost-zone tile and falls back to the torch
+# transport on a construction failure (every rank together) or a native mismatch; the instance it returns is the one
+# the halo-mode loop times, so the record's transport is the timed transport.  Stand-ins replace HaloFrames and the
+# tile comparison: a "native" transport whose tile differs (a corrupted segment), one whose attach fails on one rank,
+# and a torch transport that differs too (the run must fail).
+class _StandInHalo:
+    def __init__(self, transport):
+        self.transport = transport
+
+
+def _select_worker(rank, world, port, case, result):
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    from romis_amd import _abi
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    made = []
+
+    def make(tr):
+        if case == "attach_fails" and tr == "native" and rank == world - 1:
+            raise _abi.RestirError("stand-in: ncclCommInitRank failed")
+        made.append(tr)
+        return _StandInHalo(tr)
+
+    def check(hf):
+        # a corrupted segment on rank 0 over the native transport (every case), and over torch too in "torch_bad";
+        # summed over ranks as distributed.tile_mismatches does
+        bad = 1 if rank == 0 and (hf.transport == "native" or case == "torch_bad") else 0
+        t = torch.tensor([bad], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return int(t.item())
+
+    hf, rec, bad = bench.select_halo(torch, world, 0, "gloo", "native", make, check)
+    with open(f"{result}.{rank}", "w") as fh:
+        json.dump({"timed": hf.transport, "rec": rec, "bad": bad, "made": made}, fh)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["native_mismatch", "attach_fails", "torch_bad"])
+def test_bench_times_the_checked_halo_transport(tmp_path, case):
+    """The transport bench.py times is the one its record names and the one that passed the check: a native mismatch
+    or a failed native attach on any rank moves every rank to torch (recorded as native_check / native_error), and a
+    torch mismatch is reported (mismatches != 0: bench exits 3)."""
+    import json
+    world = 2
+    result = str(tmp_path / "r")
+    mp.spawn(_select_worker, args=(world, _free_port(), case, result), nprocs=world, join=True)
+    for rank in range(world):
+        with open(f"{result}.{rank}") as fh:
+            out = json.load(fh)
+        assert out["timed"] == out["rec"]["transport"] == "torch", (rank, out)
+        if case == "native_mismatch":
+            assert out["rec"]["native_check"] == "1 mismatching values" and out["bad"] == 0
+            assert out["made"] == ["native", "torch"]
+        elif case == "attach_fails":
+            assert out["bad"] == 0 and "native_check" not in out["rec"]
+            assert ("native_error" in out["rec"]) == (rank == world - 1)
+        else:
+            assert out["bad"] == 1 and out["rec"]["native_check"] == "1 mismatching values"

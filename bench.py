@@ -83,12 +83,6 @@ def parse():
                     help="HIP events on every n-th spatial launch of the timed region (the event-carrying dispatch "
                          "costs ~9 us of stream gaps, profiles/r4/gap); the roofline's average launch time is over "
                          "those launches")
-    ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
-                    help="frames in flight (restir_set_tuning frames.inflight): 2 overlaps frame f's final shading with "
-                         "frame f + 1's primary rays + RIS on a second stream; the spatial pass still runs alone, so "
-                         "its timed duration is the pass's (halo-mode frames: always 1).  Measured slower at C2 "
-                         "(0.461 -> 0.480 ms: RIS and final shading co-running take as long as in series; "
-                         "profiles/r4/r4e), so 1 is the default")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="restir_set_tuning knobs for A/B runs (launch shapes and timing only; results are identical)")
     ap.add_argument("--traffic-csv", default=None,
@@ -569,8 +563,6 @@ def main():
     measured = r.measure_read_bandwidth(4 << 30, 10)
     if args.prewarm_gemm_ms > 0:
         gemm_prewarm(torch, local, args.prewarm_gemm_ms)
-    if not halo:
-        r.set_tuning("frames.inflight", args.inflight)
     for _ in range(args.warmup):
         step()
     # Timed region: the spatial kernel (the roofline's) carries a HIP start / stop event pair recorded inside its
@@ -591,7 +583,6 @@ def main():
     elapsed = max_over_ranks(torch, world, t1 - t0, local)
     kt = r.timings()
     # per-kernel breakdown: serial frames (no overlap), every launch timed
-    r.set_tuning("frames.inflight", 1)
     r.reset_timings()
     r.set_tuning("timing.mask", -1)
     r.set_tuning("timing.every", 1)

@@ -35,10 +35,11 @@ KERNEL_FLAGS = ["-fno-slp-vectorize"]
 SOURCES = [
     ("kernels.hip", ["-x", "hip"] + DEVICE + KERNEL_FLAGS),
     ("restir.cpp", ["-x", "hip"] + DEVICE),
+    ("mis.hip", ["-x", "hip"] + DEVICE + KERNEL_FLAGS),
     ("bvh.cpp", ["-x", "c++"]),
     ("screen.cpp", ["-x", "c++"]),
 ]
-HEADERS = ["device_math.h", "restir_types.h", "launch.h", "bvh.h", "pow10_table.h"]
+HEADERS = ["device_math.h", "restir_types.h", "launch.h", "bvh.h", "pow10_table.h", "kernels_common.h", "launch_events.h"]
 
 
 def source_hash() -> str:

@@ -13,613 +13,7 @@
 // a per-lane loop; a wave's 64 lanes work on 64 pixels.  Reservoirs and the G-buffer are SoA float4 planes
 // read with 16-byte coalesced loads.  Visibility uses a stackless threaded BVH (no scratch stack) that the
 // ray kernels stage once per (persistent) workgroup into LDS; the light table is staged into LDS for RIS.
-#include "device_math.h"
-#include "restir_c.h"
-#include "restir_types.h"
-
-#include <float.h>
-
-namespace romis {
-
-#define ROMIS_FLT_MAX 3.402823466e+38F
-#define ROMIS_FLT_MIN 1.175494351e-38F
-
-// ---------------------------------------------------------------------------------------------------------
-// Ray / triangle, Moller-Trumbore, hit iff 0 < t <= tfar (Embree's (tnear, tfar] convention; the oracle
-// restates the same routine).
-__device__ __forceinline__ bool tri_hit(float4 v0, float4 e1_, float4 e2_, v3 o, v3 d, float tfar, float& t_out,
-                                        float& u_out, float& v_out) {
-    v3 e1 = xyz(e1_), e2 = xyz(e2_);
-    v3 pvec = vcross(d, e2);
-    float det = vdot(e1, pvec);
-    if (det == 0.0f) return false;
-    const float inv = rcp_rn(det);   // == 1.0f / det (the exact fast form, library division outside its range)
-    v3 tvec = vsub(o, xyz(v0));
-    float u = vdot(tvec, pvec) * inv;
-    if (!(u >= 0.0f && u <= 1.0f)) return false;
-    v3 qvec = vcross(tvec, e1);
-    float v = vdot(d, qvec) * inv;
-    if (!(v >= 0.0f && u + v <= 1.0f)) return false;
-    float t = vdot(e2, qvec) * inv;
-    if (!(t > 0.0f && t <= tfar)) return false;
-    t_out = t; u_out = u; v_out = v;
-    return true;
-}
-
-// tri_hit without early exits: the same expressions (u, v, t computed for every triangle), the decision as a
-// predicate; straight-line code for the closest-hit leaf loop
-__device__ __forceinline__ bool tri_test(float4 v0, float4 e1_, float4 e2_, v3 o, v3 d, float tfar, float& t, float& u,
-                                         float& v) {
-    const v3 e1 = xyz(e1_), e2 = xyz(e2_);
-    const v3 pvec = vcross(d, e2);
-    const float det = vdot(e1, pvec);
-    const float inv = rcp_rn(det);
-    const v3 tvec = vsub(o, xyz(v0));
-    u = vdot(tvec, pvec) * inv;
-    const v3 qvec = vcross(tvec, e1);
-    v = vdot(d, qvec) * inv;
-    t = vdot(e2, qvec) * inv;
-    return det != 0.0f && (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t <= tfar);
-}
-
-// The same test as an any-hit predicate without early exits (shadow rays): the same float expressions, so the
-// same decision, but straight-line code the compiler can interleave across a leaf's triangles.
-__device__ __forceinline__ bool tri_any(float4 v0, float4 e1_, float4 e2_, v3 o, v3 d, float tfar) {
-    const v3 e1 = xyz(e1_), e2 = xyz(e2_);
-    const v3 pvec = vcross(d, e2);
-    const float det = vdot(e1, pvec);
-    const float inv = rcp_rn(det);
-    const v3 tvec = vsub(o, xyz(v0));
-    const float u = vdot(tvec, pvec) * inv;
-    const v3 qvec = vcross(tvec, e1);
-    const float v = vdot(d, qvec) * inv;
-    const float t = vdot(e2, qvec) * inv;
-    return det != 0.0f && (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t <= tfar);
-}
-
-// Conservative slab test (boxes are padded on the host, the interval is widened): it may accept extra boxes,
-// never reject one that holds a valid hit, so traversal results equal the brute-force oracle.
-__device__ __forceinline__ bool box_hit(float4 lo, float4 hi, v3 o, v3 invd, float tmax_box) {
-    float tx0 = (lo.x - o.x) * invd.x, tx1 = (hi.x - o.x) * invd.x;
-    float ty0 = (lo.y - o.y) * invd.y, ty1 = (hi.y - o.y) * invd.y;
-    float tz0 = (lo.z - o.z) * invd.z, tz1 = (hi.z - o.z) * invd.z;
-    float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-    float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax_box));
-    return tmin <= tmax;
-}
-
-__device__ __forceinline__ v3 safe_inv(v3 d) {
-    return mk(1.0f / (d.x == 0.0f ? copysignf(1e-30f, d.x) : d.x), 1.0f / (d.y == 0.0f ? copysignf(1e-30f, d.y) : d.y),
-              1.0f / (d.z == 0.0f ? copysignf(1e-30f, d.z) : d.z));
-}
-
-__device__ __forceinline__ float widen(float t) { return t * 1.0001f + 1e-4f; }
-
-// The traversal arrays, either the global copies or the workgroup's LDS copy.
-struct Bvh {
-    const float4* nodes;
-    const float4* v0;
-    const float4* e1;
-    const float4* e2;
-    uint32_t num_nodes;
-};
-
-__device__ __forceinline__ Bvh global_bvh(const SceneDev& s) {
-    Bvh b;
-    b.nodes = s.nodes; b.v0 = s.tri_v0; b.e1 = s.tri_e1; b.e2 = s.tri_e2; b.num_nodes = s.num_nodes;
-    return b;
-}
-
-// Copy nodes + triangles into LDS (every thread of the block participates; ends with a barrier).
-__device__ __forceinline__ Bvh stage_bvh(const SceneDev& s, float4* lds) {
-    const uint32_t nn = 2u * s.num_nodes, nt = s.num_tris;
-    for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = s.nodes[i];
-    for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) {
-        lds[nn + i] = s.tri_v0[i];
-        lds[nn + nt + i] = s.tri_e1[i];
-        lds[nn + 2 * nt + i] = s.tri_e2[i];
-    }
-    __syncthreads();
-    Bvh b;
-    b.nodes = lds; b.v0 = lds + nn; b.e1 = lds + nn + nt; b.e2 = lds + nn + 2 * nt; b.num_nodes = s.num_nodes;
-    return b;
-}
-
-// any hit in (0, tfar] -- EmbreeInterface::anyHit (embree_interface.cpp:58-62)
-__device__ __forceinline__ bool occluded(const Bvh& b, v3 o, v3 d, float tfar) {
-    v3 invd = safe_inv(d);
-    float tb = widen(tfar);
-    uint32_t i = 0;
-    while (i < b.num_nodes) {
-        float4 lo = b.nodes[2 * i], hi = b.nodes[2 * i + 1];
-        uint32_t miss = __float_as_uint(lo.w), leaf = __float_as_uint(hi.w);
-        if (box_hit(lo, hi, o, invd, tb)) {
-            if (leaf) {
-                uint32_t first = leaf & 0xFFFFFFu, cnt = leaf >> 24;
-                for (uint32_t k = 0; k < cnt; k += 2) {   // two triangles per step (leaves hold 2 by default)
-                    bool h = tri_any(b.v0[first + k], b.e1[first + k], b.e2[first + k], o, d, tfar);
-                    if (k + 1 < cnt) h = tri_any(b.v0[first + k + 1], b.e1[first + k + 1], b.e2[first + k + 1], o, d, tfar) || h;
-                    if (h) return true;
-                }
-                i = miss;
-            } else {
-                i = i + 1;
-            }
-        } else {
-            i = miss;
-        }
-    }
-    return false;
-}
-
-// closest hit: minimal t, lowest original triangle index on ties
-__device__ __forceinline__ bool closest(const Bvh& b, v3 o, v3 d, float& t_best, float& u_best, float& v_best,
-                                        uint32_t& tri_best) {
-    v3 invd = safe_inv(d);
-    bool found = false;
-    t_best = ROMIS_FLT_MAX;
-    tri_best = 0xFFFFFFFFu;
-    uint32_t i = 0;
-    while (i < b.num_nodes) {
-        float4 lo = b.nodes[2 * i], hi = b.nodes[2 * i + 1];
-        uint32_t miss = __float_as_uint(lo.w), leaf = __float_as_uint(hi.w);
-        if (box_hit(lo, hi, o, invd, widen(t_best))) {
-            if (leaf) {
-                uint32_t first = leaf & 0xFFFFFFu, cnt = leaf >> 24;
-                for (uint32_t k = 0; k < cnt; k++) {
-                    const float4 v0 = b.v0[first + k];
-                    float t, u, v;
-                    const bool h = tri_test(v0, b.e1[first + k], b.e2[first + k], o, d, ROMIS_FLT_MAX, t, u, v);
-                    const uint32_t orig = __float_as_uint(v0.w);
-                    if (h && (!found || t < t_best || (t == t_best && orig < tri_best))) {
-                        found = true; t_best = t; u_best = u; v_best = v; tri_best = orig;
-                    }
-                }
-                i = miss;
-            } else {
-                i = i + 1;
-            }
-        } else {
-            i = miss;
-        }
-    }
-    return found;
-}
-
-// testVisibilityLightSample (utils.cpp:41-56)
-__device__ __forceinline__ bool visible(const Bvh& b, v3 P, v3 y) {
-    v3 dir = vnormalize(vsub(y, P));
-    v3 P2 = vadd(P, vscale(dir, 1e-3f));
-    float tfar = vdistance(P2, y);
-    return !occluded(b, P2, dir, tfar);
-}
-
-// ---------------------------------------------------------------------------------------------------------
-// Pixel shading context
-struct Px {
-    v3 P, N, V;
-    float t;
-    uint32_t mat;
-    float4 kd_sh;   // diffuseAlbedo.xyz (kd, or the kdTexture texel -- apply_albedo), shininess
-    float4 ks_pm;   // ks.xyz, bits(pow mode)
-    float4 pw;      // (pow underflow threshold, bits(shininess class), transparency, bits(kd_texture))
-};
-
-// acquireTexel's index (texture.cpp:5-6): the float product texCoord * (size - 1) truncated toward zero;
-// products outside [0, size - 1] (an out-of-bounds read in the reference) clamp to the edge texel
-__device__ __forceinline__ uint32_t texel_index(float c, uint32_t n) {
-    const float v = c * (float)((int)n - 1);
-    if (!(v >= 0.0f)) return 0u;
-    if (v >= (float)(n - 1u)) return n - 1u;
-    return (uint32_t)v;
-}
-
-// diffuseAlbedo (utils.cpp:33-37): with texture mapping on and a kdTexture on the material, the texel at the
-// hit's texCoord (the G-buffer plane s.gbuf_uv, view pixel p) replaces kd as the diffuse colour
-__device__ __forceinline__ void apply_albedo(const SceneDev& s, Px& r, size_t p) {
-    const uint32_t tex = __float_as_uint(r.pw.w);
-    if (s.tex_on && tex) {
-        const float2 tc = s.gbuf_uv[p];
-        const uint4 dim = s.tex_dims[tex - 1u];   // width, height, first texel
-        const float4 t = s.tex_texels[dim.z + texel_index(tc.y, dim.y) * dim.x + texel_index(tc.x, dim.x)];
-        r.kd_sh.x = t.x; r.kd_sh.y = t.y; r.kd_sh.z = t.z;
-    }
-}
-
-__device__ __forceinline__ Px make_px(const SceneDev& s, float4 a, float4 b, v3 origin, size_t p) {
-    Px r;
-    r.N = xyz(a); r.t = a.w;
-    r.P = xyz(b);
-    uint32_t m = __float_as_uint(b.w);
-    if (m >= s.num_materials) m = s.num_materials - 1;
-    r.mat = m;
-    r.kd_sh = s.materials[3 * m];
-    r.ks_pm = s.materials[3 * m + 1];
-    r.pw = s.materials[3 * m + 2];
-    r.V = vnormalize(vsub(origin, r.P));
-    apply_albedo(s, r, p);
-    return r;
-}
-
-__device__ __forceinline__ size_t gidx(const Region& rg, size_t p) { return p * rg.ps; }
-__device__ __forceinline__ size_t ridx(const Region& rg, uint32_t j, size_t p) { return (size_t)j * rg.js + p * rg.ps; }
-
-__device__ __forceinline__ Px load_px(const SceneDev& s, const Region& rg, const float4* __restrict__ n_t,
-                                      const float4* __restrict__ p_mat, size_t p, v3 origin) {
-    return make_px(s, n_t[gidx(rg, p)], p_mat[p], origin, p);
-}
-
-// std::pow(cosTheta, shininess) (shading.cpp:26) = glibc's powf (device_math.h gl_powf), specialised per
-// material with the exponent's classes precomputed on the host (restir.cpp put_material, ROMIS_PWC_*):
-//  - ks == 0 skips it (the product with ks is the same +-0 the reference gets after its NaN clean-up --
-//    DESIGN.md "Floating point");
-//  - |x| below the material's threshold is glibc's own underflow exit (+-0, negative for a negative base and an
-//    odd integer exponent), decided before the log2 / exp2 evaluation;
-//  - y = +-0 / NaN / +-inf are glibc's zeroinfnan(y) returns; otherwise of its special cases only a NaN base
-//    (whose NaN the caller's clean-up zeroes whatever its payload: cosTheta is never a signalling NaN), a
-//    negative base (invalid unless y is an integer, sign from y's parity) and a zero / subnormal base remain.
-// material_pow in two parts.  pow_pre decides every case glibc settles without its log2 / exp2 core (returns
-// true with the power in pw); otherwise it returns false with the core's input in job: the (subnormal-adjusted)
-// bits of |x| and, in bit 31, glibc's sign_bias (negative base, odd integer exponent).  pow_core(job, y) is the
-// rest of __powf.  (Evaluating only the cores some lane needs, wave-compacted through LDS across batches of
-// candidates, was measured slower in RIS: 345 -> 393-591 us, the batch state costing occupancy -- DESIGN §6.)
-__device__ __forceinline__ bool pow_pre(float x, const Px& px, float& pw, uint32_t& job) {
-    const uint32_t mode = __float_as_uint(px.ks_pm.w);
-    if (mode != ROMIS_POW_GLIBC) {
-        // ROMIS_POW_SKIP, or ROMIS_POW_SIMPLE: every base glibc settles before its core is under the threshold
-        // (+-0, NaN passed through) or a negative base with a non-integer exponent (invalid), as selects
-        const uint32_t cls = __float_as_uint(px.pw.y);
-        const float ax = fabsf(x);
-        const bool neg_odd = __builtin_signbit(x) && (cls & ROMIS_PWC_ODD);
-        const bool under = !(ax >= px.pw.x);
-        const bool invalid = x < 0.0f && !(cls & ROMIS_PWC_INT);
-        float r = under ? (__builtin_isnan(x) ? x : (neg_odd ? -0.0f : 0.0f)) : __uint_as_float(0xffc00000u);
-        const bool skip = mode == ROMIS_POW_SKIP;
-        pw = skip ? 1.0f : r;
-        job = __float_as_uint(ax) | (neg_odd ? 0x80000000u : 0u);
-        return skip || under || invalid;
-    }
-    const uint32_t cls = __float_as_uint(px.pw.y);
-    const float ax = fabsf(x);
-    if (__builtin_expect(cls & ROMIS_PWC_SPECIAL, 0)) {
-        if (cls & ROMIS_PWC_ZERO) pw = 1.0f;
-        else if (cls & ROMIS_PWC_NAN) pw = x == 1.0f ? 1.0f : __builtin_nanf("");
-        else if (__builtin_isnan(x)) pw = x;
-        else if (ax == 1.0f) pw = 1.0f;
-        else pw = ((ax < 1.0f) == ((cls & ROMIS_PWC_PINF) != 0u)) ? 0.0f : __builtin_inff();
-        return true;
-    }
-    const bool neg_odd = __builtin_signbit(x) && (cls & ROMIS_PWC_ODD);
-    if (!(ax >= px.pw.x)) { pw = __builtin_isnan(x) ? x : (neg_odd ? -0.0f : 0.0f); return true; }
-    if (x < 0.0f && !(cls & ROMIS_PWC_INT)) { pw = __uint_as_float(0xffc00000u); return true; }
-    uint32_t ix = __float_as_uint(ax);
-    if (__builtin_expect(ix < 0x00800000u, 0)) {
-        if (ix == 0u) {
-            const float z = neg_odd ? -0.0f : 0.0f;
-            pw = (cls & ROMIS_PWC_NEG) ? 1.0f / z : z;
-            return true;
-        }
-        ix = (__float_as_uint(ax * 0x1p23f) & 0x7fffffffu) - (23u << 23);
-    }
-    job = ix | (neg_odd ? 0x80000000u : 0u);
-    return false;
-}
-
-__device__ __forceinline__ float pow_core(const GlTabs& tb, uint32_t job, float y) {
-    const double ylogx = (double)y * gl_log2_inline(tb, job & 0x7fffffffu);
-    const uint32_t sign_bias = (job >> 31) ? 0x10000u : 0u;
-    if (__builtin_expect(((unsigned long long)__double_as_longlong(ylogx) >> 47 & 0xffffu) >= 0x80bfu, 0)) {
-        if (ylogx > 0x1.fffffffd1d571p+6) return gl_xflowf(sign_bias, 0x1p97f);
-        if (ylogx <= -150.0) return gl_xflowf(sign_bias, 0x1p-95f);
-        if (ylogx < -149.0) return gl_xflowf(sign_bias, 0x1.4p-75f);
-    }
-    return gl_exp2_inline(tb, ylogx, sign_bias);
-}
-
-__device__ __forceinline__ float material_pow(const GlTabs& tb, float x, const Px& px) {
-    float pw;
-    uint32_t job;
-    return pow_pre(x, px, pw, job) ? pw : pow_core(tb, job, px.kd_sh.w);
-}
-
-// computeShading (shading.cpp:7-34) in two parts around the power.  shade_pre: the light direction and distance,
-// dotNL (a back-facing light, dotNL < 0, shades to exactly 0) and the power's argument cosTheta.
-struct ShadePre {
-    float d, dotNL, cosTheta;
-};
-#ifndef ROMIS_SKIP_COS
-#define ROMIS_SKIP_COS 1
-#endif
-__device__ __forceinline__ ShadePre shade_pre(const Px& px, v3 lpos) {
-    ShadePre r;
-    v3 L = vnormalize_len(vsub(lpos, px.P), r.d);   // d = glm::distance(hitPos, lightPos), the length normalize() takes
-    r.dotNL = vdot(px.N, L);
-    r.cosTheta = 0.0f;
-    if (r.dotNL < 0.0f) return r;
-    // ks = 0 (ROMIS_POW_SKIP): the power, and so R and cosTheta, never reach the result (pow_pre returns 1 for any
-    // argument) -- skipped, ROMIS_SKIP_COS (7 of the 8 Cornell materials)
-    if (ROMIS_SKIP_COS && __float_as_uint(px.ks_pm.w) == ROMIS_POW_SKIP) return r;
-    v3 R = vnormalize(vsub(vscale(px.N, 2.0f * r.dotNL), L));
-    r.cosTheta = vdot(R, px.V);
-    return r;
-}
-// shade_post: the terms, the reference's NaN clean-up and the distance falloff
-__device__ __forceinline__ v3 shade_post(const SceneDev& s, const Px& px, v3 lcol, float dotNL, float d, float pw) {
-    v3 diffuse = vscale(vmul(lcol, xyz(px.kd_sh)), dotNL);
-    v3 specular = vscale(vmul(lcol, xyz(px.ks_pm)), pw);
-    // The reference zeroes a term holding a NaN.  When every colour x reflectance product is finite (host
-    // check, SceneDev::shade_finite), a term can only hold one through a non-finite dotNL / pow factor, so
-    // the six per-component tests run only for lanes where one of those two is non-finite.
-    if (!(s.shade_finite && __builtin_isfinite(dotNL) && __builtin_isfinite(pw))) {
-        if (vany_nan(diffuse)) diffuse = mk(0.0f, 0.0f, 0.0f);
-        if (vany_nan(specular)) specular = mk(0.0f, 0.0f, 0.0f);
-    }
-    if (fabsf(d) < 1e-5f) d = 1.0f;
-    return vdivs(vadd(diffuse, specular), d * d);
-}
-
-// computeShading (shading.cpp:7-34), general form: every IEEE special case, any material
-__device__ __forceinline__ v3 shade_ref(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,
-                                        const GlTabs& tb = gl_global_tabs()) {
-    if (!f.shading) return xyz(s.materials[3 * px.mat]);   // material.kd, not the albedo (shading.cpp:8)
-    const ShadePre sp = shade_pre(px, lpos);
-    if (sp.dotNL < 0.0f) return mk(0.0f, 0.0f, 0.0f);
-    return shade_post(s, px, lcol, sp.dotNL, sp.d, material_pow(tb, sp.cosTheta, px));
-}
-
-__device__ __forceinline__ v3 shade(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,
-                                    const GlTabs& tb = gl_global_tabs()) {
-    return shade_ref(s, f, px, lpos, lcol, tb);
-}
-
-// target pdf = glm::length(computeShading(...)) (light.cpp:84, reservoir.cpp:49)
-__device__ __forceinline__ float target_pdf(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,
-                                            const GlTabs& tb = gl_global_tabs()) {
-    return vlength(shade_ref(s, f, px, lpos, lcol, tb));
-}
-
-// target_pdf(...) > 0.0f, exactly, without the tail of computeShading where the comparison is decided before it
-// (the unbiased combine's Z, reservoir.cpp:84-96, needs only the sign).  For a ks = 0 material (ROMIS_POW_SKIP:
-// the specular term is a +-0 vector) in a scene whose colour x reflectance products are finite, with
-// a finite dotNL >= 0: the shaded vector is v_c = RN(RN(A_c dotNL) / D), A_c = lcol_c kd_c, D = RN(d' d') (d' = 1
-// below 1e-5); p = sqrt(sum RN(v_c^2)) is > 0 iff some RN(v_c^2) > 0, i.e. some |v_c| > 2^-75.  RN is monotone, so
-// max |v_c| = RN(e / D) with e = RN(max |A_c| dotNL); e > 2^-60 D decides true and e < 2^-90 D false (2^15 of margin
-// against any rounding); anything else -- other materials, non-finite or tiny values -- takes the full evaluation.
-__device__ __forceinline__ bool target_pdf_positive(const SceneDev& s, const FeaturesDev& f, const Px& px, v3 lpos, v3 lcol,
-                                                    const GlTabs& tb) {
-    if (f.shading && s.shade_finite && __float_as_uint(px.ks_pm.w) == ROMIS_POW_SKIP) {
-        const ShadePre sp = shade_pre(px, lpos);
-        if (sp.dotNL < 0.0f) return false;   // computeShading's back-facing exit: the zero vector
-        if (__builtin_isfinite(sp.dotNL)) {
-            const float A = fmaxf(fmaxf(fabsf(lcol.x * px.kd_sh.x), fabsf(lcol.y * px.kd_sh.y)), fabsf(lcol.z * px.kd_sh.z));
-            const float e = A * sp.dotNL;
-            const float dd = fabsf(sp.d) < 1e-5f ? 1.0f : sp.d;
-            const float D = dd * dd;
-            if (e > 0x1p-60f * D) return true;
-            if (e < 0x1p-90f * D) return false;
-        }
-    }
-    return target_pdf(s, f, px, lpos, lcol, tb) > 0.0f;
-}
-
-// The block's LDS copy of powf's two tables (512 B): every p-hat evaluation indexes them twice per lane, and from
-// __constant__ memory each index is a vector-memory round trip in the middle of the dependent chain (two per
-// target pdf); from LDS it is a ds_read.  Every thread of the block must call this (it ends with a barrier).
-template <bool SYNC = true>
-__device__ __forceinline__ GlTabs gl_stage_tables() {
-    __shared__ double s_gl_log2[32];
-    __shared__ unsigned long long s_gl_exp2[32];
-    if (threadIdx.x < 32u) {
-        s_gl_log2[threadIdx.x] = kGlLog2Tab[threadIdx.x];
-        s_gl_exp2[threadIdx.x] = kGlExp2Tab[threadIdx.x];
-    }
-    if (SYNC) __syncthreads();   // SYNC = false: the caller's next barrier precedes every table read
-    GlTabs t;
-    t.log2 = s_gl_log2;
-    t.exp2 = s_gl_exp2;
-    return t;
-}
-// The same copy by one LDS-DMA instruction of wave 0 (lanes 0-15 the log2 table, 16-31 the exp2 table, 16 B each):
-// no VGPR round trip and no wait of its own -- the register-staged form above waits for its loads right where it is
-// issued, before the block's own loads go out.  The caller's s_waitcnt vmcnt(0) + barrier make it visible.
-__device__ __forceinline__ GlTabs gl_stage_tables_dma() {
-    __shared__ __attribute__((aligned(16))) unsigned long long s_gl_tab[64];
-    if (threadIdx.x < 32u) {
-        const unsigned long long* src = threadIdx.x < 16u
-                                            ? reinterpret_cast<const unsigned long long*>(kGlLog2Tab) + 2u * threadIdx.x
-                                            : kGlExp2Tab + 2u * (threadIdx.x - 16u);
-        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)s_gl_tab, 16, 0, 0);
-    }
-    GlTabs t;
-    t.log2 = reinterpret_cast<const double*>(s_gl_tab);
-    t.exp2 = s_gl_tab + 32;
-    return t;
-}
-
-// ---------------------------------------------------------------------------------------------------------
-// Reservoir state (reservoir.h:28-73), one sub-reservoir
-struct Sub {
-    v3 pos, col;
-    float W;
-    uint32_t M;
-    float wsum, chosen;
-    // target pdf of the held sample at the combining pixel, cached when the sample was accepted: the
-    // final W (reservoir.cpp:61-64, light.cpp:90-93) re-evaluates exactly that value, so it is reused
-    float pd;
-    bool has_pd;
-};
-
-__device__ __forceinline__ void sub_init(Sub& r) {
-    r.pos = mk(0.0f, 0.0f, 0.0f); r.col = mk(0.0f, 0.0f, 0.0f);
-    r.W = 0.0f; r.M = 1u; r.wsum = ROMIS_FLT_MIN; r.chosen = 0.0f;
-    r.pd = 0.0f; r.has_pd = false;
-}
-
-// Reservoir::update (reservoir.cpp:10-32)
-__device__ __forceinline__ void sub_take(Sub& r, v3 pos, v3 col, float w, float u, float pd) {
-    r.M += 1u;
-    r.wsum += w;
-    if (u < (w / r.wsum)) { r.pos = pos; r.col = col; r.chosen = w; r.pd = pd; r.has_pd = true; }
-}
-
-template <int NT>
-__device__ __forceinline__ uint32_t res_update(Sub* r, uint32_t N, v3 pos, v3 col, float w, float u, float pd) {
-    if (NT == 1) {
-        sub_take(r[0], pos, col, w, u, pd);
-        return 0;
-    }
-    uint32_t k = 0;
-    float best = ROMIS_FLT_MAX;
-    const uint32_t n = NT > 0 ? (uint32_t)NT : N;
-    if (NT > 0) {
-        // compile-time N: every sub-reservoir updated by selects, no dynamic register indexing (predicated
-        // sub_take calls were merged back into one r[k] store by the compiler, which put r[] in scratch memory)
-#pragma unroll
-        for (uint32_t j = 0; j < (uint32_t)(NT > 0 ? NT : 1); j++)
-            if (r[j].wsum < best) { k = j; best = r[j].wsum; }
-        float ws = r[0].wsum;
-#pragma unroll
-        for (uint32_t j = 1; j < (uint32_t)(NT > 0 ? NT : 1); j++) ws = (j == k) ? r[j].wsum : ws;
-        ws += w;                            // sub_take's wsum += w on the routed one
-        const bool acc = u < (w / ws);      // ... and its acceptance test
-#pragma unroll
-        for (uint32_t j = 0; j < (uint32_t)(NT > 0 ? NT : 1); j++) {
-            const bool sel = j == k, take = sel && acc;
-            r[j].M += sel ? 1u : 0u;
-            r[j].wsum = sel ? ws : r[j].wsum;
-            r[j].pos = mk(take ? pos.x : r[j].pos.x, take ? pos.y : r[j].pos.y, take ? pos.z : r[j].pos.z);
-            r[j].col = mk(take ? col.x : r[j].col.x, take ? col.y : r[j].col.y, take ? col.z : r[j].col.z);
-            r[j].chosen = take ? w : r[j].chosen;
-            r[j].pd = take ? pd : r[j].pd;
-            r[j].has_pd = take || r[j].has_pd;
-        }
-    } else {
-        for (uint32_t j = 0; j < n; j++)
-            if (r[j].wsum < best) { k = j; best = r[j].wsum; }
-        sub_take(r[k], pos, col, w, u, pd);
-    }
-    return k;
-}
-
-template <int NT>
-__device__ __forceinline__ void macc_add(uint32_t* macc, uint32_t k, uint32_t m) {
-    if (NT > 0) {
-#pragma unroll
-        for (uint32_t j = 0; j < (uint32_t)(NT > 0 ? NT : 1); j++)
-            if (j == k) macc[j] += m;
-    } else {
-        macc[k] += m;
-    }
-}
-
-__device__ __forceinline__ float contribution_weight(float p, uint32_t M, float wsum) {
-    if (p == 0.0f) return 0.0f;
-    return (rcp_rn(p) * rcp_rn((float)M)) * wsum;   // rcp_rn(b) == 1.0f / b bit for bit (device_math.h)
-}
-
-__device__ __forceinline__ Sub sub_from(float4 fa, float4 fb) {
-    Sub r;
-    r.pos = xyz(fa); r.W = fa.w;
-    r.col = xyz(fb); r.M = __float_as_uint(fb.w);
-    r.wsum = 0.0f; r.chosen = 0.0f;
-    r.pd = 0.0f; r.has_pd = false;
-    return r;
-}
-
-__device__ __forceinline__ void sub_load(Sub& r, const float4* __restrict__ a, const float4* __restrict__ b, size_t i) {
-    r = sub_from(a[i], b[i]);
-}
-
-__device__ __forceinline__ void sub_store(const Sub& r, float4* __restrict__ a, float4* __restrict__ b,
-                                          float2* __restrict__ dbg, size_t i, size_t idbg) {
-    a[i] = make_float4(r.pos.x, r.pos.y, r.pos.z, r.W);
-    b[i] = make_float4(r.col.x, r.col.y, r.col.z, __uint_as_float(r.M));
-    if (dbg) dbg[idbg] = make_float2(r.wsum, r.chosen);
-}
-
-// Neighbour (x + dx, y + dy) clamped to the image (render_utils.cpp:109-110), then -- defensively -- to the
-// stored view (the host guarantees the view holds every reachable neighbour; this only prevents a fault).
-__device__ __forceinline__ size_t neighbour_index(const Region& rg, uint32_t x, uint32_t y, int dx, int dy) {
-    int nx = min(max((int)x + dx, 0), (int)rg.W - 1);
-    int ny = min(max((int)y + dy, 0), (int)rg.H - 1);
-    nx = min(max(nx, (int)rg.vx0), (int)(rg.vx0 + rg.vw) - 1);
-    ny = min(max(ny, (int)rg.vy0), (int)(rg.vy0 + rg.vh) - 1);
-    return (size_t)(ny - (int)rg.vy0) * rg.vw + (size_t)(nx - (int)rg.vx0);
-}
-
-// ---------------------------------------------------------------------------------------------------------
-// Work mapping.  Tiles of 32x8 pixels, one 256-lane block each (a wave = 32x2 pixels).
-constexpr uint32_t kTileW = 32, kTileH = 8;
-
-__device__ __forceinline__ uint32_t num_tiles(const Region& rg) {
-    return ((rg.rw + kTileW - 1) / kTileW) * ((rg.rh + kTileH - 1) / kTileH);
-}
-
-__device__ __forceinline__ bool tile_pixel_of(const Region& rg, uint32_t tile, uint32_t& x, uint32_t& y, size_t& p) {
-    const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
-    const uint32_t tx = tile % ntx, ty = tile / ntx;
-    if (rg.map2d == 2u) {   // each wave an 8x8 block of the 32x8 tile (a squarer gather footprint per wave)
-        const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
-        x = rg.rx0 + tx * kTileW + w * 8u + (l & 7u);
-        y = rg.ry0 + ty * kTileH + (l >> 3);
-    } else {
-        x = rg.rx0 + tx * kTileW + threadIdx.x % kTileW;
-        y = rg.ry0 + ty * kTileH + threadIdx.x / kTileW;
-    }
-    if (x >= rg.rx0 + rg.rw || y >= rg.ry0 + rg.rh) return false;
-    p = (size_t)(y - rg.vy0) * rg.vw + (x - rg.vx0);
-    return true;
-}
-
-// Spatial pass: blocks are dealt round-robin over the 8 XCDs (blocks b and b+8 share one --
-// MI355X_MICROARCH.md "Workgroup dispatch"), so block b is remapped to give each XCD one contiguous run of
-// tiles, i.e. a horizontal band of the image: the rows a neighbourhood gathers then sit in that XCD's L2
-// instead of being fetched by all eight (FETCH_SIZE 0.95 GB -> 0.15 GB per 1080p pass, profiles/).
-__device__ __forceinline__ uint32_t xcd_banded_tile() {
-    const uint32_t nb = gridDim.x, b = blockIdx.x;
-    const uint32_t xcd = b % 8u, q = nb / 8u, rem = nb % 8u;
-    return xcd * q + min(xcd, rem) + b / 8u;
-}
-
-__device__ __forceinline__ bool region_pixel(const Region& rg, uint32_t idx, uint32_t& x, uint32_t& y, size_t& p) {
-    if (idx >= rg.rw * rg.rh) return false;
-    x = rg.rx0 + idx % rg.rw;
-    y = rg.ry0 + idx / rg.rw;
-    p = (size_t)(y - rg.vy0) * rg.vw + (x - rg.vx0);
-    return true;
-}
-
-// Work items of a launch: 32x8 tiles (map2d) or runs of 256 row-major pixels.
-__device__ __forceinline__ uint32_t work_items(const Region& rg) {
-    return rg.map2d ? num_tiles(rg) : (rg.rw * rg.rh + 255u) / 256u;
-}
-__device__ __forceinline__ bool work_pixel(const Region& rg, uint32_t item, uint32_t& x, uint32_t& y, size_t& p) {
-    return rg.map2d ? tile_pixel_of(rg, item, x, y, p) : region_pixel(rg, item * 256u + threadIdx.x, x, y, p);
-}
-
-// Work items of a persistent block: from the dynamic queue when there is one (thread 0 takes a ticket, the
-// block shares it through LDS), else the static stride blockIdx.x, blockIdx.x + gridDim.x, ...
-struct WorkCursor {
-    WorkQueue q;
-    uint32_t item;
-    __device__ explicit WorkCursor(WorkQueue wq) : q(wq), item(0) {}
-    __device__ __forceinline__ uint32_t fetch() {
-        __shared__ uint32_t s_item;
-        __syncthreads();   // every thread has read the previous ticket
-        if (threadIdx.x == 0) s_item = atomicAdd(q.ctr, 1u) - q.base;
-        __syncthreads();
-        return s_item;
-    }
-    __device__ __forceinline__ uint32_t first() { return item = q.ctr ? fetch() : blockIdx.x; }
-    __device__ __forceinline__ uint32_t next() { return item = q.ctr ? fetch() : item + gridDim.x; }
-};
-
-}  // namespace romis
-
-using namespace romis;
-
-extern __shared__ __attribute__((aligned(16))) float4 g_lds[];
+#include "kernels_common.h"
 
 // ---------------------------------------------------------------------------------------------------------
 // genPrimaryRayHits for pixel (x, y) at view index p: writes and returns the G-buffer records (n_t, p_mat)
@@ -713,9 +107,6 @@ constexpr int kLtGeneral = 0, kLtPoint = 1, kLtGrid = 2, kLtPgram = 3, kLtRegula
 __host__ __device__ constexpr uint32_t lt_stride(int lt) {
     return lt == kLtGeneral ? 7u : lt == kLtPgram ? 4u : lt == kLtRegular ? 1u : 2u;
 }
-#ifndef ROMIS_RIS_PF
-#define ROMIS_RIS_PF 0   // build variant: software-pipelined colour loads for kLtRegular (ris_pixel)
-#endif
 template <int NT, int LT = kLtGeneral>
 __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                           const float4* lights, const Bvh& bvh, float4 nt, float4 pm, uint32_t x,
@@ -811,22 +202,9 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 // sample: the sample is a function of the candidate's draws (slots 4c .. 4c + 2), so it is drawn
                 // again once after the loop -- two selects per candidate instead of nine
                 uint32_t best = 0xFFFFFFFFu;
-                // ROMIS_RIS_PF (kLtRegular from global memory): candidate c + 1's colour is loaded while candidate c's
-                // target pdf runs (the same load, issued one iteration early)
-                constexpr bool kPf = ROMIS_RIS_PF && LT == kLtRegular;
-                uint32_t inext = 0u;
-                v3 gnext = mk(0.0f, 0.0f, 0.0f);
-                if (kPf && c_end) { inext = uniform_index(draw(ps, 0u), L); gnext = xyz(lights[inext]); }
                 for (uint32_t c = 0; c < c_end; c++) {
                     v3 pos, col;
-                    if (kPf) {
-                        const uint32_t ic = inext;
-                        const v3 gc = gnext;
-                        if (c + 1u < c_end) { inext = uniform_index(draw(ps, 4u * (c + 1u)), L); gnext = xyz(lights[inext]); }
-                        sample_reg(c, ic, gc, pos, col);
-                    } else {
-                        sample(c, pos, col);
-                    }
+                    sample(c, pos, col);
                     const float pd = target_pdf(s, f, px, pos, col, tb);
                     const float w = weight(pd);
                     r[0].M += 1u;
@@ -881,7 +259,7 @@ template <int NT, bool LDS_LIGHTS, int LT = kLtGeneral>
 __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                          const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                          float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
-                                         float* __restrict__ rp, WorkQueue wq) {
+                                         float* __restrict__ rp) {
     const float4* lights = global_lights<LT>(s);
     if (LDS_LIGHTS) {
         stage_lights<LT>(s, g_lds);
@@ -891,8 +269,7 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
     const Bvh bvh = global_bvh(s);
     const GlTabs tb = gl_stage_tables();
     const uint32_t items = work_items(rg);
-    WorkCursor cur(wq);
-    for (uint32_t item = cur.first(); item < items; item = cur.next()) {
+    for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {
         uint32_t x, y;
         size_t p;
         if (!work_pixel(rg, item, x, y, p)) continue;
@@ -984,8 +361,8 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
 #define ROMIS_RIS_KERNEL_LT(NT, LDS, LT, NAME, ATTR)                                                                  \
     extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,   \
-                                                          float4* ra, float4* rb, float2* rdbg, float* rp, WorkQueue wq) { \
-        ris_body<NT, LDS, LT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg, rp, wq);                         \
+                                                          float4* ra, float4* rb, float2* rdbg, float* rp) {           \
+        ris_body<NT, LDS, LT>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ra, rb, rdbg, rp);                             \
     }
 #define ROMIS_RIS_KERNEL(NT, LDS, NAME, ATTR) ROMIS_RIS_KERNEL_LT(NT, LDS, kLtGeneral, NAME, ATTR)
 ROMIS_RIS_KERNEL(1, false, k_ris_n1, ROMIS_RIS1_ATTR)
@@ -1282,11 +659,6 @@ __device__ __forceinline__ void spatial_body(const SceneDev& s, const Region& rg
 #define ROMIS_SPATIAL_WPE 4
 #endif
 #define ROMIS_SPATIAL_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL_WPE)))
-// k_spatial1 fits 96 VGPRs (5 waves per SIMD) without spilling; the general kernels spill there
-#ifndef ROMIS_SPATIAL1_WPE
-#define ROMIS_SPATIAL1_WPE 5
-#endif
-#define ROMIS_SPATIAL1_ATTR __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL1_WPE)))
 #define ROMIS_SPATIAL_KERNEL(NT, UB, NAME)                                                                             \
     extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, \
                                                           float oy, float oz, const float4* n_t, const float4* p_mat,    \
@@ -1302,21 +674,10 @@ ROMIS_SPATIAL_KERNEL(2, true, k_spatial_n2_unbiased)
 ROMIS_SPATIAL_KERNEL(0, true, k_spatial_n0_unbiased)
 
 // ---------------------------------------------------------------------------------------------------------
-// k_spatial1: the N = 1 biased pass (the headline configuration), written for a small VALU stream.
-// Same arithmetic and RNG slots as spatial_pixel<1, false>; what changes is how it is laid out:
-//  - 32-bit byte offsets from the plane bases (saddr + voffset loads, no 64-bit address math), neighbour
-//    clamping by v_med3 against precomputed bounds;
-//  - the five depth tests share one double reciprocal of the pixel's depth (exact: div_by_rcp_d), and are
-//    evaluated only for lanes whose normal test passed (a miss pixel's zero normal rejects every neighbour);
-//  - the pixel's own G-buffer + reservoir are loaded together with the five neighbour G-buffer records; the
-//    accepted neighbours' reservoirs are loaded one neighbour ahead of the consume sequence (91 VGPRs = 5 waves
-//    per SIMD; the whole batch at once took 111 = 4 waves and ran 8 % slower), and the target pdf of the
-//    pixel's own sample (consumed last) is evaluated while the first neighbour's reservoir is in flight;
-//  - the neighbours are consumed by a fully unrolled sequence (static register indices, no batch shifting),
-//    each behind a branch that the wave skips when none of its lanes accepted that neighbour.
-// Measured (scripts/kbench.py, 1080p C2): 99-100 us against 103-106 us for spatial_pixel<1, false>; SQ counters:
-// 15 % fewer VALU instructions (no 64-bit address math, no packed-bool bookkeeping, shared depth reciprocal).
-// Only SoA planes (Region ps = 1) and K <= kLeanK take this path (launch_spatial checks).
+// The lean N = 1 / 2 passes (k_spatial1_ntl, k_spatial1h, k_spatial2_ntl, k_spatial1u): the arithmetic and RNG slots of
+// spatial_pixel, laid out for a short VALU stream -- 32-bit byte offsets from the plane bases, neighbour clamping by
+// v_med3, one shared double reciprocal of the pixel's depth for the depth tests, a fully unrolled consume sequence
+// behind branches the wave skips when no lane accepted that neighbour.  SoA planes (Region ps = 1), K <= kLeanK.
 constexpr uint32_t kLeanK = 5;
 
 template <class T>
@@ -1348,101 +709,6 @@ struct Comb1 {
         return acc;
     }
 };
-
-template <bool DBG>
-__device__ __forceinline__ void spatial1_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
-                                               v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
-                                               const float4* __restrict__ ia, const float4* __restrict__ ib,
-                                               float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
-                                               const float* __restrict__ rp_in, float* __restrict__ rp_out,
-                                               uint32_t x, uint32_t y, const GlTabs& tb) {
-    const uint32_t K = f.K;   // <= kLeanK (host check)
-    const int rx = (int)(x - rg.vx0), ry = (int)(y - rg.vy0);
-    const uint32_t pofs = ((uint32_t)ry * rg.vw + (uint32_t)rx) << 4;
-    const float4 cn = ld_at(n_t, pofs), cpm = ld_at(p_mat, pofs);
-    const float4 ca = ld_at(ia, pofs), cb = ld_at(ib, pofs);
-    // clamp to the image (render_utils.cpp:109-110), then to the stored view; view-relative coordinates
-    const int xlo = max(0, (int)rg.vx0) - (int)rg.vx0, xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1 - (int)rg.vx0;
-    const int ylo = max(0, (int)rg.vy0) - (int)rg.vy0, yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1 - (int)rg.vy0;
-    const uint32_t ps = pix_state(key, y * rg.W + x);
-    const uint32_t span = 2u * f.R + 1u;
-    const int bx = rx - (int)f.R, by = ry - (int)f.R;
-    uint32_t qo[kLeanK];
-    float4 g[kLeanK];
-#pragma unroll
-    for (uint32_t n = 0; n < kLeanK; n++) {
-        qo[n] = pofs;
-        if (n < K) {
-            const int nx = min(max(bx + (int)__umulhi(draw(ps, 2u * n), span), xlo), xhi);
-            const int ny = min(max(by + (int)__umulhi(draw(ps, 2u * n + 1u), span), ylo), yhi);
-            qo[n] = ((uint32_t)ny * rg.vw + (uint32_t)nx) << 4;
-            g[n] = ld_at(n_t, qo[n]);
-        }
-    }
-    float4 na[kLeanK], nb[kLeanK];
-    // pixel shading context (material + view vector) while the neighbour records are in flight
-    const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
-    // A primary-ray miss (value-initialised HitInfo: material kd = ks = 0, normal 0, P not NaN): its zero normal
-    // rejects every neighbour (finite neighbour normals, s.normals_bounded: dot = +-0 < 0.906), and the target
-    // pdf of any finite-colour sample there is exactly 0, so the combine takes only the pixel's
-    // own reservoir with w = (0 * W) * M = +-0 (W finite): no sample is accepted, wSum stays FLT_MIN, M = M_own,
-    // W = 0.  The pass's result for such a lane is known without its target pdfs.
-    if (cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z) &&
-        __builtin_isfinite(ca.w) && __builtin_isfinite(cb.x + cb.y + cb.z)) {
-        st_at(oa, pofs, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-        st_at(ob, pofs, make_float4(0.0f, 0.0f, 0.0f, cb.w));
-        if (DBG) st_at(odbg, pofs >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
-        if (rp_out) st_at(rp_out, pofs >> 2, 0.0f);
-        return;
-    }
-    // depth / normal heuristic (render_utils.cpp:114-118): one shared reciprocal of the pixel's depth
-    const double rt = rcp_d(cur.t);
-    const bool rt_ok = div_fast_ok(cur.t);
-    bool ok[kLeanK];
-#pragma unroll
-    for (uint32_t n = 0; n < kLeanK; n++) {
-        ok[n] = false;
-        if (n < K) {
-            const float nd = vdot(xyz(g[n]), cur.N);
-            bool rej = nd < 0.90630778703f;
-            if (!rej) {
-                float q = div_by_rcp_d(g[n].w, rt);
-                if (!rt_ok) q = g[n].w / cur.t;
-                rej = fabsf(1.0f - q) > 0.1f;
-            }
-            ok[n] = !rej;
-        }
-    }
-    // accepted neighbours' reservoirs, one neighbour ahead of the consume sequence (two in flight: 16 VGPRs
-    // instead of 40 for the whole batch, which keeps the kernel at 91 VGPRs = 5 waves per SIMD)
-    if (ok[0]) { na[0] = ld_at(ia, qo[0]); nb[0] = ld_at(ib, qo[0]); }
-    // the pixel's own sample is consumed last; its target pdf does not depend on the stream, and when the
-    // input's producer stored it (the pdf cache rp: same pixel, same G-buffer, same sample) it is read back
-    const float pd_cur = rp_in ? ld_at(rp_in, pofs >> 2) : target_pdf(s, f, cur, xyz(ca), xyz(cb), tb);
-    Comb1 cmb;
-    cmb.pos = mk(0.0f, 0.0f, 0.0f); cmb.col = mk(0.0f, 0.0f, 0.0f);
-    cmb.wsum = ROMIS_FLT_MIN; cmb.chosen = 0.0f; cmb.pd = 0.0f; cmb.macc = 0u; cmb.has_pd = false;
-    cmb.h = ps + 2u * K * 0x9E3779B9u;
-#pragma unroll
-    for (uint32_t n = 0; n < kLeanK; n++) {
-        if (n + 1 < kLeanK && ok[n + 1]) { na[n + 1] = ld_at(ia, qo[n + 1]); nb[n + 1] = ld_at(ib, qo[n + 1]); }
-        if (ok[n]) {
-            const v3 p = xyz(na[n]), c = xyz(nb[n]);
-            cmb.take(target_pdf(s, f, cur, p, c, tb), na[n].w, __float_as_uint(nb[n].w), p, c);
-        }
-    }
-    cmb.take(pd_cur, ca.w, __float_as_uint(cb.w), xyz(ca), xyz(cb));
-    // finish_biased: M = routed sum, W from the held sample's target pdf (light.cpp:90-93 / reservoir.cpp:61-64)
-    // nothing accepted: the held sample is the initial (0, 0) one, whose shaded value is +-0 at any pixel with
-    // a non-NaN position (zero colour; NaN terms are zeroed; d >= 1e-5 or d = 1), so W = 0 (reservoir.cpp:62)
-    float p = cmb.pd;
-    if (!cmb.has_pd) p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, cmb.pos, cmb.col, tb);
-    const float W = contribution_weight(p, cmb.macc, cmb.wsum);
-    st_at(oa, pofs, make_float4(cmb.pos.x, cmb.pos.y, cmb.pos.z, W));
-    st_at(ob, pofs, make_float4(cmb.col.x, cmb.col.y, cmb.col.z, __uint_as_float(cmb.macc)));
-    if (DBG) st_at(odbg, pofs >> 1, make_float2(cmb.wsum, cmb.chosen));
-    if (rp_out) st_at(rp_out, pofs >> 2, p);
-}
 
 #ifndef ROMIS_TAB_DMA
 #define ROMIS_TAB_DMA 1   // the biased passes stage powf's tables by LDS-DMA behind their own loads (gl_stage_tables_dma)
@@ -1520,20 +786,6 @@ __device__ __forceinline__ uint32_t tile_flag_at(const MissTiles& mt, const Regi
     return mt.flags[((uint32_t)(y - (int)rg.vy0) / kTileH) * ntxv + (uint32_t)(x - (int)rg.vx0) / kTileW];
 }
 
-template <bool DBG>
-__device__ __forceinline__ void spatial1_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
-                                              v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
-                                              const float4* __restrict__ ia, const float4* __restrict__ ib,
-                                              float4* __restrict__ oa, float4* __restrict__ ob, float2* __restrict__ odbg,
-                                              const float* __restrict__ rp_in, float* __restrict__ rp_out) {
-    // 32x8 tiles in the XCD order above, one per block; waves of 8x8 pixels (rg.map2d = 2)
-    uint32_t tile, x, y;
-    size_t p;
-    const GlTabs tb = gl_stage_tables();
-    if (xcd_tile(rg, num_tiles(rg), blockIdx.x, tile) && tile_pixel_of(rg, tile, x, y, p))
-        spatial1_pixel<DBG>(s, rg, f, key, origin, n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out, x, y, tb);
-}
-
 // ---------------------------------------------------------------------------------------------------------
 // Screen-tile staging for the N = 1 / 2 biased passes: the tile's neighbourhood window, R <= kLdsSpatialR (host check).
 // (Round 4 removed k_spatial1_lds / k_spatial1_ldsr, which staged the reservoirs too -- 70 / 46 KB per block, measured
@@ -1541,16 +793,11 @@ __device__ __forceinline__ void spatial1_body(const SceneDev& s, const Region& r
 constexpr uint32_t kLdsSpatialR = 10;
 constexpr uint32_t kApronMax = (kTileW + 2u * kLdsSpatialR) * (kTileH + 2u * kLdsSpatialR);   // 1456 px
 
-// k_spatial1_ntl: the N = 1 biased pass with only the tile's n_t neighbourhood staged in LDS.  The rocprof
-// counters of k_spatial1 (profiles/r2/r2q) put its bound in the vector-memory pipeline, not in HBM or VALU:
-// TA busy 66 %, TD busy 76 %, TA address path stalled by the L1 40 % of the time -- each 16-byte gather
-// instruction touches ~50 distinct 128-byte lines (one TA/L1 cycle each), against 8 for a coalesced one.
-// The five neighbour n_t gathers are the only ones every lane issues (the reservoir gathers follow only the
-// accepted neighbours), so they are the ones replaced: the block copies the (32 + 2R) x (8 + 2R) n_t window
-// (23 KB at R = 10, 6 blocks per CU) with row-coalesced LDS-DMA loads (global_load_lds_dwordx4: no VGPR staging,
-// no ds_write pass), issued together with the pixel's own records; the powf tables are staged in the same phase,
-// so the block passes one barrier (81.3-82.5 -> 81.3 us in kbench, profiles/r2/glds).  The accepted neighbours' reservoirs stay global gathers, one neighbour ahead of the consume sequence (as in
-// spatial1_pixel).  Same arithmetic, RNG slots and update order as spatial1_pixel; R <= kLdsSpatialR.
+// k_spatial1_ntl: the N = 1 biased pass with the tile's n_t neighbourhood staged in LDS: the block copies the
+// (32 + 2R) x (8 + 2R) n_t window (23 KB at R = 10) with row-coalesced LDS-DMA loads issued with the pixel's own
+// records, so the heuristic's five neighbour records are ds_reads, not 16-byte gathers (each touching ~50 distinct
+// 128-byte lines).  The accepted neighbours' reservoirs stay global gathers, one neighbour ahead of
+// the consume sequence (k_spatial1h reads sample handles from LDS instead, point-light scenes).  R <= kLdsSpatialR.
 // The n_t window of an ntl spatial block: the tile grown by R, clipped, AW entries per row, copied to LDS by
 // LDS-DMA.  Each wave's 64 consecutive window entries l_nt[256k + 64w + lane] are written straight from global
 // memory (global_load_lds_dwordx4, lane l at the wave-uniform base + 16 l), no VGPR round trip; the caller waits
@@ -1684,7 +931,10 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     if (!live) return;   // no barrier follows
     const float4 cn = l_nt[(uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0)];
     const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
-    // primary-ray miss: the pass's result is known (spatial1_pixel)
+    // A primary-ray miss (value-initialised HitInfo: material kd = ks = 0, normal 0, P not NaN): its zero normal
+    // rejects every neighbour (finite neighbour normals, s.normals_bounded: dot = +-0 < 0.906), and the target pdf of
+    // any finite-colour sample there is exactly 0, so the combine takes only the pixel's own reservoir
+    // with w = (0 * W) * M = +-0 (W finite): nothing is accepted, wSum stays FLT_MIN, M = M_own, W = 0.
     if (cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z) &&
         __builtin_isfinite(ca.w) && __builtin_isfinite(cb.x + cb.y + cb.z)) {
         st_at(oa, pofs, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
@@ -1987,8 +1237,7 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
 #define ROMIS_SPATIAL1H_WPE 5
 #endif
 #define ROMIS_SPATIAL1H_KERNEL(DBG, TH, NAME)                                                                          \
-    extern "C" __global__ __launch_bounds__(256 * TH)                                                                 \
-    __attribute__((amdgpu_waves_per_eu(TH >= 3 ? 8 : ROMIS_SPATIAL1H_WPE))) void                                      \
+    extern "C" __global__ __launch_bounds__(256 * TH) __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL1H_WPE))) void   \
     NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
          const float4* p_mat, HandlesIn hi, float4* oa, float4* ob, float2* odbg, const float* rp_in, float* rp_out,  \
          float* how, uint32_t* hom, MissTiles mt) {                                                                   \
@@ -1998,10 +1247,7 @@ ROMIS_SPATIAL1H_KERNEL(false, 1, k_spatial1h)
 ROMIS_SPATIAL1H_KERNEL(true, 1, k_spatial1h_dbg)
 ROMIS_SPATIAL1H_KERNEL(false, 2, k_spatial1h_t2)
 ROMIS_SPATIAL1H_KERNEL(true, 2, k_spatial1h_t2_dbg)
-ROMIS_SPATIAL1H_KERNEL(false, 3, k_spatial1h_t3)
-ROMIS_SPATIAL1H_KERNEL(true, 3, k_spatial1h_t3_dbg)
-ROMIS_SPATIAL1H_KERNEL(false, 4, k_spatial1h_t4)
-ROMIS_SPATIAL1H_KERNEL(true, 4, k_spatial1h_t4_dbg)
+
 
 // k_spatial2_ntl: the biased pass for N = 2 sub-reservoirs (the reference's default, common.h:105), laid out like
 // k_spatial1_ntl (32x8 tiles in the XCD chunk order, the n_t window in LDS by LDS-DMA, one shared depth
@@ -2117,7 +1363,7 @@ __device__ __forceinline__ void spatialn_ntl_body(const SceneDev& s, const Regio
     if (!live) return;   // no barrier follows
     const float4 cn = l_nt[(uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0)];
     const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
-    // primary-ray miss (see spatial1_pixel): every neighbour is rejected and every own input weighs (0 W) M = +-0,
+    // primary-ray miss (see spatial1_ntl_body): every neighbour is rejected and every own input weighs (0 W) M = +-0,
     // so both go to sub-reservoir 0 (equal wSums FLT_MIN), nothing is accepted: M_0 = sum of the own Ms, W = 0
     bool miss = cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z);
 #pragma unroll
@@ -2197,17 +1443,6 @@ __device__ __forceinline__ void spatialn_ntl_body(const SceneDev& s, const Regio
 ROMIS_SPATIALN_NTL_KERNEL(false, 2, k_spatial2_ntl)
 ROMIS_SPATIALN_NTL_KERNEL(true, 2, k_spatial2_ntl_dbg)
 
-#define ROMIS_SPATIAL1_KERNEL(DBG, NAME)                                                                              \
-    extern "C" __global__ __launch_bounds__(256) ROMIS_SPATIAL1_ATTR void NAME(SceneDev s, Region rg, FeaturesDev f,     \
-                                                                            uint32_t key, float ox, float oy, float oz, \
-                                                                            const float4* n_t, const float4* p_mat,     \
-                                                                            const float4* ia, const float4* ib,         \
-                                                                            float4* oa, float4* ob, float2* odbg,       \
-                                                                            const float* rp_in, float* rp_out) {        \
-        spatial1_body<DBG>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);           \
-    }
-ROMIS_SPATIAL1_KERNEL(false, k_spatial1)
-ROMIS_SPATIAL1_KERNEL(true, k_spatial1_dbg)
 
 // ---------------------------------------------------------------------------------------------------------
 // k_spatial1u: the N = 1 unbiased pass (combineUnbiased, reservoir.cpp:68-104; C5 runs it with visibility reuse).
@@ -2721,691 +1956,14 @@ extern "C" __global__ __launch_bounds__(256) void k_read_stream(const float4* __
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// R-MIS / R-OMIS (renderRMIS / renderROMIS, render.cpp:64-265).  Whole images: the view is the W x H image and
-// pixel index p = y * W + x; reservoir planes [N][pixels], neighbourhoods in MIS_NBR, accumulators in MIS_ACC
-// (include/restir_c.h RESTIR_BUF_MIS_*).  One lane per pixel; the per-pixel loops follow the reference's order.
-
-// HitInfo::geometryId: the mesh index (rtcAttachGeometry order, embree_interface.cpp:46-47; one material per mesh);
-// a primary miss keeps genPrimaryRayHits' value-initialised HitInfo (render_utils.cpp:15): 0.
-__device__ __forceinline__ uint32_t geom_id_of(const SceneDev& s, float4 pm) {
-    const uint32_t m = __float_as_uint(pm.w);
-    return m + 1u >= s.num_materials ? 0u : m;
-}
-
-// areSimilar (neighbour_selection.cpp:7-22), lhs = the canonical pixel; the normal test compares the dot product
-// with the radians field, as the reference does (maxDiffCos is computed and unused)
-__device__ __forceinline__ bool are_similar(const SceneDev& s, const FeaturesDev& f, float4 ln, uint32_t lg, float4 rn,
-                                            float4 rp) {
-    if (f.same_geom && lg != geom_id_of(s, rp)) return false;
-    const float depthFracDiff = fabsf(1.0f - (ln.w / rn.w));
-    if (depthFracDiff > f.depth_frac) return false;
-    const float normalsDotProd = vdot(xyz(ln), xyz(rn));
-    if (normalsDotProd < f.normal_rad) return false;
-    return true;
-}
-
-struct MisWin { int x0, y0, x1, y1; };
-
-// indicesSimilarity's window walk (y outer, x inner, the pixel itself skipped) appending one class (similar 1 /
-// dissimilar 0): all members, or std::sample's selection sampling of `want` of the class's `len` members (member i
-// kept iff U{0..len-1-i}, keyed slot i, < the number still needed)
-__device__ uint32_t mis_emit_class(const SceneDev& s, const FeaturesDev& f, const float4* __restrict__ n_t,
-                                   const float4* __restrict__ p_mat, uint32_t W, MisWin w, uint32_t p, float4 cn,
-                                   uint32_t cg, int cls, uint64_t len, uint64_t want, bool take_all, uint32_t ps,
-                                   uint32_t* __restrict__ nbr, size_t npx, uint32_t n) {
-    uint64_t needed = take_all ? len : (want < len ? want : len);
-    uint64_t i = 0;
-    for (int ny = w.y0; ny <= w.y1 && needed; ny++) {
-        for (int nx = w.x0; nx <= w.x1 && needed; nx++) {
-            const uint32_t q = (uint32_t)ny * W + (uint32_t)nx;
-            if (q == p || (int)are_similar(s, f, cn, cg, n_t[q], p_mat[q]) != cls) continue;
-            const bool keep = take_all || (uint64_t)uniform_index(draw(ps, (uint32_t)i), (uint32_t)(len - i)) < needed;
-            if (keep) { nbr[(size_t)(1u + n) * npx + p] = q; n++; needed--; }
-            i++;
-        }
-    }
-    return n;
-}
-
-// The same walk over the count pass's similarity bits (window member m = bit m, LDS word m / 32 of the lane, stride
-// 256): windows of up to kMisMaskBits members skip re-evaluating areSimilar in the emit passes.
-constexpr uint32_t kMisMaskWords = 14, kMisMaskBits = 32u * kMisMaskWords;   // 448 >= (2 * 10 + 1)^2 - 1
-__device__ uint32_t mis_emit_class_mask(const uint32_t* __restrict__ mask, uint32_t W, MisWin w, uint32_t p, int cls,
-                                        uint64_t len, uint64_t want, bool take_all, uint32_t ps,
-                                        uint32_t* __restrict__ nbr, size_t npx, uint32_t n) {
-    uint64_t needed = take_all ? len : (want < len ? want : len);
-    uint64_t i = 0;
-    uint32_t m = 0;
-    for (int ny = w.y0; ny <= w.y1 && needed; ny++) {
-        for (int nx = w.x0; nx <= w.x1 && needed; nx++) {
-            const uint32_t q = (uint32_t)ny * W + (uint32_t)nx;
-            if (q == p) continue;
-            const int sim = (int)((mask[(m >> 5) * 256u] >> (m & 31u)) & 1u);
-            m++;
-            if (sim != cls) continue;
-            const bool keep = take_all || (uint64_t)uniform_index(draw(ps, (uint32_t)i), (uint32_t)(len - i)) < needed;
-            if (keep) { nbr[(size_t)(1u + n) * npx + p] = q; n++; needed--; }
-            i++;
-        }
-    }
-    return n;
-}
-
-// generateResampleIndicesGrid (neighbour_selection.cpp:107-122): nbr[0][p] = neighbourhood size, nbr[1 + i][p] = its
-// i-th pixel (the pixel itself first).  indicesRandom (:24-43) / indicesSimilarity (:45-105) with the reference's
-// size arithmetic (Dissimilar: `k - similar.size()` as size_t; EqualSimilarDissimilar in uint32_t).
-extern "C" __global__ __launch_bounds__(256) void k_mis_neighbours(SceneDev s, uint32_t W, uint32_t H, FeaturesDev f,
-                                                                  uint32_t key_s, uint32_t key_d,
-                                                                  const float4* __restrict__ n_t,
-                                                                  const float4* __restrict__ p_mat,
-                                                                  uint32_t* __restrict__ nbr) {
-    __shared__ uint32_t s_mask[kMisMaskWords * 256u];
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= W * H) return;
-    const size_t npx = (size_t)W * H;
-    const int x = (int)(p % W), y = (int)(p / W), rc = (int)f.R;
-    const uint32_t k = f.K;
-    const uint32_t ps_s = pix_state(key_s, p), ps_d = pix_state(key_d, p);
-    const MisWin w = {max(x - rc, 0), max(y - rc, 0), min(x + rc, (int)W - 1), min(y + rc, (int)H - 1)};
-    nbr[npx + p] = p;
-    uint32_t n = 1;
-    if (f.strategy == RESTIR_NEIGHBOURS_RANDOM) {
-        for (uint32_t c = 0; c < k; c++) {
-            const uint32_t nx = (uint32_t)w.x0 + uniform_index(draw(ps_s, 2u * c), (uint32_t)(w.x1 - w.x0 + 1));
-            const uint32_t ny = (uint32_t)w.y0 + uniform_index(draw(ps_s, 2u * c + 1u), (uint32_t)(w.y1 - w.y0 + 1));
-            nbr[(size_t)(1u + n) * npx + p] = ny * W + nx;
-            n++;
-        }
-    } else {
-        const float4 cn = n_t[p];
-        const uint32_t cg = geom_id_of(s, p_mat[p]);
-        uint32_t* mask = s_mask + threadIdx.x;
-        const bool use_mask = (uint32_t)((w.x1 - w.x0 + 1) * (w.y1 - w.y0 + 1)) - 1u <= kMisMaskBits;
-        uint64_t S = 0, D = 0;
-        uint32_t m = 0, word = 0;
-        for (int ny = w.y0; ny <= w.y1; ny++)
-            for (int nx = w.x0; nx <= w.x1; nx++) {
-                const uint32_t q = (uint32_t)ny * W + (uint32_t)nx;
-                if (q == p) continue;
-                const bool sim = are_similar(s, f, cn, cg, n_t[q], p_mat[q]);
-                if (sim) S++; else D++;
-                if (use_mask) {
-                    word |= (uint32_t)sim << (m & 31u);
-                    if ((m & 31u) == 31u) { mask[(m >> 5) * 256u] = word; word = 0; }
-                }
-                m++;
-            }
-        if (use_mask && (m & 31u)) mask[(m >> 5) * 256u] = word;
-        // emit one class: from the stored bits, or by re-evaluating areSimilar for windows past kMisMaskBits
-        auto emit = [&](int cls, uint64_t len, uint64_t want, bool take_all, uint32_t ps, uint32_t n0) {
-            return use_mask ? mis_emit_class_mask(mask, W, w, p, cls, len, want, take_all, ps, nbr, npx, n0)
-                            : mis_emit_class(s, f, n_t, p_mat, W, w, p, cn, cg, cls, len, want, take_all, ps, nbr, npx, n0);
-        };
-        if (f.strategy == RESTIR_NEIGHBOURS_SIMILAR) {
-            if (S < k) {
-                n = emit(1, S, 0, true, ps_s, n);
-                n = emit(0, D, (uint64_t)k - S, false, ps_d, n);
-            } else {
-                n = emit(1, S, k, false, ps_s, n);
-            }
-        } else if (f.strategy == RESTIR_NEIGHBOURS_DISSIMILAR) {
-            if (D < k) {
-                n = emit(0, D, 0, true, ps_d, n);
-                n = emit(1, S, (uint64_t)k - S, false, ps_s, n);
-            } else {
-                n = emit(0, D, k, false, ps_d, n);
-            }
-        } else {   // EqualSimilarDissimilar (uint32_t arithmetic as written, neighbour_selection.cpp:87-95)
-            uint32_t sS = min((k / 2u) + 1u, (uint32_t)S);
-            const uint32_t desired = k - sS;
-            if ((uint64_t)desired > D) sS = (uint32_t)((uint64_t)sS + ((uint64_t)k - D - sS));
-            n = emit(1, S, sS, false, ps_s, n);
-            n = emit(0, D, (uint32_t)(k - sS), false, ps_d, n);
-        }
-    }
-    nbr[p] = n;
-}
-
-// One R-MIS iteration (render.cpp:76-112): acc[3][pixels] += the pixel's estimate over its neighbourhood.
-template <bool LDS_BVH>
-__device__ __forceinline__ void rmis_body(const SceneDev& s, uint32_t W, uint32_t H, const FeaturesDev& f, v3 origin,
-                                          const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
-                                          const uint32_t* __restrict__ nbr, const float4* __restrict__ ra,
-                                          const float4* __restrict__ rb, float* __restrict__ acc) {
-    const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= W * H) return;
-    const size_t npx = (size_t)W * H;
-    const uint32_t N = f.N;
-    const Px cur = make_px(s, n_t[p], p_mat[p], origin, p);
-    const uint32_t c = nbr[p];
-    v3 fc = mk(0.0f, 0.0f, 0.0f);
-    for (uint32_t i = 0; i < c; i++) {
-        const uint32_t q = nbr[(size_t)(1u + i) * npx + p];
-        for (uint32_t j = 0; j < N; j++) {
-            const float4 a = ra[(size_t)j * npx + q], b = rb[(size_t)j * npx + q];
-            const v3 pos = xyz(a), col = xyz(b);
-            float misWeight;
-            if (f.mis_weight == RESTIR_MIS_EQUAL) {
-                misWeight = 1.0f / (float)c;
-            } else {   // generalisedBalanceHeuristic (render_utils.cpp:179-187)
-                const float numerator = target_pdf(s, f, cur, pos, col);
-                float denominator = ROMIS_FLT_MIN;
-                for (uint32_t i2 = 0; i2 < c; i2++) {
-                    const uint32_t q2 = nbr[(size_t)(1u + i2) * npx + p];
-                    denominator += target_pdf(s, f, make_px(s, n_t[q2], p_mat[q2], origin, q2), pos, col);
-                }
-                misWeight = numerator / denominator;
-            }
-            v3 sc = visible(bvh, cur.P, pos) ? shade(s, f, cur, pos, col) : mk(0.0f, 0.0f, 0.0f);
-            const v3 t = vscale(vscale(sc, misWeight), a.w);   // misWeight * sampleColor * outputWeight
-            fc = vadd(fc, mk(t.x / (float)N, t.y / (float)N, t.z / (float)N));
-        }
-    }
-    acc[p] += fc.x;
-    acc[npx + p] += fc.y;
-    acc[2 * npx + p] += fc.z;
-}
-
-extern "C" __global__ __launch_bounds__(256) void k_rmis_accum(SceneDev s, uint32_t W, uint32_t H, FeaturesDev f, float ox,
-                                                              float oy, float oz, const float4* n_t, const float4* p_mat,
-                                                              const uint32_t* nbr, const float4* ra, const float4* rb,
-                                                              float* acc) {
-    rmis_body<false>(s, W, H, f, mk(ox, oy, oz), n_t, p_mat, nbr, ra, rb, acc);
-}
-extern "C" __global__ __launch_bounds__(256) void k_rmis_accum_lds(SceneDev s, uint32_t W, uint32_t H, FeaturesDev f,
-                                                                  float ox, float oy, float oz, const float4* n_t,
-                                                                  const float4* p_mat, const uint32_t* nbr,
-                                                                  const float4* ra, const float4* rb, float* acc) {
-    rmis_body<true>(s, W, H, f, mk(ox, oy, oz), n_t, p_mat, nbr, ra, rb, acc);
-}
-
-// ---- Eigen 3 CompleteOrthogonalDecomposition<MatrixXf>::solve (render_utils.h:52) ---------------------------
-// ColPivHouseholderQR::computeInPlace (ColPivHouseholderQR.h:482-571), CompleteOrthogonalDecomposition::
-// computeInPlace / _solve_impl / applyZAdjointOnTheLeftInPlace (CompleteOrthogonalDecomposition.h:430-560),
-// makeHouseholder / applyHouseholderOnTheLeft / OnTheRight (Householder.h), HouseholderSequence::applyThisOnTheLeft
-// (HouseholderSequence.h:369-412) and the one-panel upper back substitution, with Eigen's SIMD reduction orders
-// (bit-exact with the reference's Eigen on tests/golden/cod_fixtures.json); correctly rounded sqrt / division.
-// Eigen's reductions with SSE2 Packet4f arithmetic (the reference's x86-64 build; no FMA), as oracle/restir_oracle.c
-// restates them: redux = DenseBase::redux with alignedStart 0 (first packet loaded, a second for 8+ elements, then
-// the tail; n < 4 in order), gemv = one row of the row-major general_matrix_vector_product (a zeroed packet over
-// the 4-blocks, then the tail); predux(p) = (p0 + p2) + (p1 + p3).
-__device__ __forceinline__ float cod_dot_redux(const float* a, const float* b, int n) {
-    if (n < 4) {
-        float r = a[0] * b[0];
-        for (int i = 1; i < n; i++) r = r + a[i] * b[i];
-        return r;
-    }
-    float p[4], q[4];
-    const int full = n / 4 * 4, end2 = n / 8 * 8;
-    for (int l = 0; l < 4; l++) p[l] = a[l] * b[l];
-    if (full > 4) {
-        for (int l = 0; l < 4; l++) q[l] = a[4 + l] * b[4 + l];
-        for (int i = 8; i < end2; i += 8)
-            for (int l = 0; l < 4; l++) {
-                p[l] = p[l] + a[i + l] * b[i + l];
-                q[l] = q[l] + a[i + 4 + l] * b[i + 4 + l];
-            }
-        for (int l = 0; l < 4; l++) p[l] = p[l] + q[l];
-        if (full > end2)
-            for (int l = 0; l < 4; l++) p[l] = p[l] + a[end2 + l] * b[end2 + l];
-    }
-    float r = (p[0] + p[2]) + (p[1] + p[3]);
-    for (int i = full; i < n; i++) r = r + a[i] * b[i];
-    return r;
-}
-__device__ __forceinline__ float cod_dot_gemv(const float* a, const float* b, int n) {
-    float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    int j = 0;
-    for (; j + 4 <= n; j += 4)
-        for (int l = 0; l < 4; l++) c[l] = c[l] + a[j + l] * b[j + l];
-    float r = (c[0] + c[2]) + (c[1] + c[3]);
-    for (; j < n; j++) r = r + a[j] * b[j];
-    return r;
-}
-// squaredNorm: vectorised over a contiguous segment, in index order over a strided row
-__device__ __forceinline__ float cod_sqnorm(const float* v, int n, int stride) {
-    if (stride == 1) return cod_dot_redux(v, v, n);
-    float s = v[0] * v[0];
-    for (int i = 1; i < n; i++) s = s + v[i * stride] * v[i * stride];
-    return s;
-}
-__device__ __forceinline__ void cod_make_householder(float* v, int m, int stride, float& tau, float& beta) {
-    const float tailSqNorm = m == 1 ? 0.0f : cod_sqnorm(v + stride, m - 1, stride);
-    const float c0 = v[0];
-    if (tailSqNorm <= ROMIS_FLT_MIN) {
-        tau = 0.0f;
-        beta = c0;
-        for (int i = 1; i < m; i++) v[i * stride] = 0.0f;
-    } else {
-        float b = sqrtf(c0 * c0 + tailSqNorm);
-        if (c0 >= 0.0f) b = -b;
-        for (int i = 1; i < m; i++) v[i * stride] = v[i * stride] / (c0 - b);
-        tau = (b - c0) / b;
-        beta = b;
-    }
-}
-// tmp = essential^* bottom: a row-major GEMV in the QR sweep (COD_HH_GEMV), an inner product when applying Q^* to
-// the right-hand side (COD_HH_DOT), in index order for Z^*'s strided essential rows (COD_HH_SEQ)
-enum { COD_HH_GEMV = 0, COD_HH_DOT = 1, COD_HH_SEQ = 2 };
-__device__ __forceinline__ void cod_householder_left(float* M, int ld, int r0, int c0, int m, int nc, const float* e,
-                                                     int estride, float tau, int kind) {
-    if (m == 1) {
-        for (int j = 0; j < nc; j++) M[r0 + (c0 + j) * ld] *= 1.0f - tau;
-        return;
-    }
-    if (tau == 0.0f) return;
-    for (int j = 0; j < nc; j++) {
-        float* col = &M[(c0 + j) * ld + r0];
-        float t;
-        if (kind == COD_HH_GEMV) {
-            t = cod_dot_gemv(e, col + 1, m - 1);
-        } else if (kind == COD_HH_DOT) {
-            t = cod_dot_redux(e, col + 1, m - 1);
-        } else {
-            t = e[0] * col[1];
-            for (int i = 1; i < m - 1; i++) t = t + e[i * estride] * col[1 + i];
-        }
-        t += col[0];
-        col[0] -= tau * t;
-        for (int i = 0; i < m - 1; i++) col[1 + i] -= (tau * e[i * estride]) * t;
-    }
-}
-// tmp = right * essential: a column-major GEMV, each row summed in index order onto a zeroed accumulator
-__device__ __forceinline__ void cod_householder_right(float* M, int ld, int r0, int c0, int nr, int m, const float* e,
-                                                      int estride, float tau) {
-    if (m == 1) {
-        for (int i = 0; i < nr; i++) M[r0 + i + c0 * ld] *= 1.0f - tau;
-        return;
-    }
-    if (tau == 0.0f) return;
-    for (int i = 0; i < nr; i++) {
-        float t = 0.0f;
-        for (int j = 0; j < m - 1; j++) t = t + M[r0 + i + (c0 + 1 + j) * ld] * e[j * estride];
-        t += M[r0 + i + c0 * ld];
-        M[r0 + i + c0 * ld] -= tau * t;
-        for (int j = 0; j < m - 1; j++) M[r0 + i + (c0 + 1 + j) * ld] -= (tau * t) * e[j * estride];
-    }
-}
-
-// x = the minimum-norm least-squares solution of A x = b; A column-major NN x NN (copied), NN <= 8
-template <int NN>
-__device__ void cod_solve_dev(const float* A, const float* b, float* x) {
-    constexpr int n = NN;
-    float qr[NN * NN], hc[NN], zc[NN], nU[NN], nD[NN], c[NN], y[NN];
-    int tr[NN], perm[NN];
-    for (int i = 0; i < n * n; i++) qr[i] = A[i];
-    for (int k = 0; k < n; k++) { nD[k] = sqrtf(cod_sqnorm(&qr[k * n], n, 1)); nU[k] = nD[k]; }
-    float mx = nU[0];
-    for (int k = 1; k < n; k++) if (nU[k] > mx) mx = nU[k];
-    const float eps = 1.1920928955078125e-07F;
-    const float threshold_helper = (mx * eps) * (mx * eps) / (float)n;
-    const float norm_downdate_threshold = sqrtf(eps);
-    int nonzero = n;
-    float maxpivot = 0.0f;
-    for (int k = 0; k < n; k++) {
-        int bi = k;
-        float bv = nU[k];
-        for (int j = k + 1; j < n; j++) if (nU[j] > bv) { bv = nU[j]; bi = j; }
-        if (nonzero == n && bv * bv < threshold_helper * (float)(n - k)) nonzero = k;
-        tr[k] = bi;
-        if (k != bi) {
-            for (int i = 0; i < n; i++) { const float t = qr[i + k * n]; qr[i + k * n] = qr[i + bi * n]; qr[i + bi * n] = t; }
-            float t = nU[k]; nU[k] = nU[bi]; nU[bi] = t;
-            t = nD[k]; nD[k] = nD[bi]; nD[bi] = t;
-        }
-        float beta;
-        cod_make_householder(&qr[k + k * n], n - k, 1, hc[k], beta);
-        qr[k + k * n] = beta;
-        if (fabsf(beta) > maxpivot) maxpivot = fabsf(beta);
-        cod_householder_left(qr, n, k, k + 1, n - k, n - k - 1, &qr[k + 1 + k * n], 1, hc[k], COD_HH_GEMV);
-        for (int j = k + 1; j < n; j++) {
-            if (nU[j] != 0.0f) {
-                float temp = fabsf(qr[k + j * n]) / nU[j];
-                temp = (1.0f + temp) * (1.0f - temp);
-                temp = temp < 0.0f ? 0.0f : temp;
-                const float ratio = nU[j] / nD[j];
-                const float temp2 = temp * (ratio * ratio);
-                if (temp2 <= norm_downdate_threshold) {
-                    nD[j] = sqrtf(cod_sqnorm(&qr[k + 1 + j * n], n - k - 1, 1));
-                    nU[j] = nD[j];
-                } else {
-                    nU[j] *= sqrtf(temp);
-                }
-            }
-        }
-    }
-    for (int k = 0; k < n; k++) perm[k] = k;
-    for (int k = 0; k < n; k++) { const int t = perm[k]; perm[k] = perm[tr[k]]; perm[tr[k]] = t; }
-    const float pre = fabsf(maxpivot) * (eps * (float)n);
-    int rank = 0;
-    for (int i = 0; i < nonzero; i++) rank += fabsf(qr[i + i * n]) > pre;
-    if (rank < n) {
-        for (int k = rank - 1; k >= 0; k--) {
-            if (k != rank - 1)
-                for (int i = 0; i <= k; i++) { const float t = qr[i + k * n]; qr[i + k * n] = qr[i + (rank - 1) * n]; qr[i + (rank - 1) * n] = t; }
-            float beta;
-            cod_make_householder(&qr[k + (rank - 1) * n], n - rank + 1, n, zc[k], beta);
-            qr[k + (rank - 1) * n] = beta;
-            if (k > 0) cod_householder_right(qr, n, 0, rank - 1, k, n - rank + 1, &qr[k + rank * n], n, zc[k]);
-            if (k != rank - 1)
-                for (int i = 0; i <= k; i++) { const float t = qr[i + k * n]; qr[i + k * n] = qr[i + (rank - 1) * n]; qr[i + (rank - 1) * n] = t; }
-        }
-    }
-    {   // _solve_impl's rank(), over the decomposition's diagonal
-        int r2 = 0;
-        for (int i = 0; i < nonzero; i++) r2 += fabsf(qr[i + i * n]) > pre;
-        rank = r2;
-    }
-    if (rank == 0) { for (int i = 0; i < n; i++) x[i] = 0.0f; return; }
-    for (int i = 0; i < n; i++) c[i] = b[i];
-    for (int k = 0; k < rank; k++) cod_householder_left(c, n, k, 0, n - k, 1, &qr[k + 1 + k * n], 1, hc[k], COD_HH_DOT);
-    for (int i = 0; i < n; i++) y[i] = i < rank ? c[i] : 0.0f;
-    for (int i = rank - 1; i >= 0; i--) {
-        if (y[i] != 0.0f) {
-            y[i] /= qr[i + i * n];
-            for (int j = 0; j < i; j++) y[j] -= y[i] * qr[j + i * n];
-        }
-    }
-    if (rank < n) {
-        for (int k = 0; k < rank; k++) {
-            if (k != rank - 1) { const float t = y[k]; y[k] = y[rank - 1]; y[rank - 1] = t; }
-            cod_householder_left(y, n, rank - 1, 0, n - rank + 1, 1, &qr[k + rank * n], n, zc[k], COD_HH_SEQ);
-            if (k != rank - 1) { const float t = y[k]; y[k] = y[rank - 1]; y[rank - 1] = t; }
-        }
-    }
-    for (int i = 0; i < n; i++) x[perm[i]] = y[i];
-}
-
-// arbitraryUnbiasedContributionWeightReciprocal (render_utils.cpp:245-257)
-__device__ __forceinline__ float aucw_reciprocal(const SceneDev& s, const FeaturesDev& f, const Px& qpx, float M,
-                                                 float wsum, float chosen, v3 pos, v3 col) {
-    const float targetPdfValue = target_pdf(s, f, qpx, pos, col);
-    if (targetPdfValue == 0.0f) return 0.0f;
-    const float mockSampleWeight = targetPdfValue / (1.0f / (float)s.num_lights);
-    const float arbitraryWeight = ((1.0f / targetPdfValue) * (1.0f / M)) * ((wsum - chosen) + mockSampleWeight);
-    return 1.0f / arbitraryWeight;
-}
-
-// One R-OMIS iteration (render.cpp:139-231), split in two launches per chunk of the pixel's T x N samples (the
-// one-lane-per-pixel form held A, b and every sample's per-distribution state at once: 251-260 VGPRs = 1-2 waves per
-// SIMD, its loads a dependent chain per distribution; 24-44 % VALU busy):
-//  - k_romis_samples_t{T}: one lane per (sample, pixel), wave = 64 pixels of one sample slot: the sample's column
-//    vector over the T distributions (arbitraryUnbiasedContributionWeightReciprocal at each distribution pixel) and
-//    its visibility-tested shaded colour -> smp rows [sample][T + 3][pixels];
-//  - k_romis_accum_t{T}[_prog]: one lane per pixel: the progressive colour, scale factor, technique matrix and
-//    contribution vector updates of those samples, in the reference's order, reading them back from smp.
-// Every value is computed by the same operations as in one pass, so the split is bit-exact.
-template <int T, bool LDS_BVH>
-__device__ __forceinline__ void romis_samples_body(const SceneDev& s, uint32_t W, uint32_t H, const FeaturesDev& f,
-                                                   v3 origin, const float4* __restrict__ n_t,
-                                                   const float4* __restrict__ p_mat, const uint32_t* __restrict__ nbr,
-                                                   const float4* __restrict__ ra, const float4* __restrict__ rb,
-                                                   const float2* __restrict__ rdbg, uint32_t s0, uint32_t ns,
-                                                   float* __restrict__ smp) {
-    const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
-    const uint32_t npx = W * H;   // launcher: ns * npx < 2^31
-    const uint32_t N = f.N;
-    const uint32_t items = ns * npx;
-    for (uint32_t it = blockIdx.x * blockDim.x + threadIdx.x; it < items; it += gridDim.x * blockDim.x) {
-        const uint32_t sl = it / npx, p = it - sl * npx;
-        const uint32_t sg = s0 + sl, pi = sg / N, si = sg - pi * N;
-        const uint32_t q = nbr[(size_t)(1u + pi) * npx + p];
-        const float4 a = ra[(size_t)si * npx + q], b4 = rb[(size_t)si * npx + q];
-        const v3 pos = xyz(a), col = xyz(b4);
-        float* out = smp + (size_t)sl * (T + 3) * npx + p;
-        // the T target-pdf evaluations as one rolled loop (one inlined copy of target_pdf)
-#pragma unroll 1
-        for (int d = 0; d < T; d++) {
-            const uint32_t qq = nbr[(size_t)(1 + d) * npx + p];
-            const float4 db = rb[(size_t)si * npx + qq];
-            const float2 dd = rdbg[(size_t)si * npx + qq];
-            out[(size_t)d * npx] = aucw_reciprocal(s, f, make_px(s, n_t[qq], p_mat[qq], origin, qq),
-                                                   (float)__float_as_uint(db.w), dd.x, dd.y, pos, col);
-        }
-        const Px cur = make_px(s, n_t[p], p_mat[p], origin, p);
-        const v3 sc = visible(bvh, cur.P, pos) ? shade(s, f, cur, pos, col) : mk(0.0f, 0.0f, 0.0f);
-        out[(size_t)T * npx] = sc.x;
-        out[(size_t)(T + 1) * npx] = sc.y;
-        out[(size_t)(T + 2) * npx] = sc.z;
-    }
-}
-
-template <int T, bool PROG>
-__device__ __forceinline__ void romis_accum_body(uint32_t W, uint32_t H, const FeaturesDev& f, uint32_t s0, uint32_t ns,
-                                                 const float* __restrict__ smp, float* __restrict__ acc) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= W * H) return;
-    const size_t npx = (size_t)W * H;
-    const uint32_t N = f.N;
-    const int32_t totalSamples = (int32_t)((uint32_t)T * N);
-    const int32_t fractionOfTotalSamples = (int32_t)N / (int32_t)T;
-    float* Am = acc;
-    float* Bv = acc + (size_t)T * T * npx;
-    const float* Al = Bv + (size_t)3 * T * npx;
-    float* Col = Bv + (size_t)6 * T * npx;
-    float A[T * T], bb[3][T], al[3][T];
-#pragma unroll
-    for (int e = 0; e < T * T; e++) A[e] = Am[(size_t)e * npx + p];
-#pragma unroll
-    for (int ch = 0; ch < 3; ch++)
-#pragma unroll
-        for (int i = 0; i < T; i++) {
-            bb[ch][i] = Bv[(size_t)(ch * T + i) * npx + p];
-            if (PROG) al[ch][i] = Al[(size_t)(ch * T + i) * npx + p];
-        }
-    v3 fc = mk(0.0f, 0.0f, 0.0f);
-    if (PROG) fc = mk(Col[p], Col[npx + p], Col[2 * npx + p]);
-    for (uint32_t sl = 0; sl < ns; sl++) {
-        const uint32_t sg = s0 + sl, pi = sg / N, si = sg - pi * N;
-        if (PROG && si == 0u)   // the start of neighbourhood entry pi (render.cpp:156-160)
-            fc = vadd(fc, mk(Al[(size_t)pi * npx + p], Al[(size_t)(T + pi) * npx + p], Al[(size_t)(2 * T + pi) * npx + p]));
-        const float* in = smp + (size_t)sl * (T + 3) * npx + p;
-        float v[T];
-#pragma unroll
-        for (int d = 0; d < T; d++) v[d] = in[(size_t)d * npx];
-        const v3 sc = mk(in[(size_t)T * npx], in[(size_t)(T + 1) * npx], in[(size_t)(T + 2) * npx]);
-        if (PROG) {
-            v3 sa = mk(0.0f, 0.0f, 0.0f);
-            float sf = ROMIS_FLT_MIN;
-#pragma unroll
-            for (int d = 0; d < T; d++) {
-                sa = vadd(sa, vscale(mk(al[0][d], al[1][d], al[2][d]), v[d]));
-                sf += (float)fractionOfTotalSamples * v[d];
-            }
-            const v3 term = vsub(mk(sc.x / sf, sc.y / sf, sc.z / sf), mk(sa.x / sf, sa.y / sf, sa.z / sf));
-            const float inv = 1.0f / (float)totalSamples;
-            fc = vadd(fc, mk(inv * term.x, inv * term.y, inv * term.z));
-        }
-        float scaleFactor = ROMIS_FLT_MIN;
-#pragma unroll
-        for (int d = 0; d < T; d++) scaleFactor += (float)N * v[d];
-        scaleFactor = 1.0f / scaleFactor;
-#pragma unroll
-        for (int d = 0; d < T; d++) v[d] *= scaleFactor;
-#pragma unroll
-        for (int j = 0; j < T; j++)
-#pragma unroll
-            for (int i = 0; i < T; i++) A[i + j * T] += v[i] * v[j];
-#pragma unroll
-        for (int row = 0; row < T; row++) {
-            const float scaleColVecConst = scaleFactor * v[row];
-            bb[0][row] += sc.x * scaleColVecConst;
-            bb[1][row] += sc.y * scaleColVecConst;
-            bb[2][row] += sc.z * scaleColVecConst;
-        }
-    }
-#pragma unroll
-    for (int e = 0; e < T * T; e++) Am[(size_t)e * npx + p] = A[e];
-#pragma unroll
-    for (int ch = 0; ch < 3; ch++)
-#pragma unroll
-        for (int i = 0; i < T; i++) Bv[(size_t)(ch * T + i) * npx + p] = bb[ch][i];
-    if (PROG) { Col[p] = fc.x; Col[npx + p] = fc.y; Col[2 * npx + p] = fc.z; }
-}
-
-// Progressive R-OMIS (render.cpp:148-152): at the start of iteration i >= 1 with i % progressiveUpdateMod == 0, each
-// colour's alpha vector = the least-squares solution over the technique matrix and contribution vector so far.
-template <int T>
-__device__ __forceinline__ void romis_alphas_body(uint32_t W, uint32_t H, float* __restrict__ acc) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= W * H) return;
-    const size_t npx = (size_t)W * H;
-    float A[T * T], bv[T], xv[T];
-    for (int e = 0; e < T * T; e++) A[e] = acc[(size_t)e * npx + p];
-    for (int ch = 0; ch < 3; ch++) {
-        for (int i = 0; i < T; i++) bv[i] = acc[(size_t)(T * T + ch * T + i) * npx + p];
-        cod_solve_dev<T>(A, bv, xv);
-        for (int i = 0; i < T; i++) acc[(size_t)(T * T + 3 * T + ch * T + i) * npx + p] = xv[i];
-    }
-}
-
-// saveAlphasVisualisation (render.cpp:227-229, visualiseAlphas render_utils.cpp:189-243): after an iteration, each
-// colour's alpha vector solved from the sums so far (the sums themselves untouched; progressive alphas live in their
-// own rows).  Technique i, colour ch -> image 3 i + ch; a pixel is glm::mix(0, (1, .5, 0), a) for a > 0 and
-// glm::mix(0, (0, .5, 1), -a) otherwise (x (1 - a) + y a, unfused), stored as Screen::writeBitmapToFile's 8-bit word
-// (clamp to [0, 1], x255, truncate; bytes B, G, R, A = 255).  A bitmap's rows run bottom-up, and Screen::setPixel
-// flips y, so image pixel order = this grid's order (y = 0 bottom): out[(3 i + ch) npx + p].
-__device__ __forceinline__ uint32_t vis_u8(float v) {
-    const float m = (v < 0.0f) ? 0.0f : v;   // glm::clamp: a NaN passes through ...
-    const float c = (1.0f < m) ? 1.0f : m;
-    if (c != c) return 0u;                   // ... and truncates to 0 (screen.cpp's to_u8)
-    return (uint32_t)(int)__fmul_rn(c, 255.0f);
-}
-__device__ __forceinline__ float vis_mix(float y, float a) {
-    return __fadd_rn(__fmul_rn(0.0f, __fsub_rn(1.0f, a)), __fmul_rn(y, a));
-}
-template <int T>
-__device__ __forceinline__ void romis_vis_body(uint32_t W, uint32_t H, const float* __restrict__ acc,
-                                               uint32_t* __restrict__ out) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= W * H) return;
-    const size_t npx = (size_t)W * H;
-    float A[T * T], bv[T], xv[T];
-    for (int e = 0; e < T * T; e++) A[e] = acc[(size_t)e * npx + p];
-    for (int ch = 0; ch < 3; ch++) {
-        for (int i = 0; i < T; i++) bv[i] = acc[(size_t)(T * T + ch * T + i) * npx + p];
-        cod_solve_dev<T>(A, bv, xv);
-        for (int i = 0; i < T; i++) {
-            const float a = xv[i];
-            const bool pos = a > 0.0f;
-            const float m = pos ? a : -a;
-            const float r = vis_mix(pos ? 1.0f : 0.0f, m), g = vis_mix(0.5f, m), b = vis_mix(pos ? 0.0f : 1.0f, m);
-            out[(size_t)(3 * i + ch) * npx + p] = vis_u8(b) | (vis_u8(g) << 8) | (vis_u8(r) << 16) | 0xFF000000u;
-        }
-    }
-}
-
-#define ROMIS_ROMIS_SAMPLES(T, LDS, NAME)                                                                           \
-    extern "C" __global__ __launch_bounds__(256) void NAME(SceneDev s, uint32_t W, uint32_t H, FeaturesDev f, float ox,  \
-                                                          float oy, float oz, const float4* n_t, const float4* p_mat,  \
-                                                          const uint32_t* nbr, const float4* ra, const float4* rb,      \
-                                                          const float2* rdbg, uint32_t s0, uint32_t ns, float* smp) {   \
-        romis_samples_body<T, LDS>(s, W, H, f, mk(ox, oy, oz), n_t, p_mat, nbr, ra, rb, rdbg, s0, ns, smp);             \
-    }
-#define ROMIS_ROMIS_ACCUM(T, PROG, NAME)                                                                             \
-    extern "C" __global__ __launch_bounds__(256) void NAME(uint32_t W, uint32_t H, FeaturesDev f, uint32_t s0,           \
-                                                          uint32_t ns, const float* smp, float* acc) {                 \
-        romis_accum_body<T, PROG>(W, H, f, s0, ns, smp, acc);                                                          \
-    }
-#define ROMIS_ROMIS_KERNELS(T)                                                                                        \
-    ROMIS_ROMIS_SAMPLES(T, false, k_romis_samples_t##T)                                                               \
-    ROMIS_ROMIS_SAMPLES(T, true, k_romis_samples_lds_t##T)                                                            \
-    ROMIS_ROMIS_ACCUM(T, false, k_romis_accum_t##T)                                                                   \
-    ROMIS_ROMIS_ACCUM(T, true, k_romis_accum_prog_t##T)                                                               \
-    extern "C" __global__ __launch_bounds__(256) void k_romis_alphas_t##T(uint32_t W, uint32_t H, float* acc) {         \
-        romis_alphas_body<T>(W, H, acc);                                                                              \
-    }                                                                                                                 \
-    extern "C" __global__ __launch_bounds__(256) void k_romis_vis_t##T(uint32_t W, uint32_t H, const float* acc,        \
-                                                                      uint32_t* out) {                                \
-        romis_vis_body<T>(W, H, acc, out);                                                                            \
-    }                                                                                                                 \
-    extern "C" __global__ __launch_bounds__(256) void k_romis_solve_t##T(uint32_t W, uint32_t H, FeaturesDev f,         \
-                                                                        const float* acc, float* rgb) {               \
-        romis_solve_body<T>(W, H, f, acc, rgb);                                                                        \
-    }                                                                                                                 \
-    extern "C" __global__ __launch_bounds__(256) void k_debug_cod_t##T(const float* A, const float* b, float* x,        \
-                                                                      uint32_t count) {                               \
-        const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;                                                     \
-        if (i >= count) return;                                                                                       \
-        float a[T * T], bv[T], xv[T];                                                                                 \
-        for (int e = 0; e < T * T; e++) a[e] = A[(size_t)i * T * T + e];                                              \
-        for (int e = 0; e < T; e++) bv[e] = b[(size_t)i * T + e];                                                     \
-        cod_solve_dev<T>(a, bv, xv);                                                                                  \
-        for (int e = 0; e < T; e++) x[(size_t)i * T + e] = xv[e];                                                     \
-    }
-
-// Direct R-OMIS screen (render.cpp:234-263): three solves per pixel, component sums, tone map, Screen y-flip.
-template <int T>
-__device__ __forceinline__ void romis_solve_body(uint32_t W, uint32_t H, const FeaturesDev& f, const float* __restrict__ acc,
-                                                 float* __restrict__ rgb) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= W * H) return;
-    const size_t npx = (size_t)W * H;
-    float A[T * T], bv[T], xs[3][T];
-    for (int e = 0; e < T * T; e++) A[e] = acc[(size_t)e * npx + p];
-    for (int ch = 0; ch < 3; ch++) {
-        for (int i = 0; i < T; i++) bv[i] = acc[(size_t)(T * T + ch * T + i) * npx + p];
-        cod_solve_dev<T>(A, bv, xs[ch]);
-    }
-    v3 c = mk(0.0f, 0.0f, 0.0f);
-    for (int row = 0; row < T; row++) { c.x += xs[0][row]; c.y += xs[1][row]; c.z += xs[2][row]; }
-    if (f.tone_map) {
-        const float g = 1.0f / f.gamma;
-        v3 e = vscale(mk(-c.x, -c.y, -c.z), f.exposure);
-        v3 mapped = mk(1.0f - pm_expf(e.x), 1.0f - pm_expf(e.y), 1.0f - pm_expf(e.z));
-        c = mk(pm_powf(mapped.x, g), pm_powf(mapped.y, g), pm_powf(mapped.z, g));
-    }
-    const uint32_t x = p % W, y = p / W;
-    float* o = rgb + 3 * ((size_t)(H - 1u - y) * W + x);
-    o[0] = c.x; o[1] = c.y; o[2] = c.z;
-}
-
-ROMIS_ROMIS_KERNELS(1)
-ROMIS_ROMIS_KERNELS(2)
-ROMIS_ROMIS_KERNELS(3)
-ROMIS_ROMIS_KERNELS(4)
-ROMIS_ROMIS_KERNELS(5)
-ROMIS_ROMIS_KERNELS(6)
-ROMIS_ROMIS_KERNELS(7)
-ROMIS_ROMIS_KERNELS(8)
-
-// combineToScreen (render_utils.cpp:68-85): R-MIS and progressive R-OMIS colour sums / iterations, tone map, y-flip.
-extern "C" __global__ __launch_bounds__(256) void k_mis_combine(uint32_t W, uint32_t H, FeaturesDev f, const float* col,
-                                                               float* rgb) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= W * H) return;
-    const size_t npx = (size_t)W * H;
-    const float it = (float)f.iterations;
-    v3 c = mk(col[p] / it, col[npx + p] / it, col[2 * npx + p] / it);
-    if (f.tone_map) {
-        const float g = 1.0f / f.gamma;
-        v3 e = vscale(mk(-c.x, -c.y, -c.z), f.exposure);
-        v3 mapped = mk(1.0f - pm_expf(e.x), 1.0f - pm_expf(e.y), 1.0f - pm_expf(e.z));
-        c = mk(pm_powf(mapped.x, g), pm_powf(mapped.y, g), pm_powf(mapped.z, g));
-    }
-    const uint32_t x = p % W, y = p / W;
-    float* o = rgb + 3 * ((size_t)(H - 1u - y) * W + x);
-    o[0] = c.x; o[1] = c.y; o[2] = c.z;
-}
-
-// ---------------------------------------------------------------------------------------------------------
 // Host launchers (launch.h)
 #include "launch.h"
-
-#include <hip/hip_ext.h>
+#include "launch_events.h"
 
 #include <mutex>
 #include <set>
 
 namespace romis {
-
-// Timed launches: restir.cpp's TIMED hands a start / stop event pair to the next launch, which records them
-// inside its own dispatch (hipExtLaunchKernelGGL) -- no separate event packets, hence no stream gaps.
-namespace {
-thread_local hipEvent_t g_ev_start = nullptr, g_ev_stop = nullptr;
-thread_local bool g_launched = false;
-}  // namespace
 
 void set_launch_events(hipEvent_t start, hipEvent_t stop) {
     g_ev_start = start;
@@ -3414,25 +1972,12 @@ void set_launch_events(hipEvent_t start, hipEvent_t stop) {
 }
 bool launch_events_used() { return g_launched; }
 
-#define ROMIS_LAUNCH(kernel, grid, block, lds, stream, ...)                                                    \
-    do {                                                                                                      \
-        /* a multi-launch stage: start event on its first kernel, stop event after its last */              \
-        hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, g_launched ? nullptr : g_ev_start, g_ev_stop, 0, \
-                              __VA_ARGS__);                                                                   \
-        g_launched = true;                                                                                    \
-    } while (0)
-
 namespace {
-constexpr uint32_t kBlock = 256;
 static_assert(kTileW * kTileH == kBlock, "one lane per tile pixel");
-constexpr size_t kLdsBudget = 64 * 1024;
 
 inline uint32_t items_of(const Region& rg) {
     return rg.map2d ? ((rg.rw + kTileW - 1) / kTileW) * ((rg.rh + kTileH - 1) / kTileH) : (rg.rw * rg.rh + kBlock - 1) / kBlock;
 }
-// cap = 0: one block per work item; else a persistent grid of at most `cap` blocks
-inline dim3 grid_capped(uint32_t items, uint32_t cap) { return dim3(cap && items > cap ? cap : items); }
-inline size_t bvh_lds_bytes(const SceneDev& s) { return ((size_t)2 * s.num_nodes + (size_t)3 * s.num_tris) * 16; }
 inline size_t lights_lds_bytes(const SceneDev& s) { return (size_t)7 * s.num_lights * 16; }
 // The RIS light-table form (ris_pixel's LT) for this scene and N: the compact tables of the _pt / _grid kernels
 // (N = 1, 2) when the scene's lights allow them and ris.compact is on, else the general records.
@@ -3452,9 +1997,9 @@ inline Region with_map(Region rg, uint32_t map2d) { rg.map2d = map2d; return rg;
 hipError_t launch_primary(const SceneDev& s, const Region& rg0, const CameraDev& cam, float4* n_t, float4* p_mat,
                           float4* n_t2, const Tuning& tu, hipStream_t stream) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
-    const Region rg = with_map(rg0, tu.primary_2d);
+    const Region rg = with_map(rg0, 1u);
     const size_t lds = bvh_lds_bytes(s);
-    const dim3 grid = grid_capped(items_of(rg), tu.primary_blocks);
+    const dim3 grid(items_of(rg));
     if (tu.primary_lds && lds <= kLdsBudget)
         ROMIS_LAUNCH(k_primary_lds, grid, dim3(kBlock), lds, stream, s, rg, cam, n_t, p_mat, n_t2);
     else
@@ -3464,16 +2009,10 @@ hipError_t launch_primary(const SceneDev& s, const Region& rg0, const CameraDev&
 
 hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
                       const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, float* rp,
-                      const Tuning& tu, QueueState& qs, hipStream_t stream) {
+                      const Tuning& tu, hipStream_t stream) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     const Region rg = with_map(rg0, 0);
-    WorkQueue wq{nullptr, 0u};
-    dim3 grid = grid_capped(items_of(rg), tu.ris_blocks);
-    if (tu.ris_queue && qs.ctr) {
-        grid = dim3(std::min(items_of(rg), tu.ris_queue));
-        wq = WorkQueue{qs.ctr, qs.base};
-        qs.base += items_of(rg) + grid.x;
-    }
+    const dim3 grid(items_of(rg));
     const int lt = ris_light_form(s, f, tu);
     const size_t lds = ris_lights_lds_bytes(s, lt);
     const bool staged = tu.ris_lds && s.num_lights > 0 && lds <= kLdsBudget;
@@ -3486,7 +2025,7 @@ hipError_t launch_ris(const SceneDev& s, const Region& rg0, const FeaturesDev& f
                     : (f.N == 1 ? k_ris_n1 : (f.N == 2 ? k_ris_n2 : k_ris_n0));
     const size_t lds_used = lds;
     ROMIS_LAUNCH(k, grid, dim3(kBlock), staged ? lds_used : 0, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ra,
-                       rb, rdbg, f.N == 1 ? rp : nullptr, wq);
+                       rb, rdbg, f.N == 1 ? rp : nullptr);
     return hipGetLastError();
 }
 
@@ -3496,10 +2035,10 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
                               bool* tmiss_written, Handles h) {
     if (tmiss_written) *tmiss_written = false;
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
-    const Region rg = with_map(rg0, tu.primary_2d);
+    const Region rg = with_map(rg0, 1u);
     // MissTiles flags: one 32 x 8 tile per block, N <= 2 (the caller allocates one byte per tile and passes them on
     // only when *tmiss_written)
-    if (!rg.map2d || tu.ris_blocks || f.N > 2) tmiss = nullptr;
+    if (!rg.map2d || f.N > 2) tmiss = nullptr;
     if (tmiss_written) *tmiss_written = tmiss != nullptr;
     const size_t bvh = bvh_lds_bytes(s);
     if (bvh > kLdsBudget) return hipErrorInvalidValue;   // caller checks primary_ris_fits()
@@ -3515,7 +2054,7 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
                                           : (f.N == 1 ? k_primary_ris_n1_pg : k_primary_ris_n2_pg))
            : use_lights ? (f.N == 1 ? k_primary_ris_n1_lds : (f.N == 2 ? k_primary_ris_n2_lds : k_primary_ris_n0_lds))
                         : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
-    ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.ris_blocks), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
+    ROMIS_LAUNCH(k, dim3(items_of(rg)), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
                  cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr, tu.ris_late, tmiss,
                  tmiss ? skip_res : 0u, lt == kLtPoint && f.N == 1 ? h.w : nullptr, lt == kLtPoint && f.N == 1 ? h.m : nullptr);
     return hipGetLastError();
@@ -3525,7 +2064,7 @@ bool primary_ris_fits(const SceneDev& s) { return bvh_lds_bytes(s) <= kLdsBudget
 
 bool spatial_handles_ok(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes) {
     if (!tu.spatial_handles || passes == 0 || f.N != 1 || f.unbiased || f.K > kLeanK || f.R > kLdsSpatialR) return false;
-    if (!tu.spatial_lean || !tu.spatial_xcd || !tu.spatial_wave8 || tu.spatial_lds != 3u || !tu.ris_compact) return false;
+    if (!tu.spatial_lean || !tu.ris_compact) return false;
     if (s.light_types != 1u || s.num_lights == 0 || s.num_lights > 254u) return false;   // point lights; index L = zero
     // every M: RIS M, then each biased pass sums at most K + 1 inputs
     uint64_t m = f.M;
@@ -3537,13 +2076,13 @@ bool spatial_handles_ok(const SceneDev& s, const FeaturesDev& f, const Tuning& t
 // unbiased) for these features and knobs, SoA planes -- the condition for RIS's skip_res
 // launch_final's k_final_n1_sorted writes background tiles from the flags without reading them
 bool final_reads_flags(const SceneDev& s, const FeaturesDev& f, const Tuning& tu) {
-    return f.N == 1 && tu.final_sort && tu.final_lds && tu.final_2d && bvh_lds_bytes(s) <= kLdsBudget;
+    return f.N == 1 && tu.final_sort && tu.final_lds && bvh_lds_bytes(s) <= kLdsBudget;
 }
 
 bool spatial_reads_flags(const SceneDev& s, const FeaturesDev& f, const Tuning& tu) {
-    if (f.N != 1 || f.K > kLeanK || !tu.spatial_lean || !tu.spatial_xcd || !tu.spatial_wave8) return false;
+    if (f.N != 1 || f.K > kLeanK || !tu.spatial_lean) return false;
     if (f.unbiased) return !f.spatial_vis || bvh_lds_bytes(s) <= kLdsBudget;   // k_spatial1u[_vis]
-    return f.R <= kLdsSpatialR && tu.spatial_lds == 3u;                       // k_spatial1_ntl / _t2
+    return f.R <= kLdsSpatialR;                                               // k_spatial1_ntl / _t2, k_spatial1h
 }
 
 hipError_t launch_temporal(const SceneDev& s, const Region& rg0, const FeaturesDev& f, uint32_t key, const float* o,
@@ -3568,8 +2107,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
     if (!mt.flags) mt.m = mt.gbuf = 0u;
     if (vis_written) *vis_written = false;
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
-    Region rg = with_map(rg0, tu.spatial_xcd);   // XCD-banded order works on 2D tiles
-    if (rg.map2d && tu.spatial_wave8) rg.map2d = 2u;
+    Region rg = with_map(rg0, 2u);   // 32 x 8 tiles of 8 x 8 waves (the lean kernels' XCD tile order, xcd_tile)
     uint32_t grid = items_of(rg);
     const size_t bvh_bytes = bvh_lds_bytes(s);
     const bool lean = tu.spatial_lean && f.N == 1 && f.K <= kLeanK && rg.ps == 1u && rg.map2d == 2u &&
@@ -3592,7 +2130,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         if (vis_written) *vis_written = vo != nullptr;
         return hipGetLastError();
     }
-    if (lean2 && !f.unbiased && f.R <= kLdsSpatialR && tu.spatial_lds == 3u) {
+    if (lean2 && !f.unbiased && f.R <= kLdsSpatialR) {
         // N = 2 biased: one block per tile in the XCD chunk order (xcd_tile); spatial.lds != 3 selects the general
         // kernel for A/B runs, as for N = 1.  No pdf cache at N = 2 (*rp_written stays false)
         const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
@@ -3604,7 +2142,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
                      key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, mt);
         return hipGetLastError();
     }
-    if (lean && !f.unbiased) {
+    if (lean && !f.unbiased && f.R <= kLdsSpatialR) {
         // one block per tile (the lean kernels do not loop over tiles, so spatial.blocks does not apply here),
         // grid rounded to the XCD that owns the most tiles (xcd_tile)
         const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW, nty = (rg.rh + kTileH - 1) / kTileH;
@@ -3619,9 +2157,10 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         // 32x16 tiles (k_spatial1_ntl_t2) where the auto XCD chunk is at most 2 tile rows (wide images): C4 222 ->
         // 203 us, C2 76.8 -> 79.0 (cfg_kbench, profiles/r3/r3k); spatial.th = 1 / 2 forces either
         const uint32_t th = tu.spatial_th ? tu.spatial_th : (8192u / std::max(rg.rw, 1u) <= 2u ? 2u : 1u);
-        if (hin.w && tu.spatial_lds == 3u && f.R <= kLdsSpatialR) {
-            // sample handles (k_spatial1h[_tN]): 32 x 8 TH tiles, TH = spatial.th (auto: 2); the XCD chunks hold
-            // xcd_rows tile rows (the automatic count divided by TH)
+        if (hin.w) {
+            // sample handles (k_spatial1h[_t2]): 32 x 8 TH tiles, TH = spatial.th (auto: 2 -- C2 66.9 us against 76.2 for
+            // 32 x 8, 70.6 / 68.4 for 32 x 24 / 32 x 32, kbench, profiles/r5); the XCD chunks hold xcd_rows tile rows
+            // (the automatic count divided by TH)
             const uint32_t hth = tu.spatial_th ? tu.spatial_th : 2u;
             if (hth > 1u) {
                 const uint32_t ntyh = (rg.rh + hth * kTileH - 1) / (hth * kTileH);
@@ -3638,12 +2177,10 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
             }
             const size_t lds = (size_t)h_lds_f4(hth) * 16u + (size_t)(2u * s.num_lights + 2u) * 16u;
             const HandlesIn hi{hin.w, hin.m};
-            auto k = hth == 4u ? (odbg ? k_spatial1h_t4_dbg : k_spatial1h_t4)
-                   : hth == 3u ? (odbg ? k_spatial1h_t3_dbg : k_spatial1h_t3)
-                   : hth == 2u ? (odbg ? k_spatial1h_t2_dbg : k_spatial1h_t2) : (odbg ? k_spatial1h_dbg : k_spatial1h);
+            auto k = hth == 2u ? (odbg ? k_spatial1h_t2_dbg : k_spatial1h_t2) : (odbg ? k_spatial1h_dbg : k_spatial1h);
             ROMIS_LAUNCH(k, dim3(grid), dim3(hth * kBlock), lds, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, hi, oa,
                          ob, odbg, rp_in, rp_out, hout.w, hout.m, mt);
-        } else if (tu.spatial_lds == 3u && f.R <= kLdsSpatialR && th >= 2u) {
+        } else if (th >= 2u) {
             // 32x16 tiles: the chunks hold half as many (twice as tall) tile rows
             const uint32_t nty2 = (rg.rh + 2u * kTileH - 1) / (2u * kTileH);
             if (rg.xcd_rows) {
@@ -3656,7 +2193,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
             ROMIS_LAUNCH(odbg ? k_spatial1_ntl_t2_dbg : k_spatial1_ntl_t2, dim3(grid), dim3(2u * kBlock),
                          apron_max(2) * 16u, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg,
                          rp_in, rp_out, mt);
-        } else if (tu.spatial_lds == 3u && f.R <= kLdsSpatialR) {
+        } else {
             if (tu.spatial_xcd_cols == kXcdColsAuto && rg.xcd_rows && ntx >= 24u) {
                 // 2-D chunks: 8 tile rows x a third of the tile row (an odd number of chunks per chunk row, so the
                 // round-robin XCDs cover every column).  C2: fetch 83 -> 66 B/px at the same time (profiles/r4/r4g,
@@ -3665,20 +2202,13 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
                 rg.xcd_cols = (ntx + 2u) / 3u;
                 grid = xcd_grid(rg, ntx, nty);
             }
-#ifndef ROMIS_NTL_EXTRA_LDS
-#define ROMIS_NTL_EXTRA_LDS 0   // occupancy experiments (build variants): extra dynamic LDS per block
-#endif
             ROMIS_LAUNCH(odbg ? k_spatial1_ntl_dbg : k_spatial1_ntl, dim3(grid), dim3(kBlock),
-                         kApronMax * 16u + ROMIS_NTL_EXTRA_LDS, stream,
+                         kApronMax * 16u, stream,
                          s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out, mt);
-        } else {
-            ROMIS_LAUNCH(odbg ? k_spatial1_dbg : k_spatial1, dim3(grid), dim3(kBlock), 0, stream, s, rg, f, key, o[0], o[1],
-                         o[2], n_t, p_mat, ia, ib, oa, ob, odbg, rp_in, rp_out);
         }
         if (rp_written) *rp_written = rp_out != nullptr;
         return hipGetLastError();
     }
-    if (tu.spatial_blocks) grid = std::min(grid, std::max(8u, tu.spatial_blocks));   // the general kernels loop
     auto k = f.unbiased ? (f.N == 1 ? k_spatial_n1_unbiased : (f.N == 2 ? k_spatial_n2_unbiased : k_spatial_n0_unbiased))
                         : (f.N == 1 ? k_spatial_n1_biased : (f.N == 2 ? k_spatial_n2_biased : k_spatial_n0_biased));
     const uint32_t bvh_lds = (f.unbiased && f.spatial_vis && bvh_bytes <= kLdsBudget) ? 1u : 0u;
@@ -3691,7 +2221,7 @@ hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev&
                         const float4* p_mat, const float4* ra, const float4* rb, float* rgb, const Tuning& tu,
                         hipStream_t stream, const uint8_t* vis_in, MissTiles mt) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
-    const Region rg = with_map(rg0, tu.final_2d);
+    const Region rg = with_map(rg0, 1u);
     const size_t lds = bvh_lds_bytes(s);
     const bool use_lds = tu.final_lds && lds <= kLdsBudget;
     auto k = use_lds ? (f.N == 1 ? k_final_n1_lds : (f.N == 2 ? k_final_n2_lds : k_final_n0_lds))
@@ -3707,7 +2237,7 @@ hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev&
                          p_mat, ra, rb, rgb, rg.map2d ? mt : MissTiles{nullptr, 0u, 0u});
         return hipGetLastError();
     }
-    ROMIS_LAUNCH(k, grid_capped(items_of(rg), tu.final_blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,
+    ROMIS_LAUNCH(k, dim3(items_of(rg)), dim3(kBlock), use_lds ? lds : 0, stream, s, rg, f,
                        o[0], o[1], o[2], n_t, p_mat, ra, rb, rgb);
     return hipGetLastError();
 }
@@ -3736,90 +2266,6 @@ hipError_t launch_read_stream(const float4* buf, size_t n4, float* sink, hipStre
 hipError_t launch_debug_math(const float* x, const float* y, float* pw, float* ex, uint32_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_debug_math, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, x, y, pw, ex, n);
-    return hipGetLastError();
-}
-
-// ---- R-MIS / R-OMIS ---------------------------------------------------------------------------------------
-namespace {
-typedef void (*RomisSamplesFn)(SceneDev, uint32_t, uint32_t, FeaturesDev, float, float, float, const float4*, const float4*,
-                               const uint32_t*, const float4*, const float4*, const float2*, uint32_t, uint32_t, float*);
-typedef void (*RomisAccumFn)(uint32_t, uint32_t, FeaturesDev, uint32_t, uint32_t, const float*, float*);
-typedef void (*RomisAlphasFn)(uint32_t, uint32_t, float*);
-typedef void (*RomisSolveFn)(uint32_t, uint32_t, FeaturesDev, const float*, float*);
-typedef void (*RomisVisFn)(uint32_t, uint32_t, const float*, uint32_t*);
-typedef void (*DebugCodFn)(const float*, const float*, float*, uint32_t);
-#define ROMIS_T_TABLE(PFX) {PFX##1, PFX##2, PFX##3, PFX##4, PFX##5, PFX##6, PFX##7, PFX##8}
-const RomisSamplesFn kRomisSamples[8] = ROMIS_T_TABLE(k_romis_samples_t);
-const RomisSamplesFn kRomisSamplesLds[8] = ROMIS_T_TABLE(k_romis_samples_lds_t);
-const RomisAccumFn kRomisAccum[8] = ROMIS_T_TABLE(k_romis_accum_t);
-const RomisAccumFn kRomisAccumProg[8] = ROMIS_T_TABLE(k_romis_accum_prog_t);
-const RomisAlphasFn kRomisAlphas[8] = ROMIS_T_TABLE(k_romis_alphas_t);
-const RomisSolveFn kRomisSolve[8] = ROMIS_T_TABLE(k_romis_solve_t);
-const RomisVisFn kRomisVis[8] = ROMIS_T_TABLE(k_romis_vis_t);
-const DebugCodFn kDebugCod[8] = ROMIS_T_TABLE(k_debug_cod_t);
-inline dim3 px_grid(size_t npx) { return dim3((uint32_t)((npx + kBlock - 1) / kBlock)); }
-}  // namespace
-
-hipError_t launch_mis_neighbours(const SceneDev& s, uint32_t W, uint32_t H, const FeaturesDev& f, uint32_t key_s, uint32_t key_d,
-                                 const float4* n_t, const float4* p_mat, uint32_t* nbr, hipStream_t stream) {
-    ROMIS_LAUNCH(k_mis_neighbours, px_grid((size_t)W * H), dim3(kBlock), 0, stream, s, W, H, f, key_s, key_d, n_t, p_mat, nbr);
-    return hipGetLastError();
-}
-
-hipError_t launch_mis_accumulate(const SceneDev& s, uint32_t W, uint32_t H, const FeaturesDev& f, const float* o,
-                                 const float4* n_t, const float4* p_mat, const uint32_t* nbr, const float4* ra,
-                                 const float4* rb, const float2* rdbg, uint32_t iteration, float* acc, float* smp,
-                                 uint32_t smp_samples, const Tuning& tu, hipStream_t stream) {
-    const size_t lds = bvh_lds_bytes(s);
-    const bool use_lds = tu.final_lds && lds <= kLdsBudget;   // shadow rays: the BVH staged like k_final's
-    const dim3 grid = px_grid((size_t)W * H);
-    if (f.mode == RESTIR_MODE_RMIS) {
-        ROMIS_LAUNCH(use_lds ? k_rmis_accum_lds : k_rmis_accum, grid, dim3(kBlock), use_lds ? lds : 0, stream, s, W, H, f,
-                     o[0], o[1], o[2], n_t, p_mat, nbr, ra, rb, acc);
-    } else {
-        const uint32_t T = f.K + 1u;
-        if (T < 1u || T > 8u) return hipErrorInvalidValue;
-        if (f.progressive && iteration >= 1u && iteration % f.prog_mod == 0u)   // alphas from the sums so far
-            ROMIS_LAUNCH(kRomisAlphas[T - 1], grid, dim3(kBlock), 0, stream, W, H, acc);
-        // the T x N samples in chunks of smp_samples (the scratch rows ensure_mis sized), in the reference's order
-        const RomisSamplesFn ks = use_lds ? kRomisSamplesLds[T - 1] : kRomisSamples[T - 1];
-        const RomisAccumFn ka = f.progressive ? kRomisAccumProg[T - 1] : kRomisAccum[T - 1];
-        const uint32_t npx = W * H, S = T * f.N;
-        if (smp_samples == 0u || (uint64_t)smp_samples * npx >= (1ull << 31)) return hipErrorInvalidValue;
-        for (uint32_t s0 = 0; s0 < S; s0 += smp_samples) {
-            const uint32_t ns = std::min(smp_samples, S - s0);
-            const uint32_t blocks = std::min<uint32_t>((ns * npx + kBlock - 1u) / kBlock, 8192u);
-            ROMIS_LAUNCH(ks, dim3(blocks), dim3(kBlock), use_lds ? lds : 0, stream, s, W, H, f, o[0], o[1], o[2], n_t,
-                         p_mat, nbr, ra, rb, rdbg, s0, ns, smp);
-            ROMIS_LAUNCH(ka, grid, dim3(kBlock), 0, stream, W, H, f, s0, ns, smp, acc);
-        }
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_mis_finish(uint32_t W, uint32_t H, const FeaturesDev& f, const float* acc, float* rgb, hipStream_t stream) {
-    const dim3 grid = px_grid((size_t)W * H);
-    const uint32_t T = f.K + 1u;
-    if (f.mode == RESTIR_MODE_ROMIS && !f.progressive) {
-        if (T < 1u || T > 8u) return hipErrorInvalidValue;
-        ROMIS_LAUNCH(kRomisSolve[T - 1], grid, dim3(kBlock), 0, stream, W, H, f, acc, rgb);
-    } else {
-        const float* col = f.mode == RESTIR_MODE_ROMIS ? acc + (size_t)(T * T + 6u * T) * W * H : acc;
-        ROMIS_LAUNCH(k_mis_combine, grid, dim3(kBlock), 0, stream, W, H, f, col, rgb);
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_romis_vis(uint32_t W, uint32_t H, uint32_t T, const float* acc, uint32_t* out, hipStream_t stream) {
-    if (T < 1u || T > 8u) return hipErrorInvalidValue;
-    ROMIS_LAUNCH(kRomisVis[T - 1], px_grid((size_t)W * H), dim3(kBlock), 0, stream, W, H, acc, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_debug_cod(uint32_t n, const float* A, const float* b, float* x, uint32_t count, hipStream_t stream) {
-    if (count == 0) return hipSuccess;
-    if (n < 1u || n > 8u) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(kDebugCod[n - 1], px_grid(count), dim3(kBlock), 0, stream, A, b, x, count);
     return hipGetLastError();
 }
 

@@ -6,14 +6,14 @@
 namespace romis {
 
 // The target-pdf cache (N = 1, SoA planes, nullable): rp[p] = the target pdf of pixel p's held sample at p.
-// RIS / temporal / k_spatial1 write it for their output; temporal and k_spatial1 read it for the input's own
+// RIS / temporal / the lean spatial passes write it for their output; temporal and the passes read it for the input's own
 // sample instead of re-evaluating it (same pixel, same G-buffer, same sample: the same bits).
 // n_t2 (nullable): a second record buffer that also receives the G-buffer n_t (the ping-pong partner)
 hipError_t launch_primary(const SceneDev& s, const Region& rg, const CameraDev& cam, float4* n_t, float4* p_mat,
                           float4* n_t2, const Tuning& tu, hipStream_t stream);
 hipError_t launch_ris(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, const float* origin,
                       const float4* n_t, const float4* p_mat, float4* ra, float4* rb, float2* rdbg, float* rp,
-                      const Tuning& tu, QueueState& qs, hipStream_t stream);
+                      const Tuning& tu, hipStream_t stream);
 // genPrimaryRayHits + genCanonicalSamples in one kernel over the same region (needs the BVH to fit in LDS)
 hipError_t launch_primary_ris(const SceneDev& s, const Region& rg, const CameraDev& cam, const FeaturesDev& f, uint32_t key,
                               float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb, float2* rdbg,

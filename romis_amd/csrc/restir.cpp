@@ -223,27 +223,9 @@ struct restir_ctx {
     DevBuf hnd[2];                                  // sample handles of rec[i] (N = 1 point lights, k_spatial1h)
     int cur = 0;
     uint32_t rgb_w = 0, rgb_h = 0;
-    // Frames in flight (tuning frames.inflight = 2): restir_render alternates two frame slots -- slot 0 is the buffers
-    // above on `stream`, slot 1 its own buffers on its own stream -- so that frame f + 1's primary rays and RIS run
-    // while frame f is shaded.  Only that overlap is allowed: a frame's RIS waits for the other slot's last spatial
-    // pass (`after_spatial`) and its spatial passes wait for the other slot's final shading (`after_final`), so a
-    // spatial pass never shares the GPU with another kernel (its timed duration stays the pass alone).
-    struct Slot1 {
-        hipStream_t stream = nullptr;
-        DevBuf n_t, p_mat, rec[2], rp[2], rgb, uv, vis, tmiss, hnd[2];
-    } slot1;
-    struct {
-        hipEvent_t after_spatial[2] = {nullptr, nullptr}, after_final[2] = {nullptr, nullptr}, joined = nullptr;
-        bool has[2] = {false, false};
-        int next = 0;          // the slot of the next pipelined frame
-        int last = 0;          // the slot holding the last frame's rgb
-        bool slot1_busy = false;   // slot 1 may have work the context stream has not waited for
-    } pipe;
 
     // launch-shape knobs (restir_set_tuning)
     Tuning tuning{};
-    DevBuf queue_ctr;      // WorkQueue ticket counter (4 bytes, zeroed at creation, never reset)
-    QueueState queue{};
 
     // RNG
     uint32_t seed = RESTIR_DEFAULT_SEED;
@@ -652,7 +634,6 @@ restir_status timed_end(restir_ctx* c, Pending& p, hipError_t launch_err) {
 
 restir_status collect_timings(restir_ctx* c) {
     if (c->pending.empty()) return RESTIR_OK;
-    if (c->slot1.stream) HIP_TRY(hipStreamSynchronize(c->slot1.stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (Pending& p : c->pending) {
         float ms = 0.0f;
@@ -710,16 +691,15 @@ struct FrameBufs {
     bool records;
     size_t npx;
     uint32_t N;
-    int slot = 0;   // restir_render's frame slot (frames in flight); everything else uses slot 0
-    DevBuf* rec_() const { return slot ? c->slot1.rec : c->rec; }
-    DevBuf& n_t_() const { return slot ? c->slot1.n_t : c->n_t; }
-    DevBuf* rp_() const { return slot ? c->slot1.rp : c->rp; }
-    float4* pm() const { return (slot ? c->slot1.p_mat : c->p_mat).as<float4>(); }
-    DevBuf& rgb() const { return slot ? c->slot1.rgb : c->rgb; }
-    DevBuf& uv() const { return slot ? c->slot1.uv : c->uv; }
-    DevBuf& vis() const { return slot ? c->slot1.vis : c->vis; }
-    DevBuf& tmiss() const { return slot ? c->slot1.tmiss : c->tmiss; }
-    DevBuf* hnd_() const { return slot ? c->slot1.hnd : c->hnd; }
+    DevBuf* rec_() const { return c->rec; }
+    DevBuf& n_t_() const { return c->n_t; }
+    DevBuf* rp_() const { return c->rp; }
+    float4* pm() const { return c->p_mat.as<float4>(); }
+    DevBuf& rgb() const { return c->rgb; }
+    DevBuf& uv() const { return c->uv; }
+    DevBuf& vis() const { return c->vis; }
+    DevBuf& tmiss() const { return c->tmiss; }
+    DevBuf* hnd_() const { return c->hnd; }
     // the sample-handle planes of rec[i]: W then M | index << 24, one 4-byte plane each (ensure_handles)
     Handles h(int i) const {
         float* w = hnd_()[i].as<float>();
@@ -736,12 +716,11 @@ struct FrameBufs {
     Region region(Region r) const { return records ? with_records(r, N) : r; }
 };
 
-restir_status ensure_records(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N, FrameBufs& fb, int slot = 0) {
+restir_status ensure_records(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N, FrameBufs& fb) {
     const size_t npx = (size_t)vw * vh;
     fb = FrameBufs{c, c->tuning.records != 0, npx, N};
-    fb.slot = slot;
-    const hipStream_t st = slot ? c->slot1.stream : c->stream;
-    ST_TRY((slot ? c->slot1.p_mat : c->p_mat).ensure(npx * 16));
+    const hipStream_t st = c->stream;
+    ST_TRY(c->p_mat.ensure(npx * 16));
     if (!fb.records) ST_TRY(fb.n_t_().ensure(npx * 16));
     const size_t rec_bytes = npx * (fb.records ? 1u + 2u * N : 2u * N) * 16;
     DevBuf* rec = fb.rec_();
@@ -752,7 +731,7 @@ restir_status ensure_records(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N
     }
     if (!fb.records && N == 1)
         for (int i = 0; i < 2; i++) ST_TRY(fb.rp_()[i].ensure(npx * 4));
-    if (!slot) { c->vw = vw; c->vh = vh; c->N = N; }
+    c->vw = vw; c->vh = vh; c->N = N;
     return RESTIR_OK;
 }
 
@@ -781,20 +760,6 @@ static restir_status scene_for(restir_ctx* c, const FeaturesDev& f, size_t npx, 
     return RESTIR_OK;
 }
 
-// Frames in flight: the context stream waits for whatever slot 1 still has in flight (every entry point that works
-// on the context stream after a pipelined frame calls this; a no-op when frames were never pipelined).
-static restir_status join_slots(restir_ctx* c) {
-    c->pipe.last = 0;   // the caller works on slot 0 (its rgb is the context's)
-    if (!c->pipe.slot1_busy) return RESTIR_OK;
-    if (!c->pipe.joined) HIP_TRY(hipEventCreateWithFlags(&c->pipe.joined, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(c->pipe.joined, c->slot1.stream));
-    HIP_TRY(hipStreamWaitEvent(c->stream, c->pipe.joined, 0));
-    c->pipe.slot1_busy = false;
-    c->pipe.has[0] = c->pipe.has[1] = false;   // the next pipelined frame starts a fresh pair
-    c->pipe.next = 0;
-    return RESTIR_OK;
-}
-
 extern "C" {
 
 restir_status restir_create(int device, restir_ctx** out) {
@@ -814,12 +779,6 @@ restir_status restir_create(int device, restir_ctx** out) {
     c->device = device;
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; return fail(RESTIR_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e)); }
-    if (c->queue_ctr.ensure(64) != RESTIR_OK || hipMemset(c->queue_ctr.p, 0, 64) != hipSuccess) {
-        (void)hipStreamDestroy(c->stream);
-        delete c;
-        return fail(RESTIR_ERR_HIP, "work-queue counter allocation failed");
-    }
-    c->queue.ctr = c->queue_ctr.as<uint32_t>();
     *out = c;
     return RESTIR_OK;
 }
@@ -832,23 +791,15 @@ void restir_destroy(restir_ctx* c) {
         std::lock_guard<std::mutex> lk(c->mu);
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
-        if (c->slot1.stream) (void)hipStreamSynchronize(c->slot1.stream);
-        for (DevBuf* b : {&c->slot1.n_t, &c->slot1.p_mat, &c->slot1.rec[0], &c->slot1.rec[1], &c->slot1.rp[0],
-                          &c->slot1.rp[1], &c->slot1.rgb, &c->slot1.uv, &c->slot1.vis, &c->vis,
-                          &c->slot1.tmiss, &c->tmiss, &c->hnd[0], &c->hnd[1], &c->slot1.hnd[0], &c->slot1.hnd[1]})
-            b->release();
-        for (hipEvent_t* e : {&c->pipe.after_spatial[0], &c->pipe.after_spatial[1], &c->pipe.after_final[0],
-                              &c->pipe.after_final[1], &c->pipe.joined})
-            if (*e) (void)hipEventDestroy(*e);
+        for (DevBuf* b : {&c->vis, &c->tmiss, &c->hnd[0], &c->hnd[1]}) b->release();
         for (DevBuf* b : {&c->nodes, &c->tri_v0, &c->tri_e1, &c->tri_e2, &c->tri_n0, &c->tri_n1, &c->tri_n2,
                           &c->materials, &c->lights, &c->light_c2, &c->light_c4, &c->light_col, &c->tex_texels, &c->tex_dims, &c->tri_uv, &c->uv, &c->n_t, &c->p_mat, &c->ra[0], &c->ra[1], &c->rb[0], &c->rb[1],
-                          &c->dbg[0], &c->dbg[1], &c->rgb, &c->queue_ctr, &c->halo_scratch, &c->rec[0], &c->rec[1], &c->rp[0], &c->rp[1]})
+                          &c->dbg[0], &c->dbg[1], &c->rgb, &c->halo_scratch, &c->rec[0], &c->rec[1], &c->rp[0], &c->rp[1]})
             b->release();
         for (Pending& p : c->pending) { (void)hipEventDestroy(p.start); (void)hipEventDestroy(p.stop); }
         for (hipEvent_t ev : c->free_events) (void)hipEventDestroy(ev);
         c->pool->close();   // frames still alive free their records themselves on release
         release_rccl(c);
-        if (c->slot1.stream) (void)hipStreamDestroy(c->slot1.stream);
         (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -1048,7 +999,6 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     std::vector<float> nodes = bvh.nodes;
     if (nodes.empty()) nodes.assign(8, 0.0f);
 
-    ST_TRY(join_slots(c));
     HIP_TRY(hipStreamSynchronize(c->stream));   // previous frames (either slot) may still read the old scene
     ST_TRY(c->nodes.upload(nodes.data(), nodes.size() * 4, c->stream));
     ST_TRY(c->tri_v0.upload(v0.data(), v0.size() * 4, c->stream));
@@ -1236,7 +1186,7 @@ static restir_status render_mis(restir_ctx* c, const restir_camera* cam, const r
     for (uint32_t it = 0; it < features->max_iterations_mis; it++) {
         TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, it), camd.origin, nt, pm,
                                           c->ra[0].as<float4>(), c->rb[0].as<float4>(), c->dbg[0].as<float2>(), nullptr,
-                                          c->tuning, c->queue, c->stream));
+                                          c->tuning, c->stream));
         TIMED(c, RESTIR_K_MIS, launch_mis_accumulate(s, W, H, f, camd.origin, nt, pm, c->mis_nbr.as<uint32_t>(),
                                                      c->ra[0].as<float4>(), c->rb[0].as<float4>(), c->dbg[0].as<float2>(), it,
                                                      c->mis_acc.as<float>(), c->mis_smp.as<float>(), c->mis_smp_samples,
@@ -1267,8 +1217,7 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
         if (tile && (tile->global_width != width || tile->global_height != height || tile->x0 || tile->y0 ||
                      tile->width != width || tile->height != height))
             return fail(RESTIR_ERR_UNSUPPORTED, "R-MIS / R-OMIS render whole images only (no screen tiles)");
-        ST_TRY(join_slots(c));
-        return render_mis(c, cam, features, width, height, out_rgb);
+            return render_mis(c, cam, features, width, height, out_rgb);
     }
 
     restir_tile t{};
@@ -1313,22 +1262,9 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
             return fail(RESTIR_ERR_INVALID, "temporal predecessor grid was rendered with the other buffer layout");
     }
 
-    // frame slot (frames in flight, restir_ctx::Slot1): slot 0 = the context's buffers and stream
-    const bool pipe = c->tuning.inflight > 1u;
-    if (!pipe) ST_TRY(join_slots(c));
-    const int k = pipe ? c->pipe.next : 0;
-    if (k == 1 && !c->slot1.stream) HIP_TRY(hipStreamCreateWithFlags(&c->slot1.stream, hipStreamNonBlocking));
-    const hipStream_t st = k ? c->slot1.stream : c->stream;
-    if (pipe)
-        for (int e = 0; e < 2; e++)
-            if (!c->pipe.after_spatial[e]) {
-                HIP_TRY(hipEventCreateWithFlags(&c->pipe.after_spatial[e], hipEventDisableTiming));
-                HIP_TRY(hipEventCreateWithFlags(&c->pipe.after_final[e], hipEventDisableTiming));
-            }
-    const bool wait_other = pipe && c->pipe.has[k ^ 1];
-
+    const hipStream_t st = c->stream;
     FrameBufs fb;
-    ST_TRY(ensure_records(c, t.gwidth, t.gheight, N, fb, k));
+    ST_TRY(ensure_records(c, t.gwidth, t.gheight, N, fb));
     c->stage_ok = false;   // ensure_records re-sized the shared view state: the stage API must be reconfigured
     ST_TRY(fb.rgb().ensure((size_t)t.width * t.height * 12));
     c->rgb_w = t.width; c->rgb_h = t.height;
@@ -1342,14 +1278,12 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     float4* pm = fb.pm();
     int cur = 0;
 
-    // frames in flight: this frame's primary rays and RIS start once the other slot's spatial passes are done
-    if (wait_other) HIP_TRY(hipStreamWaitEvent(st, c->pipe.after_spatial[k ^ 1], 0));
     const uint32_t ris_key = restir_rng_key(c->seed, frame, RESTIR_STAGE_RIS, 0);
     // background tiles (MissTiles): N <= 2, no temporal reuse (its output is not the RIS result), the fused kernel with
     // one 32 x 8 tile per block; the spatial shortcuts also need bounded normals (their miss tests)
     uint8_t* tmiss = nullptr;
     const bool fused = c->tuning.fuse_primary_ris && primary_ris_fits(s);
-    if (c->tuning.miss_tiles && fused && N <= 2 && !temporal && c->tuning.primary_2d && !c->tuning.ris_blocks &&
+    if (c->tuning.miss_tiles && fused && N <= 2 && !temporal &&
         s.normals_bounded && !fb.records) {
         const size_t tiles = (size_t)((t.gwidth + 31u) / 32u) * ((t.gheight + 7u) / 8u);
         ST_TRY(fb.tmiss().ensure((tiles + 3u) & ~(size_t)3u));   // whole words: the spatial pass reads its flag's word
@@ -1386,7 +1320,7 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     } else {
         TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, view, camd, fb.nt(0), pm, fb.nt2(), c->tuning, st));
         TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, ris_key, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), nullptr,
-                                          fb.rp(cur), c->tuning, c->queue, st));
+                                          fb.rp(cur), c->tuning, st));
     }
     if (temporal) {
         ST_TRY(use_prev(prev, c->device, st));   // the predecessor's records are complete (its producer's stream)
@@ -1396,8 +1330,6 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                               fb.rp(cur), fb.rp(cur), c->tuning, st));
         used_prev(prev, st);
     }
-    // ... and its spatial passes once the other slot's final shading is done: a spatial pass runs alone
-    if (wait_other) HIP_TRY(hipStreamWaitEvent(st, c->pipe.after_final[k ^ 1], 0));
     bool rp_ok = fb.rp(cur) != nullptr;   // the current grid's target-pdf cache holds its samples' pdfs
     // the last pass's own-pixel shadow rays (unbiased + visibility reuse, N = 1) go on to final shading
     uint8_t* vis = nullptr;
@@ -1426,16 +1358,8 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                              handles && pass + 1 < passes ? fb.h(nxt) : Handles{nullptr, nullptr}));
         cur = nxt;
     }
-    if (pipe) HIP_TRY(hipEventRecord(c->pipe.after_spatial[k], st));
     TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), fb.rgb().as<float>(),
                                           c->tuning, st, vis_ok ? vis : nullptr, MissTiles{tmiss, 0u, 0u}));
-    if (pipe) {
-        HIP_TRY(hipEventRecord(c->pipe.after_final[k], st));
-        c->pipe.has[k] = true;
-        c->pipe.next = k ^ 1;
-        if (k == 1) c->pipe.slot1_busy = true;
-    }
-    c->pipe.last = k;
     c->cur = cur;
 
     if (out_next) {
@@ -1517,7 +1441,6 @@ restir_status restir_synchronize(restir_ctx* c) {
     if (!c) return fail(RESTIR_ERR_INVALID, "ctx is NULL");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
-    if (c->slot1.stream) HIP_TRY(hipStreamSynchronize(c->slot1.stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
@@ -1529,11 +1452,8 @@ restir_status restir_download_rgb(restir_ctx* c, float* out_rgb, size_t count) {
     if (need == 0) return fail(RESTIR_ERR_STATE, "nothing rendered yet");
     if (count < need) return fail(RESTIR_ERR_INVALID, "buffer holds %zu floats, need %zu", count, need);
     HIP_TRY(hipSetDevice(c->device));
-    // the last frame's rgb: slot 1's buffer and stream when frames were in flight and it rendered last
-    const bool s1 = c->pipe.last == 1;
-    const hipStream_t st = s1 ? c->slot1.stream : c->stream;
-    HIP_TRY(hipMemcpyAsync(out_rgb, (s1 ? c->slot1.rgb : c->rgb).p, need * 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipMemcpyAsync(out_rgb, c->rgb.p, need * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
 
@@ -1543,7 +1463,6 @@ restir_status restir_stage_configure(restir_ctx* c, uint32_t width, uint32_t hei
     if (!c || width == 0 || height == 0 || n < 1 || n > RESTIR_MAX_N) return fail(RESTIR_ERR_INVALID, "bad stage size");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
-    ST_TRY(join_slots(c));
     ST_TRY(ensure_work(c, width, height, n, true));
     ST_TRY(c->rgb.ensure((size_t)width * height * 12));
     c->rgb_w = width; c->rgb_h = height;
@@ -1615,7 +1534,6 @@ restir_status restir_stage_download(restir_ctx* c, restir_buffer which, void* ho
     if (!c->stage_ok) return fail(RESTIR_ERR_STATE, "restir_stage_configure first"); \
     if (!c->has_scene) return fail(RESTIR_ERR_STATE, "restir_set_scene first");      \
     HIP_TRY(hipSetDevice(c->device));                                               \
-    ST_TRY(join_slots(c))
 
 restir_status restir_stage_primary(restir_ctx* c, const restir_camera* cam) {
     if (!cam) return fail(RESTIR_ERR_INVALID, "camera is NULL");
@@ -1650,7 +1568,7 @@ restir_status restir_stage_ris(restir_ctx* c, const restir_camera* cam, const re
     const int cur = c->cur;
     TIMED(c, RESTIR_K_RIS, launch_ris(sd, c->stage_rg, d, key, camd.origin, c->n_t.as<float4>(), c->p_mat.as<float4>(),
                                       c->ra[cur].as<float4>(), c->rb[cur].as<float4>(),
-                                      debug ? c->dbg[cur].as<float2>() : nullptr, nullptr, c->tuning, c->queue, c->stream));
+                                      debug ? c->dbg[cur].as<float2>() : nullptr, nullptr, c->tuning, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RESTIR_OK;
 }
@@ -1806,7 +1724,6 @@ restir_status restir_measure_read_bandwidth(restir_ctx* c, uint64_t bytes, uint3
     if (!c || !out_gbps || iters == 0 || bytes < (1u << 20)) return fail(RESTIR_ERR_INVALID, "bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
-    ST_TRY(join_slots(c));
     const size_t n4 = (size_t)(bytes / 16);
     DevBuf buf, sink;
     ST_TRY(buf.ensure(n4 * 16));
@@ -1861,7 +1778,6 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
     std::lock_guard<std::mutex> lk(c->mu);
     if (!c->has_scene) return fail(RESTIR_ERR_STATE, "restir_halo_begin before restir_set_scene");
     HIP_TRY(hipSetDevice(c->device));
-    ST_TRY(join_slots(c));
     const FeaturesDev f = to_dev(features);
     const uint32_t passes = features->spatial_reuse ? features->spatial_resampling_passes : 0u;
     restir_tile t{};
@@ -1917,7 +1833,7 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
     // reservoirs only on the owned rectangle
     TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, h.view, h.camd, fb.nt(0), pm, fb.nt2(), c->tuning, c->stream));
     TIMED(c, RESTIR_K_RIS, launch_ris(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_RIS, 0), h.camd.origin,
-                                      fb.nt(0), pm, fb.ra(0), fb.rb(0), nullptr, fb.rp(0), c->tuning, c->queue, c->stream));
+                                      fb.nt(0), pm, fb.ra(0), fb.rb(0), nullptr, fb.rp(0), c->tuning, c->stream));
     if (temporal)
         TIMED(c, RESTIR_K_TEMPORAL,
               launch_temporal(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_TEMPORAL, 0), h.camd.origin, fb.nt(0),
@@ -2367,36 +2283,18 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     std::lock_guard<std::mutex> lk(c->mu);
     Tuning& t = c->tuning;
     const uint32_t v = (uint32_t)value;
-    if (!std::strcmp(key, "primary.blocks")) t.primary_blocks = v;
-    else if (!std::strcmp(key, "primary.lds")) t.primary_lds = v;
-    else if (!std::strcmp(key, "primary.2d")) t.primary_2d = v;
-    else if (!std::strcmp(key, "ris.blocks")) t.ris_blocks = v;
+    if (!std::strcmp(key, "primary.lds")) t.primary_lds = v;
     else if (!std::strcmp(key, "ris.lds")) t.ris_lds = v;
-    else if (!std::strcmp(key, "spatial.xcd")) t.spatial_xcd = v;
-    else if (!std::strcmp(key, "spatial.blocks")) t.spatial_blocks = v;
     else if (!std::strcmp(key, "spatial.xcd_rows")) t.spatial_xcd_rows = v;
     else if (!std::strcmp(key, "spatial.xcd_cols")) t.spatial_xcd_cols = v;
     else if (!std::strcmp(key, "ris.late")) t.ris_late = v;
     else if (!std::strcmp(key, "miss.tiles")) t.miss_tiles = v;
     else if (!std::strcmp(key, "miss.gbuf")) t.miss_gbuf = v;
     else if (!std::strcmp(key, "final.miss")) t.final_miss = v;
-    else if (!std::strcmp(key, "spatial.lds")) {
-        if (v != 0u && v != 3u)
-            return fail(RESTIR_ERR_INVALID, "spatial.lds: 0 (gathers) or 3 (n_t window, default); 1, 2 and 4 were measured "
-                                            "slower and removed in round 4 (profiles/r4/pruned)");
-        t.spatial_lds = v;
-    }
-    else if (!std::strcmp(key, "spatial.wave8")) t.spatial_wave8 = v;
     else if (!std::strcmp(key, "spatial.lean")) t.spatial_lean = v;
-    else if (!std::strcmp(key, "spatial.th")) { if (v > 4) return fail(RESTIR_ERR_INVALID, "spatial.th: 0 (auto), 1 .. 4"); t.spatial_th = v; }
+    else if (!std::strcmp(key, "spatial.th")) { if (v > 2) return fail(RESTIR_ERR_INVALID, "spatial.th: 0 (auto), 1 or 2"); t.spatial_th = v; }
     else if (!std::strcmp(key, "spatial.handles")) t.spatial_handles = v;
     else if (!std::strcmp(key, "fuse.primary_ris")) t.fuse_primary_ris = v;
-    else if (!std::strcmp(key, "frames.inflight")) {
-        if (v < 1u || v > 2u) return fail(RESTIR_ERR_INVALID, "frames.inflight: 1 or 2");
-        HIP_TRY(hipSetDevice(c->device));
-        if (v == 1u) ST_TRY(join_slots(c));
-        t.inflight = v;
-    }
     else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;
     else if (!std::strcmp(key, "timing.every")) { t.timing_every = v ? v : 1u; for (auto& q : c->timing_seq) q = 0; }
     else if (!std::strcmp(key, "timing.fence")) {
@@ -2409,15 +2307,12 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
         }
         t.timing_fence = v;
     }
-    else if (!std::strcmp(key, "ris.queue")) t.ris_queue = v;
     else if (!std::strcmp(key, "ris.compact")) t.ris_compact = v;
     else if (!std::strcmp(key, "bvh.max_leaf")) t.bvh_max_leaf = v;
     else if (!std::strcmp(key, "final.sort")) t.final_sort = v;
     else if (!std::strcmp(key, "mis.chunk")) t.mis_chunk = v;   // applies from the next ensure_mis
     else if (!std::strcmp(key, "layout.records")) t.records = v;   // frame-path buffer layout
-    else if (!std::strcmp(key, "final.blocks")) t.final_blocks = v;
     else if (!std::strcmp(key, "final.lds")) t.final_lds = v;
-    else if (!std::strcmp(key, "final.2d")) t.final_2d = v;
     else return fail(RESTIR_ERR_INVALID, "unknown tuning key '%s'", key);
     return RESTIR_OK;
 }

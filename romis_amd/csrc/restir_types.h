@@ -95,7 +95,7 @@ struct Region {
     // lives at index j * js + p * ps.  SoA planes: ps = 1, js = view pixels.  Per-pixel records
     // [n_t, a_0, b_0, a_1, b_1, ...] (restir_render): ps = 1 + 2N, js = 2, with res_a = rec + 1, res_b = rec + 2.
     uint32_t ps, js;
-    uint32_t xcd_rows;   // k_spatial1's XCD tile order (xcd_tile); 0 elsewhere
+    uint32_t xcd_rows;   // the lean spatial passes' XCD tile order (xcd_tile); 0 elsewhere
     uint32_t xcd_cols;   // chunk width in tiles (xcd_tile); 0 = the whole row of tiles
 };
 
@@ -122,12 +122,8 @@ struct Handles {
 constexpr uint32_t kXcdRowsAuto = 255u;
 constexpr uint32_t kXcdColsAuto = 255u;
 struct Tuning {
-    uint32_t primary_blocks = 0;   // grid cap (persistent blocks); 0 = one block per work item
     uint32_t primary_lds = 1;      // stage the BVH in LDS when it fits
-    uint32_t primary_2d = 1;
-    uint32_t ris_blocks = 0;
     uint32_t ris_lds = 1;          // stage the light table in LDS when it fits
-    uint32_t ris_queue = 0;        // persistent blocks (this many) pulling tiles from a WorkQueue; 0 = off
     uint32_t ris_compact = 1;      // N <= 2: compact light tables for point-light-only scenes and light grids (_pt /
                                    // _grid RIS kernels, kernels.hip ris_light_form)
     uint32_t miss_tiles = 1;       // restir_render: background-tile flags (MissTiles) from RIS to the spatial passes
@@ -137,44 +133,27 @@ struct Tuning {
                                    // window fix-up's per-entry flag loads outweigh the saved stores at 1080p)
     uint32_t ris_late = 1;         // fused primary + RIS, one tile per block: stage the light table only for tiles with
                                    // a pixel that runs the candidate loop (0: every tile, before the primary rays)
-    uint32_t spatial_xcd = 1;      // XCD-banded tile order
-    uint32_t spatial_lds = 3;      // N = 1 biased: 3 the n_t window in LDS (k_spatial1_ntl, default), 0 no window
-                                   // (k_spatial1, gathers; also any R > 10)
-    uint32_t spatial_xcd_rows = 255; // k_spatial1: XCD x takes every 8th chunk of this many tile rows (0: one band;
+    uint32_t spatial_xcd_rows = 255; // lean passes: XCD x takes every 8th chunk of this many tile rows (0: one band;
                                      // 255 = kXcdRowsAuto: as many as keep a chunk's records in one XCD's L2)
     uint32_t spatial_xcd_cols = 255; // chunk width in tiles (0: full rows); 2-D chunks keep the +-R window rows of
                                      // consecutive tile rows in the XCD's L2.  255 = kXcdColsAuto: the N = 1 biased
                                      // pass on 32 x 8 tiles takes 8 tile rows x a third of the tile row when the row
                                      // has >= 24 tiles (C2: 1.20 -> 1.0x traffic, same time), full rows elsewhere
-    uint32_t spatial_blocks = 0;
-    uint32_t spatial_wave8 = 1;    // waves cover 8x8 pixel blocks instead of 32x2 rows (-2..4 %, kbench)
     uint32_t fuse_primary_ris = 1; // restir_render: k_primary_ris instead of k_primary + k_ris when the BVH fits LDS
-    uint32_t spatial_lean = 1;     // N = 1 biased passes through k_spatial1 (0: the general kernel)
+    uint32_t spatial_lean = 1;     // the lean N = 1 / 2 passes (0: the general kernels)
     uint32_t spatial_th = 0;       // N = 1 biased ntl pass: tile height in 8-row units (1: 32x8, 2: 32x16 k_spatial1_ntl_t2; 0: by width)
     uint32_t spatial_handles = 1;  // restir_render, N = 1 biased, point lights: the passes read sample handles (k_spatial1h)
     uint32_t timing_mask = 0xFFFFFFFFu;   // kernels (bit = RESTIR_K_*) bracketed by HIP events when timing is on
-    uint32_t inflight = 1;         // restir_render frame slots: 2 overlaps frame f's final shading with frame f + 1's
-                                   // primary rays + RIS (restir_ctx::Slot1; every spatial pass still runs alone)
     uint32_t timing_every = 1;     // events on every n-th launch of a timed kernel (the others launch plain)
     uint32_t timing_fence = 0;     // 1: timing events with the default system-scope release (a cache writeback after
                                    // the timed kernel: 6.7 + 4.6 us of stream gaps per C2 frame, profiles/r4); 0:
                                    // hipEventDisableSystemFence (read only after a stream synchronisation)
     uint32_t records = 0;          // frame path: per-pixel records (1) or SoA planes (0); planes measured faster
     uint32_t bvh_max_leaf = 2;     // triangles per BVH leaf (used by restir_set_scene); 2 beat 1/4/8 (kbench)
-    uint32_t final_blocks = 0;
     uint32_t final_lds = 1;
-    uint32_t final_2d = 1;
     uint32_t final_miss = 1;       // k_final_n*_sorted: primary-ray misses read p_mat + (pos, W) only (SceneDev::miss_shade_zero)
     uint32_t final_sort = 1;       // N = 1: bin each tile's shadow rays by target before tracing (-2.4 %, r2ah)
     uint32_t mis_chunk = 0;        // R-OMIS samples per k_romis_samples / k_romis_accum pair; 0 = the scratch budget
-};
-
-// Dynamic tile queue for persistent grids: a never-reset ticket counter; a launch hands out tickets
-// base .. base + items + grid - 1 (every block fetches until its first out-of-range ticket), so the host knows
-// the next launch's base without reading the counter back.
-struct WorkQueue {
-    uint32_t* ctr;     // nullptr: no queue (block b takes work items b, b + grid, ...)
-    uint32_t base;
 };
 
 // Halo segments of one exchange (restir_halo_plan), pixel prefix offsets into the packed buffer.
@@ -183,12 +162,6 @@ struct HaloSegs {
     uint32_t n;
     uint32_t x0[RESTIR_MAX_HALO_SEGS], y0[RESTIR_MAX_HALO_SEGS], w[RESTIR_MAX_HALO_SEGS], h[RESTIR_MAX_HALO_SEGS];
     uint32_t px0[RESTIR_MAX_HALO_SEGS + 1];   // px0[i] = pixels before segment i; px0[n] = total
-};
-
-// Host side of the queue: the context's counter and the next launch's base.
-struct QueueState {
-    uint32_t* ctr = nullptr;
-    uint32_t base = 0;
 };
 
 struct CameraDev {

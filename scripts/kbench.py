@@ -20,32 +20,19 @@ import numpy as np  # noqa: E402
 
 from romis_amd import _abi, restir, scene  # noqa: E402
 
-DEFAULTS = {"primary.blocks": 0, "primary.lds": 1, "primary.2d": 1, "ris.blocks": 0, "ris.lds": 1, "ris.queue": 0, "ris.compact": 1,
-            "ris.late": 1, "miss.tiles": 1, "miss.gbuf": 2, "spatial.xcd": 1, "spatial.xcd_rows": 255, "spatial.xcd_cols": 255, "spatial.lds": 3, "spatial.blocks": 0, "spatial.wave8": 1, "spatial.lean": 1, "spatial.th": 0, "spatial.handles": 1, "fuse.primary_ris": 1, "bvh.max_leaf": 2, "final.blocks": 0, "final.lds": 1, "final.2d": 1,
-            "final.sort": 1, "final.miss": 1, "layout.records": 0}
+DEFAULTS = {"primary.lds": 1, "ris.lds": 1, "ris.compact": 1, "ris.late": 1, "miss.tiles": 1, "miss.gbuf": 2,
+            "spatial.xcd_rows": 255, "spatial.xcd_cols": 255, "spatial.lean": 1, "spatial.th": 0, "spatial.handles": 1,
+            "fuse.primary_ris": 1, "bvh.max_leaf": 2, "final.lds": 1, "final.sort": 1, "final.miss": 1, "layout.records": 0}
 
 VARIANTS = {
     "default": {},
     "handles_off": {"spatial.handles": 0},
     "handles_t1": {"spatial.th": 1},
-    "handles_t3": {"spatial.th": 3},
-    "handles_t4": {"spatial.th": 4},
     "ntl_t2": {"spatial.handles": 0, "spatial.th": 2},
     "feat_no_tonemap": {"@enable_tone_mapping": 0},
-    "primary_1d_global": {"primary.2d": 0, "primary.lds": 0},
-    "primary_1d_lds": {"primary.2d": 0},
     "primary_2d_global": {"primary.lds": 0},
-    "primary_2d_lds_p1024": {"primary.blocks": 1024},
-    "primary_2d_lds_p2048": {"primary.blocks": 2048},
     "ris_nolds": {"ris.lds": 0},
-    "ris_p2048": {"ris.blocks": 2048},
-    "ris_lds_p2048": {"ris.lds": 1, "ris.blocks": 2048},
-    "ris_q1280": {"ris.queue": 1280},
-    "ris_q2560": {"ris.queue": 2560},
-    "ris_q1024": {"ris.queue": 1024},
-    "spatial_noxcd": {"spatial.xcd": 0},
     "spatial_band": {"spatial.xcd_rows": 0},
-    "spatial_gather": {"spatial.lds": 0},
 
     "spatial_rows1": {"spatial.xcd_rows": 1},
     "spatial_rows2": {"spatial.xcd_rows": 2},
@@ -58,17 +45,12 @@ VARIANTS = {
     "unfused": {"fuse.primary_ris": 0},
     "final_unsorted": {"final.sort": 0},
     "layout_records": {"layout.records": 1},
-    "spatial_rows": {"spatial.wave8": 0},
     "bvh_leaf1": {"bvh.max_leaf": 1},
     "bvh_leaf3": {"bvh.max_leaf": 3},
     "bvh_leaf4": {"bvh.max_leaf": 4},
     "bvh_leaf1_sort": {"bvh.max_leaf": 1, "final.sort": 1},
     "bvh_leaf8": {"bvh.max_leaf": 8},
-    "final_1d_global": {"final.2d": 0, "final.lds": 0},
-    "final_1d_lds": {"final.2d": 0},
     "final_2d_global": {"final.lds": 0},
-    "final_2d_lds_p1024": {"final.blocks": 1024},
-    "final_2d_lds_p2048": {"final.blocks": 2048},
 }
 
 

@@ -202,28 +202,27 @@ def test_temporal_bit_exact(gpu, oracle, N, clamp):
     assert_bits(gpu.download(_abi.BUF_RES_DBG), od, "wSum/chosen")
 
 
-# spatial kernels of an N = 1 biased pass: k_spatial1 (gathers; XCD order in 4-row chunks or one band),
-# k_spatial1_ntl (n_t staged, the default; _t2: 32x16 tiles), the general kernel
-SPATIAL_VARIANTS = {"gather": {"spatial.lean": 1, "spatial.lds": 0},
-                    "gather_band": {"spatial.lean": 1, "spatial.lds": 0, "spatial.xcd_rows": 0},
-                    "ntl": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 1},
-                    "ntl_rows2": {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 2},
-                    "ntl_t2": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 2},
-                    "ntl_t2_band": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 2, "spatial.xcd_rows": 0},
+# spatial kernels of a stage-API pass (no sample handles: those are restir_render's, test_spatial_handles_*):
+# k_spatial1_ntl (n_t staged, N = 1 biased; _t2: 32x16 tiles) in several XCD tile orders, k_spatial2_ntl, k_spatial1u,
+# the general kernels
+SPATIAL_VARIANTS = {"default": {},
+                    "ntl": {"spatial.lean": 1, "spatial.th": 1},
+                    "ntl_band": {"spatial.lean": 1, "spatial.th": 1, "spatial.xcd_rows": 0},
+                    "ntl_rows2": {"spatial.lean": 1, "spatial.xcd_rows": 2},
+                    "ntl_t2": {"spatial.lean": 1, "spatial.th": 2},
+                    "ntl_t2_band": {"spatial.lean": 1, "spatial.th": 2, "spatial.xcd_rows": 0},
                     # 2-D XCD chunks (2 x 2 tiles; the image's 3 tile columns leave a partial chunk on the right)
-                    "ntl_2d": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 1, "spatial.xcd_rows": 2,
-                               "spatial.xcd_cols": 2},
-                    "ntl_t2_2d": {"spatial.lean": 1, "spatial.lds": 3, "spatial.th": 2, "spatial.xcd_rows": 1,
-                                  "spatial.xcd_cols": 2},
+                    "ntl_2d": {"spatial.lean": 1, "spatial.th": 1, "spatial.xcd_rows": 2, "spatial.xcd_cols": 2},
+                    "ntl_t2_2d": {"spatial.lean": 1, "spatial.th": 2, "spatial.xcd_rows": 1, "spatial.xcd_cols": 2},
                     "general": {"spatial.lean": 0}}
-SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.lds": 3, "spatial.xcd_rows": 255, "spatial.xcd_cols": 255, "spatial.th": 0}
+SPATIAL_DEFAULTS = {"spatial.lean": 1, "spatial.xcd_rows": 255, "spatial.xcd_cols": 255, "spatial.th": 0}
 
 
-# every (scene, N, combine mode) through the default knobs ("gather" selects the lean gather kernel for N = 1 biased
-# and the general kernels otherwise); the other variants differ only for N = 1 biased passes, so they run only there
-SPATIAL_CASES = ([("gather", name, N, mode) for name in ("nightclub_128pt", "cornell_parallelogram") for N in (1, 2, 3)
+# every (scene, N, combine mode) through the default knobs; the other variants differ only for N = 1 biased passes,
+# so they run only there
+SPATIAL_CASES = ([("default", name, N, mode) for name in ("nightclub_128pt", "cornell_parallelogram") for N in (1, 2, 3)
                   for mode in ("biased", "unbiased", "unbiased_vis")] +
-                 [(lean, name, 1, "biased") for lean in SPATIAL_VARIANTS if lean != "gather"
+                 [(lean, name, 1, "biased") for lean in SPATIAL_VARIANTS if lean != "default"
                   for name in ("nightclub_128pt", "cornell_parallelogram")] +
                  [("ntl_2d", "cornell_parallelogram", N, mode) for N in (1, 2) for mode in ("unbiased_vis", "biased")
                   if (N, mode) != (1, "biased")])
@@ -417,7 +416,7 @@ def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased, M, 
     assert_grid(grid, res, name)
 
 
-@pytest.mark.parametrize("th", [1, 2, 3, 4])
+@pytest.mark.parametrize("th", [1, 2])
 @pytest.mark.parametrize("w,h,passes,M", [(96, 64, 1, 32), (37, 23, 2, 32), (130, 70, 2, 1), (64, 1, 1, 16)])
 def test_spatial_handles_frames_match_oracle(gpu, oracle, th, w, h, passes, M):
     """The biased passes over sample handles (k_spatial1h[_tN], round 5: W and M | light index planes staged in LDS
@@ -891,55 +890,6 @@ def test_full_size_c3_sequence_band_parity(gpu, oracle, N):
         assert np.array_equal(m[:, gs], np.ascontiguousarray(b[..., 3]).view(np.uint32)), f"C3 grid M rows {y0}.."
 
 
-@pytest.mark.parametrize("temporal,passes,N", [(0, 1, 1), (1, 2, 1), (1, 1, 2)])
-def test_frames_in_flight_match_serial_frames(gpu, oracle, temporal, passes, N):
-    """frames.inflight = 2: restir_render alternates two frame slots (buffers + stream), frame f + 1's primary rays
-    and RIS overlapping frame f's final shading.  A sequence of frames (temporal reuse threading each grid into the
-    next, predecessors released as it goes) must equal the serial frames bit for bit -- RGB, returned grids and
-    restir_download_rgb of the last frame -- and the stage API afterwards must see a joined context."""
-    name = "nightclub_128pt"
-    s = get_scene(name)
-    gpu.set_scene(s)
-    cam = scene.camera_for(name, W, H)
-    f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=passes, temporal_reuse=temporal)
-
-    def run(inflight, frames=5):
-        gpu.set_tuning("frames.inflight", inflight)
-        gpu.set_seed(SEED, 0)
-        out, prev = [], None
-        for fr in range(frames):
-            want_rgb = fr % 2 == 1                      # some frames asynchronous (no RGB read back)
-            rgb, grid = gpu.render_restir(prev if temporal else None, cam, W, H, f, want_rgb=want_rgb,
-                                          want_grid=bool(temporal) or fr == frames - 1)
-            out.append((rgb, grid.download() if grid is not None else None))
-            prev = grid
-        last = gpu.download_rgb(W, H)
-        gpu.set_tuning("frames.inflight", 1)
-        return out, last
-
-    try:
-        serial, last_s = run(1)
-        piped, last_p = run(2)
-        for fr, ((a, ga), (b, gb)) in enumerate(zip(serial, piped)):
-            if a is not None:
-                assert_bits(b, a, f"frame {fr} rgb")
-            if ga is not None:
-                for x, y in zip(ga, gb):
-                    assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), f"frame {fr} grid"
-        assert_bits(last_p, last_s, "download_rgb of the last frame")
-        # the stage API after pipelined frames (joined streams): RIS on the oracle's inputs stays bit-exact
-        _, osc, cam2 = setup(gpu, oracle, name, 1)
-        n_t, p_mat = oracle.gbuffer(osc, cam2, W, H)
-        gpu.upload(_abi.BUF_GBUF_N_T, n_t)
-        gpu.upload(_abi.BUF_GBUF_P_MAT, p_mat)
-        f1 = _abi.default_features(num_samples_in_reservoir=1)
-        gpu.stage_ris(cam2, f1, key(_abi.RESTIR_STAGE_RIS))
-        a, b, _ = oracle_ris(oracle, osc, f1, cam2, n_t, p_mat)
-        assert_bits(gpu.download(_abi.BUF_RES_A), a, "stage res_a after pipelined frames")
-    finally:
-        gpu.set_tuning("frames.inflight", 1)
-
-
 @pytest.mark.parametrize("name,passes,unbiased,vis,tiled,tune", [
     ("cornell_1024", 1, 0, 0, 0, {}), ("cornell_1024", 2, 0, 0, 0, {}), ("cornell_4096", 1, 1, 1, 0, {}),
     ("cornell_4096", 2, 1, 1, 0, {}), ("cornell_4096", 1, 1, 0, 0, {}), ("nightclub_128pt", 1, 0, 0, 0, {}),
@@ -948,8 +898,6 @@ def test_frames_in_flight_match_serial_frames(gpu, oracle, temporal, passes, N):
     # the window fix-up, on 32 x 8 and on 32 x 16 tiles
     ("cornell_1024", 1, 0, 0, 0, {"miss.gbuf": 1}), ("cornell_1024", 2, 0, 0, 0, {"miss.gbuf": 1}),
     ("cornell_1024", 1, 0, 0, 0, {"miss.gbuf": 1, "spatial.th": 2}), ("nightclub_128pt", 1, 0, 0, 0, {"miss.gbuf": 1}),
-    # a persistent RIS grid writes no flags: restir_render then passes none on (and RIS skips no stores)
-    ("cornell_1024", 1, 0, 0, 0, {"ris.blocks": 64, "miss.gbuf": 1}), ("cornell_4096", 1, 1, 1, 0, {"ris.blocks": 64}),
     # N = 2 (the reference default): k_spatial2_ntl and k_final_n2_sorted read the flags too
     ("cornell_1024", 1, 0, 0, 0, {"N": 2}), ("cornell_1024", 2, 0, 0, 0, {"N": 2}), ("nightclub_128pt", 1, 0, 0, 0, {"N": 2}),
     ("cornell_1024", 2, 0, 0, 1, {"N": 2}), ("cornell_4096", 1, 1, 1, 0, {"N": 2})])
@@ -985,7 +933,6 @@ def test_miss_tiles_match_full_reads(gpu, name, passes, unbiased, vis, tiled, tu
         gpu.set_tuning("miss.tiles", 1)
         gpu.set_tuning("miss.gbuf", 2)
         gpu.set_tuning("spatial.th", 0)
-        gpu.set_tuning("ris.blocks", 0)
     assert_bits(on_rgb, off_rgb, f"{name} rgb")
     for a, b in zip(off_grid, on_grid):
         assert np.array_equal(np.asarray(a).view(np.uint32), np.asarray(b).view(np.uint32)), f"{name} grid"

@@ -7,7 +7,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # knobs that select timing / frame-slot behaviour, not a kernel's launch shape (the bench sets them itself)
-NOT_SHAPES = {"frames.inflight", "mis.chunk", "timing.every", "timing.fence", "timing.mask"}
+NOT_SHAPES = {"mis.chunk", "timing.every", "timing.fence", "timing.mask"}
 
 
 def _knobs():

@@ -143,6 +143,13 @@ def gemm_prewarm(torch, local, ms):
     del a, b
 
 
+def camera_record(framing):
+    """The JSON record of a config's camera framing (config.camera; JSON types, so records compare after a round trip)."""
+    from romis_amd import scene
+    assert framing == "framed", framing
+    return json.loads(json.dumps(dict(scene.CORNELL_FRAMED, kind="framed (scene.CORNELL_FRAMED)")))
+
+
 def committed_traffic(cfg):
     """The spatial kernel's HBM bytes per launch from profiles/traffic.json (written by
     scripts/collect_profiles.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench), used
@@ -166,7 +173,7 @@ def committed_traffic(cfg):
         for entries, profile in groups:
             for e in entries:
                 rc = e.get("config") or {}
-                if e.get("xcd_order", "chunks") == "chunks" and all(rc.get(k) == cfg.get(k) for k in keys):
+                if e.get("variant", e.get("xcd_order", "chunks")) == "chunks" and all(rc.get(k) == cfg.get(k) for k in keys):
                     return e["traffic_bytes_per_launch"], profile
     except (OSError, ValueError, KeyError):
         pass
@@ -603,8 +610,8 @@ def main():
            "tiles": [tx, ty], "M": cf["M"], "N": args.N, "k": args.k, "r": args.r, "passes": passes,
            "temporal": cf["temporal"], "unbiased": cf["unbiased"], "spatial_visibility": cf["vis"],
            "parallelism": f"screen tiles {tx}x{ty}, " + (f"RCCL reservoir halo {args.r}px" if halo else f"ghost {ghost}px")}
-    if cf.get("camera") == "framed":
-        cfg["camera"] = dict(scene.CORNELL_FRAMED, kind="framed (scene.CORNELL_FRAMED)")
+    if cf.get("camera"):
+        cfg["camera"] = camera_record(cf["camera"])
 
     # roofline of the spatial pass: algorithmic bytes per pixel = read 32 (own G-buffer) + 32 N (own
     # reservoir), write 32 N; neighbour gathers are cache traffic, not counted

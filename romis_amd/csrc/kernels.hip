@@ -88,8 +88,9 @@ extern "C" __global__ __launch_bounds__(256) void k_primary_lds(SceneDev s, Regi
 // LT: the light table's form (host-detected scene properties; genCanonicalSamples' switch, light.cpp:55-78, reduces
 // to one case, so the candidate loop carries no lane-divergent light-type branch):
 //   kLtGeneral  7 float4 per light (SceneDev::lights);
-//   kLtPoint    every light a point light (light_types == 1): the compact table SceneDev::light_c2, 2 float4 per
-//               light (rows 0 and 3 of its record: position, colour);
+//   kLtPoint    every light a point light (light_types == 1): the compact table SceneDev::light_c2, two planes (rows 0
+//               and 3 of every record: positions, then colours -- a random light's 16-byte LDS read meets 16 bank
+//               groups instead of the 8 of 32-byte records);
 //   kLtGrid     every light a parallelogram with light 0's edges and one colour at all four of its corners
 //               (SceneDev::lights_grid: the reference's regularLightGrid, scene.cpp:5-28): light_c2 holds its
 //               corner v0 and colour; the shared edges are read from light 0's record, and the two identical
@@ -173,13 +174,15 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
             };
             auto sample = [&](uint32_t c, v3& pos, v3& col) {
                 const float4* lt = record(c);
-                if (LT == kLtPoint) {
-                    pos = xyz(lt[0]); col = xyz(lt[1]);
+                if (LT == kLtPoint) {   // the light_c2 planes: position at [i], colour at [L + i]
+                    const uint32_t i = uniform_index(draw(ps, 4u * c), L);
+                    pos = xyz(lights[i]); col = xyz(lights[L + i]);
                 } else if (LT == kLtGrid) {   // sampleParallelogramLight, as sample_rec's type-2 case
+                    const uint32_t i = uniform_index(draw(ps, 4u * c), L);
                     float a = rand01(draw(ps, 4u * c + 1u));
                     float b = rand01(draw(ps, 4u * c + 2u));
-                    pos = vadd(vadd(xyz(lt[0]), vscale(shared_row(1), a)), vscale(shared_row(2), b));
-                    const v3 gc = xyz(lt[1]);
+                    pos = vadd(vadd(xyz(lights[i]), vscale(shared_row(1), a)), vscale(shared_row(2), b));
+                    const v3 gc = xyz(lights[L + i]);
                     const v3 m = vmix(gc, gc, a);   // = vmix(c0, c1, a) = vmix(c2, c3, a): all four corners are gc
                     col = vmix(m, m, b);
                 } else if (LT == kLtRegular) {   // the corner of light i by arithmetic (scene.cpp:14-15)
@@ -1072,13 +1075,13 @@ __device__ __forceinline__ void h_stage(const SceneDev& s, const Region& rg, con
                                              (__attribute__((address_space(3))) void*)(l_m + kThreads * k + w64), 4, 0, 0);
         }
     }
-    // light table: entries d = 0 .. L positions, L + 1 .. 2L + 1 colours (light_c2 rows 0 and 1); d = L and 2L + 1 are
+    // light table: entries d = 0 .. L positions, L + 1 .. 2L + 1 colours (the light_c2 planes); d = L and 2L + 1 are
     // the zero sample's, stored by two threads
     const uint32_t L = s.num_lights, nd = 2u * L + 2u;
     for (uint32_t d0 = 0; d0 < nd; d0 += kThreads) {
         const uint32_t d = d0 + threadIdx.x;
         if (d < nd && d != L && d != 2u * L + 1u) {
-            const float4* src = d < L ? s.light_c2 + 2u * d : s.light_c2 + 2u * (d - L - 1u) + 1u;
+            const float4* src = d < L ? s.light_c2 + d : s.light_c2 + (d - 1u);
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
                                              (__attribute__((address_space(3))) void*)(l_lt + d0 + w64), 16, 0, 0);
         }

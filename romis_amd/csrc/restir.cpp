@@ -1026,10 +1026,12 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     std::vector<float> lc4(16 * std::max<uint32_t>(pgram ? num_lights : 1u, 1u), 0.0f);
     for (uint32_t i = 0; pgram && i < num_lights; i++) std::memcpy(&lc4[16 * i], &lt[28 * i], 64);
     ST_TRY(c->light_c4.upload(lc4.data(), lc4.size() * 4, c->stream));
+    // two planes (SceneDev::light_c2): rows 0 of every light, then rows 3 -- a random light's 16-byte read from an LDS
+    // copy then lands on one of 16 bank groups instead of 8 (32-byte records)
     std::vector<float> lc2(8 * std::max<uint32_t>(num_lights, 1), 0.0f);
     for (uint32_t i = 0; i < num_lights; i++) {
-        std::memcpy(&lc2[8 * i], &lt[28 * i], 16);
-        std::memcpy(&lc2[8 * i + 4], &lt[28 * i + 12], 16);
+        std::memcpy(&lc2[4 * i], &lt[28 * i], 16);
+        std::memcpy(&lc2[4 * (num_lights + i)], &lt[28 * i + 12], 16);
     }
     ST_TRY(c->light_c2.upload(lc2.data(), lc2.size() * 4, c->stream));
     std::vector<float> lcol(4 * std::max<uint32_t>(num_lights, 1), 0.0f);   // c0 of every light (kLtRegular)

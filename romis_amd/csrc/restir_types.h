@@ -52,7 +52,8 @@ struct SceneDev {
     uint32_t num_lights;
     uint32_t light_types;      // bit t set <=> a light of type t is present
     float light_scale;         // L when 1/L is a power of two (then p / (1/L) == p * L exactly), else 0
-    const float4* light_c2;    // compact table: rows 0 and 3 of every light's record (p0 / position, first colour)
+    const float4* light_c2;    // compact table, two planes: row 0 of every light's record (p0 / position), then row 3
+                               // (first colour) -- light i's rows at [i] and [num_lights + i]
     uint32_t lights_grid;      // every light a parallelogram with light 0's edges (rows 1, 2) and c0 = c1 = c2 = c3
     const float4* light_c4;    // rows 0..3 of every light's record (v0, edge01, edge02, c0): the kLtPgram table
     uint32_t lights_pgram;     // every light a parallelogram with c0 = c1 = c2 = c3

@@ -8,8 +8,8 @@ OUT=$REPO/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$REPO" || exit 1
 export TMPDIR=/tmp
-for C in c1 c2 c3 c4 c5; do
-    STEPS=200; WARM=20; [ $C = c5 ] && STEPS=30 && WARM=5
+for C in c1 c2 c3 c4 c5 c4f c5f; do
+    STEPS=200; WARM=20; case $C in c5|c5f) STEPS=30; WARM=5;; c4f) STEPS=100;; esac
     timeout -k 10 300 python3 bench.py --config $C --steps $STEPS --warmup $WARM > "$OUT/bench_$C.json" 2> "$OUT/bench_$C.err" || { tail -5 "$OUT/bench_$C.err"; exit 60; }
     echo "$C $(python3 -c "import json,sys; d=json.load(open('$OUT/bench_$C.json')); r=d.get('roofline') or {}; print(d['ms_per_step'], d['value'], r.get('avg_launch_us'), r.get('frac'), (d.get('roofline_ris') or {}).get('frac'))")"
 done

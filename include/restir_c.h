@@ -486,19 +486,23 @@ typedef enum restir_kernel {
     RESTIR_K_COUNT = 7
 } restir_kernel;
 restir_status restir_enable_timing(restir_ctx* ctx, int enable);
-/* Launch-shape knobs (never change results): "primary.blocks|lds|2d", "ris.blocks|lds", "spatial.xcd|blocks|lean",
- * "final.blocks|lds|2d", "fuse.primary_ris" (restir_render runs primary rays + RIS as one kernel, default 1).  *.blocks = persistent grid cap (0 = one block per work item).  "timing.mask": the
- * kernels (bit 1 << RESTIR_K_*) restir_enable_timing brackets with HIP events (default all).  "bvh.max_leaf":
- * triangles per BVH leaf for the next restir_set_scene (default 2).  "layout.records": restir_render's buffers as
- * per-pixel records [n_t, res_a, res_b] (1) or SoA planes (0, default).  "ris.compact": initial RIS (N = 1, 2) reads
- * a compact light table when the scene allows one -- point lights only, a light grid, one-colour parallelograms --
- * instead of the 7-float4 records (default 1; restir_set_scene detects the form bit for bit).  Round 4:
- * "spatial.xcd_rows|xcd_cols" (the spatial pass's XCD chunk shape; 255 = automatic), "spatial.th" (1: 32x8, 2: 32x16
- * tiles, 0: by width), "spatial.lds" (3: the n_t window in LDS, 0: gathers), "ris.late" (stage the light table after
- * the primary rays, only for tiles that need it), "final.miss" (final shading reads only p_mat and (pos, W) for a
- * primary-ray miss), "miss.tiles" (background-tile flags from RIS to the spatial passes and final shading, N = 1 without
- * temporal reuse), "miss.gbuf" (0 / 1 / 2 = auto: RIS also skips background tiles' G-buffer stores), "frames.inflight"
- * (1 / 2 frame slots), "timing.every" / "timing.fence" (event sampling).  All default on where measured faster. */
+/* Launch-shape knobs (never change results): "primary.lds", "ris.lds", "final.lds" (stage the BVH / light table in
+ * LDS when it fits), "fuse.primary_ris" (restir_render runs primary rays + RIS as one kernel), "spatial.lean" (the
+ * lean N = 1 / 2 passes; 0: the general kernels), "timing.mask": the kernels (bit 1 << RESTIR_K_*) restir_enable_timing
+ * brackets with HIP events (default all).  "bvh.max_leaf": triangles per BVH leaf for the next restir_set_scene
+ * (default 2).  "layout.records": restir_render's buffers as per-pixel records [n_t, res_a, res_b] (1) or SoA planes
+ * (0, default).  "ris.compact": initial RIS (N = 1, 2) reads a compact light table when the scene allows one -- point
+ * lights only, a light grid, one-colour parallelograms -- instead of the 7-float4 records (default 1; restir_set_scene
+ * detects the form bit for bit).  "spatial.xcd_rows|xcd_cols" (the spatial pass's XCD chunk shape; 255 = automatic),
+ * "spatial.th" (0: auto, 1: 32x8, 2: 32x16 tiles), "spatial.handles" (N = 1 biased passes over a point-light scene read
+ * sample handles, k_spatial1h; default 1), "ris.late" (stage the light table after the primary rays, only for tiles that
+ * need it), "final.sort" (bin each tile's shadow rays by target), "final.miss" (final shading reads only p_mat and
+ * (pos, W) for a primary-ray miss), "miss.tiles" (background-tile flags from RIS to the spatial passes and final
+ * shading, N <= 2 without temporal reuse), "miss.gbuf" (0 / 1 / 2 = auto: RIS also skips background tiles' G-buffer
+ * stores), "timing.every" / "timing.fence" (event sampling), "mis.chunk" (R-OMIS samples per launch pair).  All default
+ * on where measured faster.  Round 5 removed the knobs measured slower in two rounds (persistent *.blocks grids, the
+ * RIS work queue, the gather-only spatial pass, non-XCD / row-wave tile orders, 1-D primary / final maps, frames in
+ * flight): unknown keys are RESTIR_ERR_INVALID. */
 restir_status restir_set_tuning(restir_ctx* ctx, const char* key, int value);
 restir_status restir_timings(restir_ctx* ctx, double* ms /*[RESTIR_K_COUNT]*/, uint64_t* launches /*[RESTIR_K_COUNT]*/);
 restir_status restir_reset_timings(restir_ctx* ctx);

@@ -113,7 +113,8 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                                           const float4* lights, const Bvh& bvh, float4 nt, float4 pm, uint32_t x,
                                           uint32_t y, size_t p, float4* __restrict__ ra, float4* __restrict__ rb,
                                           float2* __restrict__ rdbg, float* __restrict__ rp, const GlTabs& tb,
-                                          float* __restrict__ hw = nullptr, uint32_t* __restrict__ hm = nullptr) {
+                                          float* __restrict__ hw = nullptr, uint32_t* __restrict__ hm = nullptr,
+                                          bool store_res = true) {
     const uint32_t L = s.num_lights;
     uint32_t hidx = L;   // the held sample's light index for the handle planes (k_spatial1h; L = the zero sample)
     const size_t npx = (size_t)rg.vw * rg.vh;
@@ -237,7 +238,9 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
         } else if (NT == 1 && rp) {
             rp[p] = target_pdf(s, f, make_px(s, nt, pm, origin, p), r[0].pos, r[0].col, tb);   // no lights: the initial sample
         }
-        for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, ridx(rg, j, p), j * npx + p);
+        // store_res = false: the sample handles are the reservoirs' only reader (restir_render's handle passes)
+        if (store_res || rdbg)
+            for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, ridx(rg, j, p), j * npx + p);
         if (NT == 1 && LT == kLtPoint && hw) { hw[p] = r[0].W; hm[p] = r[0].M | (hidx << 24); }
     }
 }
@@ -290,7 +293,8 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
                                                  float4* __restrict__ p_mat, float4* __restrict__ n_t2,
                                                  float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
                                                  float* __restrict__ rp, uint32_t late_ok, uint8_t* __restrict__ tmiss,
-                                                 uint32_t skip_res, float* __restrict__ hw, uint32_t* __restrict__ hm) {
+                                                 uint32_t skip_res, float* __restrict__ hw, uint32_t* __restrict__ hm,
+                                                 uint32_t res_dead) {
     const uint32_t bvh_f4 = 2u * s.num_nodes + 3u * s.num_tris;
     const float4* lights = global_lights<LT>(s);
     const uint32_t items = work_items(rg);
@@ -334,7 +338,8 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         // pdfs are not stored -- the first spatial pass substitutes them from the flag; bit 1 (above), nor its G-buffer
         // records (a single unbiased pass, which substitutes those too)
         if (live && (any || !tmiss || !(skip_res & 1u)))
-            ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb, hw, hm);
+            ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb, hw, hm,
+                              !(hw && res_dead));
         return;
     }
     for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {
@@ -343,7 +348,8 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         if (!work_pixel(rg, item, x, y, p)) continue;
         float4 nt, pm;
         primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, nt, pm);
-        ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb, hw, hm);
+        ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb, hw, hm,
+                          !(hw && res_dead));
     }
 }
 
@@ -394,9 +400,9 @@ ROMIS_RIS_KERNEL_LT(2, false, kLtPgram, k_ris_n2_pg, ROMIS_RIS_ATTR)
                                                           uint32_t key, float4* n_t, float4* p_mat, float4* n_t2,      \
                                                           float4* ra, float4* rb, float2* rdbg, float* rp,             \
                                                           uint32_t late_ok, uint8_t* tmiss, uint32_t skip_res,         \
-                                                          float* hw, uint32_t* hm) {                                   \
+                                                          float* hw, uint32_t* hm, uint32_t res_dead) {                \
         primary_ris_body<NT, LDS, LT>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp, late_ok, tmiss, skip_res,   \
-                                      hw, hm);                                                                         \
+                                      hw, hm, res_dead);                                                               \
     }
 #define ROMIS_PRIMARY_RIS_KERNEL(NT, LDS, NAME, ATTR) ROMIS_PRIMARY_RIS_KERNEL_LT(NT, LDS, kLtGeneral, NAME, ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(1, true, k_primary_ris_n1_lds, ROMIS_RIS1_ATTR)
@@ -719,11 +725,17 @@ struct Comb1 {
 #ifndef ROMIS_FLAG_SMEM
 #define ROMIS_FLAG_SMEM 1   // a block's single background-tile flag through the scalar cache (tiles_known_miss)
 #endif
-// Tile of block b (XCD b % 8, block b runs on XCD b % 8): XCD x owns every 8th chunk of rg.xcd_rows tile
-// rows (chunks x, x + 8, x + 16, ...), walked row-major, so its L2 holds the chunk's G-buffer and reservoirs
-// while the gathers reach 10 px across tile borders; interleaving short chunks spreads cheap (background)
-// and expensive rows evenly over the XCDs -- contiguous bands left the background XCDs idle (1.28x the mean
-// work on the busiest XCD at C2, 1.02x with 2-row chunks).  rg.xcd_rows = 0: one contiguous band per XCD.
+#ifndef ROMIS_XCD_BAL
+#define ROMIS_XCD_BAL 1   // the chunks left after the last full round of 8 are split evenly over the XCDs (xcd_grid)
+#endif
+// Tile of block b (XCD b % 8, block b runs on XCD b % 8): XCD x owns every 8th chunk of rg.xcd_rows tile rows (or
+// of xcd_rows x xcd_cols tiles: 2-D chunks numbered row-major), walked row-major, so its L2 holds the chunk's G-buffer
+// and reservoirs while the neighbourhoods reach 10 px across tile borders; interleaving short chunks spreads cheap
+// (background) and expensive rows evenly over the XCDs -- contiguous bands left the background XCDs idle (1.28x the
+// mean work on the busiest XCD at C2, 1.02x with 2-row chunks).  The chunks of the last, partial round (rg.xcd_full
+// = blocks per XCD in the full rounds, xcd_grid) are cut into 8 contiguous runs of rg.xcd_run tile slots, one per
+// XCD: a partial round of whole chunks left 1-7 XCDs a chunk more than the others (C2: 5 against 4).
+// rg.xcd_rows = 0: one contiguous band per XCD.
 __device__ __forceinline__ bool xcd_tile(const Region& rg, uint32_t T, uint32_t b, uint32_t& tile) {
     const uint32_t x = b % 8u, j = b / 8u;
     if (rg.xcd_rows == 0u) {
@@ -732,28 +744,40 @@ __device__ __forceinline__ bool xcd_tile(const Region& rg, uint32_t T, uint32_t 
         return j < q + (x < rem ? 1u : 0u);
     }
     const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
-    if (rg.xcd_cols == 0u || rg.xcd_cols >= ntx) {
-        const uint32_t chunk = rg.xcd_rows * ntx;
-        const uint32_t i = j / chunk;
-        tile = ((x + 8u * i) * rg.xcd_rows) * ntx + (j - i * chunk);
+    const bool rows = rg.xcd_cols == 0u || rg.xcd_cols >= ntx;
+    const uint32_t cw = rows ? ntx : rg.xcd_cols, ch = rg.xcd_rows * cw;
+    uint32_t c, k;   // chunk, tile slot in the chunk
+    if (j < rg.xcd_full) {
+        const uint32_t i = j / ch;
+        c = x + 8u * i;
+        k = j - i * ch;
+    } else {
+        const uint32_t r = j - rg.xcd_full;
+        if (r >= rg.xcd_run) return false;
+        const uint32_t q = x * rg.xcd_run + r, i = q / ch;
+        c = 8u * (rg.xcd_full / ch) + i;
+        k = q - i * ch;
+    }
+    if (rows) {
+        tile = c * ch + k;
         return tile < T;
     }
-    // 2-D chunks of xcd_rows x xcd_cols tiles, numbered row-major over the image; XCD x takes chunks x, x + 8, ...
-    const uint32_t cw = rg.xcd_cols, ncx = (ntx + cw - 1u) / cw, chunk = rg.xcd_rows * cw;
-    const uint32_t i = j / chunk, k = j - i * chunk, c = x + 8u * i;
+    const uint32_t ncx = (ntx + cw - 1u) / cw;
     const uint32_t cr = c / ncx, tr = k / cw;
     const uint32_t col = (c - cr * ncx) * cw + (k - tr * cw);
     tile = (cr * rg.xcd_rows + tr) * ntx + col;
     return col < ntx && tile < T;
 }
 
-// Blocks for xcd_tile's order over ntx x nty tiles (rg.xcd_rows, rg.xcd_cols set): every XCD gets as many as the one
-// that owns the most chunks.
-inline uint32_t xcd_grid(const Region& rg, uint32_t ntx, uint32_t nty) {
+// Blocks for xcd_tile's order over ntx x nty tiles (rg.xcd_rows, rg.xcd_cols set); sets rg.xcd_full / xcd_run.
+inline uint32_t xcd_grid(Region& rg, uint32_t ntx, uint32_t nty) {
     if (rg.xcd_rows == 0u) return ntx * nty;
-    const uint32_t cw = (rg.xcd_cols == 0u || rg.xcd_cols >= ntx) ? ntx : rg.xcd_cols;
+    const uint32_t cw = (rg.xcd_cols == 0u || rg.xcd_cols >= ntx) ? ntx : rg.xcd_cols, ch = rg.xcd_rows * cw;
     const uint32_t chunks = ((nty + rg.xcd_rows - 1u) / rg.xcd_rows) * ((ntx + cw - 1u) / cw);
-    return 8u * ((chunks + 7u) / 8u) * rg.xcd_rows * cw;
+    const uint32_t rounds = ROMIS_XCD_BAL ? chunks / 8u : (chunks + 7u) / 8u;
+    rg.xcd_full = rounds * ch;
+    rg.xcd_run = (chunks > 8u * rounds) ? ((chunks - 8u * rounds) * ch + 7u) / 8u : 0u;
+    return 8u * (rg.xcd_full + rg.xcd_run);
 }
 
 // MissTiles (restir_types.h): every RIS tile (32 x 8, numbered row-major over the view) meeting the pixel rect
@@ -2059,7 +2083,8 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
                         : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
     ROMIS_LAUNCH(k, dim3(items_of(rg)), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
                  cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr, tu.ris_late, tmiss,
-                 tmiss ? skip_res : 0u, lt == kLtPoint && f.N == 1 ? h.w : nullptr, lt == kLtPoint && f.N == 1 ? h.m : nullptr);
+                 tmiss ? skip_res : 0u, lt == kLtPoint && f.N == 1 ? h.w : nullptr, lt == kLtPoint && f.N == 1 ? h.m : nullptr,
+                 h.res_dead);
     return hipGetLastError();
 }
 

@@ -20,7 +20,7 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg, const CameraD
                               float* rp, const Tuning& tu, hipStream_t stream, uint8_t* tmiss = nullptr,
                               uint32_t skip_res = 0u,    // bit 0: background reservoirs, bit 1: background G-buffer
                               bool* tmiss_written = nullptr,    // the flags were written (else pass none on)
-                              Handles h = Handles{nullptr, nullptr});   // N = 1 point-light kernels: sample handles
+                              Handles h = Handles{nullptr, nullptr, 0u});   // N = 1 point-light kernels: sample handles
 // restir_render's N = 1 biased passes over sample handles (k_spatial1h): the scene, features and knobs allow them and
 // every M `passes` passes can produce fits the handle's 24 bits
 bool spatial_handles_ok(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes);
@@ -38,8 +38,8 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg, const FeaturesDev
                           float4* ob, float2* odbg, const float* rp_in, const float* rp_nb, float* rp_out,
                           bool* rp_written, const Tuning& tu, hipStream_t stream, uint8_t* vis_out = nullptr,
                           bool* vis_written = nullptr, MissTiles mt = MissTiles{nullptr, 0u, 0u},
-                          Handles hin = Handles{nullptr, nullptr},    // the input's sample handles (k_spatial1h)
-                          Handles hout = Handles{nullptr, nullptr});  // the output's, for a later pass
+                          Handles hin = Handles{nullptr, nullptr, 0u},    // the input's sample handles (k_spatial1h)
+                          Handles hout = Handles{nullptr, nullptr, 0u});  // the output's, for a later pass
 hipError_t launch_final(const SceneDev& s, const Region& rg, const FeaturesDev& f, const float* origin,
                         const float4* n_t, const float4* p_mat, const float4* ra, const float4* rb, float* rgb,
                         const Tuning& tu, hipStream_t stream, const uint8_t* vis_in = nullptr,

@@ -703,7 +703,7 @@ struct FrameBufs {
     // the sample-handle planes of rec[i]: W then M | index << 24, one 4-byte plane each (ensure_handles)
     Handles h(int i) const {
         float* w = hnd_()[i].as<float>();
-        return w ? Handles{w, reinterpret_cast<uint32_t*>(w + npx)} : Handles{nullptr, nullptr};
+        return w ? Handles{w, reinterpret_cast<uint32_t*>(w + npx), 0u} : Handles{nullptr, nullptr, 0u};
     }
     float4* nt(int i) const { return records ? rec_()[i].as<float4>() : n_t_().as<float4>(); }
     float4* ra(int i) const { return rec_()[i].as<float4>() + (records ? 1 : 0); }
@@ -1310,11 +1310,14 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                          (size_t)t.gwidth * t.gheight * 16u <= 0xFFFFFFFFull;
     if (handles)
         for (int i = 0; i < 2; i++) ST_TRY(fb.hnd_()[i].ensure((size_t)t.gwidth * t.gheight * 8u + 16u));
+    // the handle passes read RIS's samples through the handles alone (the last pass writes the returned grid)
+    Handles ris_handles = fb.h(cur);
+    ris_handles.res_dead = 1u;
     if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)
         bool written = false;
         TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),
                                                           fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st, tmiss, skip_mode,
-                                                          &written, handles ? fb.h(cur) : Handles{nullptr, nullptr}));
+                                                          &written, handles ? ris_handles : Handles{nullptr, nullptr, 0u}));
         if (!written) {   // (then RIS skipped nothing either: its skips need the flags)
             tmiss = nullptr;
             skip_mode = 0u;
@@ -1356,8 +1359,8 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                              // a background pixel holds M = f.M after RIS and after every biased pass; an unbiased pass
                              // sums its neighbours' M, which only pass 0 knows
                              MissTiles{tmiss, (!f.unbiased || pass == 0) ? f.M : 0u, (skip_mode & 2u) ? 1u : 0u},
-                             handles ? fb.h(cur) : Handles{nullptr, nullptr},
-                             handles && pass + 1 < passes ? fb.h(nxt) : Handles{nullptr, nullptr}));
+                             handles ? fb.h(cur) : Handles{nullptr, nullptr, 0u},
+                             handles && pass + 1 < passes ? fb.h(nxt) : Handles{nullptr, nullptr, 0u}));
         cur = nxt;
     }
     TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), fb.rgb().as<float>(),

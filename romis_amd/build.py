@@ -112,5 +112,28 @@ def main(argv=None) -> int:
     return 0
 
 
+
+# C++ programs over the C++ binding (include/romis_amd/restir.hpp): the reference-side callers the C++ wrapper tests
+# drive (tests/test_cpp_wrapper.py).  Built on the build host next to the library; the GPU box runs the prebuilt ones.
+CPP_PROGRAMS = [("render_scene.cpp", "render_scene"), ("render_threads.cpp", "render_threads"),
+                ("write_outputs.cpp", "write_outputs")]
+CPP_DIR = os.path.join(ROOT, "tests", "cpp")
+
+
+def build_cpp_program(src: str, out: str) -> str:
+    """g++ one program against libromis_amd.so (rpath to the in-tree build) when it is older than its sources."""
+    lib = LIB if os.path.exists(LIB) else build()
+    libdir = os.path.dirname(lib)
+    deps = [src, os.path.join(CPP_DIR, "scene_io.h"), os.path.join(ROOT, "include", "restir_c.h"),
+            os.path.join(ROOT, "include", "romis_amd", "restir.hpp")]
+    if _stale(out, deps):
+        subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-pthread", f"-I{os.path.join(ROOT, 'include')}",
+                               src, "-o", out, f"-L{libdir}", "-lromis_amd", f"-Wl,-rpath,{libdir}"])
+    return out
+
+
+def build_cpp_programs() -> list[str]:
+    return [build_cpp_program(os.path.join(CPP_DIR, src), os.path.join(OUT, out)) for src, out in CPP_PROGRAMS]
+
 if __name__ == "__main__":
     sys.exit(main())

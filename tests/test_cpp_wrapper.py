@@ -20,23 +20,10 @@ SRC_THREADS = os.path.join(ROOT, "tests", "cpp", "render_threads.cpp")
 BIN_THREADS = os.path.join(ROOT, "romis_amd", "_build", "render_threads")
 
 
-def _stale(target, deps):
-    return not os.path.exists(target) or any(os.path.getmtime(d) > os.path.getmtime(target) for d in deps)
-
-
 def build_cpp(src=SRC, out=BIN):
-    """Compile a test driver against libromis_amd.so (done by __graft_entry__.build() on the build host; on the
-    GPU box the prebuilt binary is used)."""
+    """A C++ program over the binding (romis_amd.build.build_cpp_program; __graft_entry__.build() prebuilds them)."""
     from romis_amd import build
-    lib = build.LIB if os.path.exists(build.LIB) else build.build()
-    libdir = os.path.dirname(lib)
-    deps = [src, os.path.join(ROOT, "tests", "cpp", "scene_io.h"), os.path.join(ROOT, "include", "restir_c.h"),
-            os.path.join(ROOT, "include", "romis_amd", "restir.hpp")]
-    if _stale(out, deps):
-        cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-pthread", f"-I{os.path.join(ROOT, 'include')}", src,
-               "-o", out, f"-L{libdir}", "-lromis_amd", f"-Wl,-rpath,{libdir}"]
-        subprocess.check_call(cmd)
-    return out
+    return build.build_cpp_program(src, out)
 
 
 def write_scene(path, sc, cam):

@@ -901,12 +901,13 @@ def test_full_size_c3_sequence_band_parity(gpu, oracle, N):
     # N = 2 (the reference default): k_spatial2_ntl and k_final_n2_sorted read the flags too
     ("cornell_1024", 1, 0, 0, 0, {"N": 2}), ("cornell_1024", 2, 0, 0, 0, {"N": 2}), ("nightclub_128pt", 1, 0, 0, 0, {"N": 2}),
     ("cornell_1024", 2, 0, 0, 1, {"N": 2}), ("cornell_4096", 1, 1, 1, 0, {"N": 2})])
-def test_miss_tiles_match_full_reads(gpu, name, passes, unbiased, vis, tiled, tune):
+def test_miss_tiles_match_full_reads(gpu, oracle, name, passes, unbiased, vis, tiled, tune):
     """MissTiles (miss.tiles = 1, the default): RIS flags the 32 x 8 tiles whose pixels all missed the scene, and the
     spatial passes and final shading write those tiles' known results without reading them.  Frames at 640 x 360
     (the Cornell box fills the middle: most tiles, and most unbiased neighbourhoods, are background), whole and as a
     ghost-zoned screen tile (2 x 2 plan, rank 3: the RIS, spatial and final regions start at different offsets), must
-    equal the frames rendered with the flags off bit for bit -- RGB and the returned grid."""
+    equal the frames rendered with the flags off bit for bit -- RGB and the returned grid -- and, for whole frames, the
+    oracle's frame (RGB)."""
     from romis_amd import restir
     tune = dict(tune)
     N = tune.pop("N", 1)
@@ -933,6 +934,9 @@ def test_miss_tiles_match_full_reads(gpu, name, passes, unbiased, vis, tiled, tu
         gpu.set_tuning("miss.tiles", 1)
         gpu.set_tuning("miss.gbuf", 2)
         gpu.set_tuning("spatial.th", 0)
+    if tile is None:
+        want, _, _ = oracle.render_frame(oracle.OracleScene(s), cam, f, w, h, SEED, 0, threads=16)
+        assert_bits(on_rgb, want, f"{name} rgb against the oracle")
     assert_bits(on_rgb, off_rgb, f"{name} rgb")
     for a, b in zip(off_grid, on_grid):
         assert np.array_equal(np.asarray(a).view(np.uint32), np.asarray(b).view(np.uint32)), f"{name} grid"

@@ -725,17 +725,13 @@ struct Comb1 {
 #ifndef ROMIS_FLAG_SMEM
 #define ROMIS_FLAG_SMEM 1   // a block's single background-tile flag through the scalar cache (tiles_known_miss)
 #endif
-#ifndef ROMIS_XCD_BAL
-#define ROMIS_XCD_BAL 1   // the chunks left after the last full round of 8 are split evenly over the XCDs (xcd_grid)
-#endif
-// Tile of block b (XCD b % 8, block b runs on XCD b % 8): XCD x owns every 8th chunk of rg.xcd_rows tile rows (or
-// of xcd_rows x xcd_cols tiles: 2-D chunks numbered row-major), walked row-major, so its L2 holds the chunk's G-buffer
-// and reservoirs while the neighbourhoods reach 10 px across tile borders; interleaving short chunks spreads cheap
-// (background) and expensive rows evenly over the XCDs -- contiguous bands left the background XCDs idle (1.28x the
-// mean work on the busiest XCD at C2, 1.02x with 2-row chunks).  The chunks of the last, partial round (rg.xcd_full
-// = blocks per XCD in the full rounds, xcd_grid) are cut into 8 contiguous runs of rg.xcd_run tile slots, one per
-// XCD: a partial round of whole chunks left 1-7 XCDs a chunk more than the others (C2: 5 against 4).
-// rg.xcd_rows = 0: one contiguous band per XCD.
+// Tile of block b (XCD b % 8, block b runs on XCD b % 8): XCD x owns every 8th chunk of rg.xcd_rows tile
+// rows (chunks x, x + 8, x + 16, ...), walked row-major, so its L2 holds the chunk's G-buffer and reservoirs
+// while the neighbourhoods reach 10 px across tile borders; interleaving short chunks spreads cheap (background)
+// and expensive rows evenly over the XCDs -- contiguous bands left the background XCDs idle (1.28x the mean
+// work on the busiest XCD at C2, 1.02x with 2-row chunks).  rg.xcd_rows = 0: one contiguous band per XCD.
+// (Round 5: splitting the last, partial round of chunks evenly over the XCDs instead measured no faster -- C2
+// handle pass 67.2 vs 66.8 us, the n_t-window pass with 2-D chunks 74.5 vs 70.6, C4f 431 vs 434; profiles/r5.)
 __device__ __forceinline__ bool xcd_tile(const Region& rg, uint32_t T, uint32_t b, uint32_t& tile) {
     const uint32_t x = b % 8u, j = b / 8u;
     if (rg.xcd_rows == 0u) {
@@ -744,40 +740,28 @@ __device__ __forceinline__ bool xcd_tile(const Region& rg, uint32_t T, uint32_t 
         return j < q + (x < rem ? 1u : 0u);
     }
     const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
-    const bool rows = rg.xcd_cols == 0u || rg.xcd_cols >= ntx;
-    const uint32_t cw = rows ? ntx : rg.xcd_cols, ch = rg.xcd_rows * cw;
-    uint32_t c, k;   // chunk, tile slot in the chunk
-    if (j < rg.xcd_full) {
-        const uint32_t i = j / ch;
-        c = x + 8u * i;
-        k = j - i * ch;
-    } else {
-        const uint32_t r = j - rg.xcd_full;
-        if (r >= rg.xcd_run) return false;
-        const uint32_t q = x * rg.xcd_run + r, i = q / ch;
-        c = 8u * (rg.xcd_full / ch) + i;
-        k = q - i * ch;
-    }
-    if (rows) {
-        tile = c * ch + k;
+    if (rg.xcd_cols == 0u || rg.xcd_cols >= ntx) {
+        const uint32_t chunk = rg.xcd_rows * ntx;
+        const uint32_t i = j / chunk;
+        tile = ((x + 8u * i) * rg.xcd_rows) * ntx + (j - i * chunk);
         return tile < T;
     }
-    const uint32_t ncx = (ntx + cw - 1u) / cw;
+    // 2-D chunks of xcd_rows x xcd_cols tiles, numbered row-major over the image; XCD x takes chunks x, x + 8, ...
+    const uint32_t cw = rg.xcd_cols, ncx = (ntx + cw - 1u) / cw, chunk = rg.xcd_rows * cw;
+    const uint32_t i = j / chunk, k = j - i * chunk, c = x + 8u * i;
     const uint32_t cr = c / ncx, tr = k / cw;
     const uint32_t col = (c - cr * ncx) * cw + (k - tr * cw);
     tile = (cr * rg.xcd_rows + tr) * ntx + col;
     return col < ntx && tile < T;
 }
 
-// Blocks for xcd_tile's order over ntx x nty tiles (rg.xcd_rows, rg.xcd_cols set); sets rg.xcd_full / xcd_run.
-inline uint32_t xcd_grid(Region& rg, uint32_t ntx, uint32_t nty) {
+// Blocks for xcd_tile's order over ntx x nty tiles (rg.xcd_rows, rg.xcd_cols set): every XCD gets as many as the one
+// that owns the most chunks.
+inline uint32_t xcd_grid(const Region& rg, uint32_t ntx, uint32_t nty) {
     if (rg.xcd_rows == 0u) return ntx * nty;
-    const uint32_t cw = (rg.xcd_cols == 0u || rg.xcd_cols >= ntx) ? ntx : rg.xcd_cols, ch = rg.xcd_rows * cw;
+    const uint32_t cw = (rg.xcd_cols == 0u || rg.xcd_cols >= ntx) ? ntx : rg.xcd_cols;
     const uint32_t chunks = ((nty + rg.xcd_rows - 1u) / rg.xcd_rows) * ((ntx + cw - 1u) / cw);
-    const uint32_t rounds = ROMIS_XCD_BAL ? chunks / 8u : (chunks + 7u) / 8u;
-    rg.xcd_full = rounds * ch;
-    rg.xcd_run = (chunks > 8u * rounds) ? ((chunks - 8u * rounds) * ch + 7u) / 8u : 0u;
-    return 8u * (rg.xcd_full + rg.xcd_run);
+    return 8u * ((chunks + 7u) / 8u) * rg.xcd_rows * cw;
 }
 
 // MissTiles (restir_types.h): every RIS tile (32 x 8, numbered row-major over the view) meeting the pixel rect
@@ -1198,6 +1182,9 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
         }
     }
     __syncthreads();
+#ifdef ROMIS_H_PRIO   // build variants: static priority for one half of the block's waves (MI355X_MICROARCH.md)
+    if ((threadIdx.x >= 256u) == (ROMIS_H_PRIO == 1)) __builtin_amdgcn_s_setprio(1);
+#endif
     if (!live) return;   // no barrier follows
     const uint32_t own = (uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0);
     const float4 cn = l_nt[own];

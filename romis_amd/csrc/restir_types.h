@@ -98,8 +98,6 @@ struct Region {
     uint32_t ps, js;
     uint32_t xcd_rows;   // the lean spatial passes' XCD tile order (xcd_tile); 0 elsewhere
     uint32_t xcd_cols;   // chunk width in tiles (xcd_tile); 0 = the whole row of tiles
-    uint32_t xcd_full;   // xcd_tile: blocks per XCD in the full rounds of 8 chunks (xcd_grid)
-    uint32_t xcd_run;    // xcd_tile: tile slots per XCD of the last, partial round
 };
 
 // Background tiles (restir_render, N <= 2, no temporal reuse): the fused primary + RIS kernel writes one byte per

@@ -1103,7 +1103,7 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
                                                HandlesIn hi, float4* __restrict__ oa, float4* __restrict__ ob,
                                                float2* __restrict__ odbg, const float* __restrict__ rp_in,
                                                float* __restrict__ rp_out, float* __restrict__ how,
-                                               uint32_t* __restrict__ hom, MissTiles mt) {
+                                               uint32_t* __restrict__ hom, MissTiles mt, uint32_t odead) {
     constexpr uint32_t kTH = kTileH * TH;
     float4* const l_nt = g_lds;
     float* const l_w = reinterpret_cast<float*>(g_lds + apron_max(TH));
@@ -1122,8 +1122,10 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
             const int mx = tx0 + (int)((mw & 3u) * 8u + (ml & 7u)), my = ty0 + (int)((mw >> 2) * 8u + (ml >> 3));
             if (mx <= x1 && my <= y1) {
                 const uint32_t mp = (uint32_t)(my - (int)rg.vy0) * rg.vw + (uint32_t)(mx - (int)rg.vx0);
-                st_at(oa, mp << 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-                st_at(ob, mp << 4, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(mt.m)));
+                if (!odead) {
+                    st_at(oa, mp << 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+                    st_at(ob, mp << 4, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(mt.m)));
+                }
                 if (DBG) st_at(odbg, mp << 3, make_float2(ROMIS_FLT_MIN, 0.0f));
                 if (rp_out) rp_out[mp] = 0.0f;
                 if (how) { how[mp] = 0.0f; hom[mp] = mt.m | (L << 24); }
@@ -1182,9 +1184,6 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
         }
     }
     __syncthreads();
-#ifdef ROMIS_H_PRIO   // build variants: static priority for one half of the block's waves (MI355X_MICROARCH.md)
-    if ((threadIdx.x >= 256u) == (ROMIS_H_PRIO == 1)) __builtin_amdgcn_s_setprio(1);
-#endif
     if (!live) return;   // no barrier follows
     const uint32_t own = (uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0);
     const float4 cn = l_nt[own];
@@ -1195,8 +1194,10 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
     const Px cur = make_px(s, cn, cpm, origin, pix);
     if (cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z) &&
         __builtin_isfinite(cw) && __builtin_isfinite(ccol.x + ccol.y + ccol.z)) {
-        st_at(oa, pix << 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-        st_at(ob, pix << 4, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(cm & kHandleM)));
+        if (!odead) {
+            st_at(oa, pix << 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+            st_at(ob, pix << 4, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(cm & kHandleM)));
+        }
         if (DBG) st_at(odbg, pix << 3, make_float2(ROMIS_FLT_MIN, 0.0f));
         if (rp_out) rp_out[pix] = 0.0f;
         if (how) { how[pix] = 0.0f; hom[pix] = (cm & kHandleM) | (L << 24); }
@@ -1240,8 +1241,10 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
     float p = cmb.pd;
     if (!cmb.has_pd) p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, pos, col, tb);
     const float W = contribution_weight(p, cmb.macc, cmb.wsum);
-    st_at(oa, pix << 4, make_float4(pos.x, pos.y, pos.z, W));
-    st_at(ob, pix << 4, make_float4(col.x, col.y, col.z, __uint_as_float(cmb.macc)));
+    if (!odead) {   // odead: a later handle pass is the output's only reader
+        st_at(oa, pix << 4, make_float4(pos.x, pos.y, pos.z, W));
+        st_at(ob, pix << 4, make_float4(col.x, col.y, col.z, __uint_as_float(cmb.macc)));
+    }
     if (DBG) st_at(odbg, pix << 3, make_float2(cmb.wsum, cmb.chosen));
     if (rp_out) rp_out[pix] = p;
     if (how) { how[pix] = W; hom[pix] = cmb.macc | (cmb.li << 24); }
@@ -1254,8 +1257,9 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
     extern "C" __global__ __launch_bounds__(256 * TH) __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL1H_WPE))) void   \
     NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
          const float4* p_mat, HandlesIn hi, float4* oa, float4* ob, float2* odbg, const float* rp_in, float* rp_out,  \
-         float* how, uint32_t* hom, MissTiles mt) {                                                                   \
-        spatial1h_body<DBG, TH>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, hi, oa, ob, odbg, rp_in, rp_out, how, hom, mt); \
+         float* how, uint32_t* hom, MissTiles mt, uint32_t odead) {                                                   \
+        spatial1h_body<DBG, TH>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, hi, oa, ob, odbg, rp_in, rp_out, how, hom, mt,  \
+                                odead);                                                                                \
     }
 ROMIS_SPATIAL1H_KERNEL(false, 1, k_spatial1h)
 ROMIS_SPATIAL1H_KERNEL(true, 1, k_spatial1h_dbg)
@@ -2194,7 +2198,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
             const HandlesIn hi{hin.w, hin.m};
             auto k = hth == 2u ? (odbg ? k_spatial1h_t2_dbg : k_spatial1h_t2) : (odbg ? k_spatial1h_dbg : k_spatial1h);
             ROMIS_LAUNCH(k, dim3(grid), dim3(hth * kBlock), lds, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, hi, oa,
-                         ob, odbg, rp_in, rp_out, hout.w, hout.m, mt);
+                         ob, odbg, rp_in, rp_out, hout.w, hout.m, mt, hout.res_dead);
         } else if (th >= 2u) {
             // 32x16 tiles: the chunks hold half as many (twice as tall) tile rows
             const uint32_t nty2 = (rg.rh + 2u * kTileH - 1) / (2u * kTileH);

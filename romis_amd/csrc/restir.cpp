@@ -1360,7 +1360,9 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                              // sums its neighbours' M, which only pass 0 knows
                              MissTiles{tmiss, (!f.unbiased || pass == 0) ? f.M : 0u, (skip_mode & 2u) ? 1u : 0u},
                              handles ? fb.h(cur) : Handles{nullptr, nullptr, 0u},
-                             handles && pass + 1 < passes ? fb.h(nxt) : Handles{nullptr, nullptr, 0u}));
+                             // a pass before the last is read by the next one's handles alone: no reservoir planes
+                             handles && pass + 1 < passes ? Handles{fb.h(nxt).w, fb.h(nxt).m, 1u}
+                                                          : Handles{nullptr, nullptr, 0u}));
         cur = nxt;
     }
     TIMED(c, RESTIR_K_FINAL, launch_final(s, owned, f, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), fb.rgb().as<float>(),

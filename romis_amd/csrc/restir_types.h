@@ -117,7 +117,7 @@ struct MissTiles {
 struct Handles {
     float* w;
     uint32_t* m;
-    uint32_t res_dead;   // (RIS output) the handles are the reservoir planes' only reader: RIS skips their stores
+    uint32_t res_dead;   // (an output) the handles are the reservoir planes' only reader: RIS / the pass skips their stores
 };
 
 // Launch-shape knobs (restir_set_tuning); they never change results, only speed.

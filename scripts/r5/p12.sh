@@ -6,4 +6,4 @@ REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$REPO" || exit 1
 export TMPDIR=/tmp
 bash scripts/kbench_libs.sh r5p12/times "--only default --rounds 9 --frames 10" prio_hi prio_lo ris_w8 ris_w6 || exit 41
-bash scripts/kbench_libs.sh r5p12/times2 "--only default --rounds 9 --frames 10" prio_hi prio_lo ris_w8 ris_w6 || exit 42
+

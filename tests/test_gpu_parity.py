@@ -421,7 +421,8 @@ def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased, M, 
 def test_spatial_handles_frames_match_oracle(gpu, oracle, th, w, h, passes, M):
     """The biased passes over sample handles (k_spatial1h[_tN], round 5: W and M | light index planes staged in LDS
     beside the n_t window, point lights) at every tile height, ragged sizes, 1 and 2 passes: RGB and the returned grid
-    bit-exact with the oracle (render_utils.cpp:87-140, reservoir.cpp:40-66)."""
+    bit-exact with the oracle (render_utils.cpp:87-140, reservoir.cpp:40-66); a pass before the last writes only its
+    handles.  The RGB without a returned grid (bench.py's render) too."""
     name = "nightclub_128pt"
     s = get_scene(name)
     gpu.set_scene(s)
@@ -433,11 +434,14 @@ def test_spatial_handles_frames_match_oracle(gpu, oracle, th, w, h, passes, M):
     try:
         gpu.set_seed(SEED, 0)
         rgb, grid = gpu.render_restir(None, cam, w, h, f)
+        gpu.set_seed(SEED, 0)
+        rgb_ng, _ = gpu.render_restir(None, cam, w, h, f, want_grid=False)
     finally:
         gpu.set_tuning("spatial.th", 0)
     want, res, _ = oracle.render_frame(osc, cam, f, w, h, SEED, 0)
     assert_bits(rgb, want, f"th={th} {w}x{h} passes={passes}")
     assert_grid(grid, res, f"th={th} {w}x{h} passes={passes}")
+    assert_bits(rgb_ng, want, f"no grid th={th} {w}x{h} passes={passes}")
 
 
 @pytest.mark.parametrize("w,h,N,passes,M", [(1, 1, 1, 2, 32), (37, 23, 2, 2, 32), (33, 9, 1, 1, 1), (40, 24, 32, 1, 8),

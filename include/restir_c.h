@@ -260,7 +260,8 @@ restir_status restir_set_scene_textured(restir_ctx* ctx, const restir_mesh* mesh
  * a new reference to the frame's final reservoir grid.  `out_rgb` (nullable, host, width*height*3 floats,
  * row 0 = top) -- when NULL the call only enqueues work and returns without synchronising; the image stays
  * on the device (restir_download_rgb).  `tile` (nullable) restricts the frame to one screen tile of a
- * larger image (multi-GPU); NULL = the whole width x height image. */
+ * larger image (multi-GPU); NULL = the whole width x height image.  A tiled frame's grid is defined on the owned
+ * rect: its ghost ring (computed only for the owned pixels' spatial neighbourhoods) holds intermediate values. */
 restir_status restir_render(restir_ctx* ctx, const restir_camera* cam, const restir_features* features,
                             uint32_t width, uint32_t height, const restir_tile* tile,
                             const restir_frame* prev, restir_frame** out_next, float* out_rgb);

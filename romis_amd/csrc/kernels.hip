@@ -117,6 +117,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                                           bool store_res = true) {
     const uint32_t L = s.num_lights;
     uint32_t hidx = L;   // the held sample's light index for the handle planes (k_spatial1h; L = the zero sample)
+    float ha = 0.0f, hb = 0.0f;   // kLtRegular: its fractions (grid handles, k_spatial1g_t2)
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
     const float invL = 1.0f / (float)L;
@@ -218,7 +219,8 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 if (best != 0xFFFFFFFFu) {
                     sample(best, r[0].pos, r[0].col);
                     r[0].has_pd = true;
-                    if (LT == kLtPoint) hidx = uniform_index(draw(ps, 4u * best), L);
+                    if (LT == kLtPoint || LT == kLtRegular) hidx = uniform_index(draw(ps, 4u * best), L);
+                    if (LT == kLtRegular) { ha = rand01(draw(ps, 4u * best + 1u)); hb = rand01(draw(ps, 4u * best + 2u)); }
                 }
             } else {
                 for (uint32_t c = 0; c < c_end; c++) {
@@ -242,6 +244,8 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
         if (store_res || rdbg)
             for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, ridx(rg, j, p), j * npx + p);
         if (NT == 1 && LT == kLtPoint && hw) { hw[p] = r[0].W; hm[p] = r[0].M | (hidx << 24); }
+        if (NT == 1 && LT == kLtRegular && hw)   // grid handle: (W, M | i << 19, a, b) in one float4 plane
+            reinterpret_cast<float4*>(hw)[p] = make_float4(r[0].W, __uint_as_float(r[0].M | (hidx << 19)), ha, hb);
     }
 }
 
@@ -719,6 +723,27 @@ struct Comb1 {
     }
 };
 
+// Light-grid sample handles (round 5; SceneDev::lights_regular, the reference's regularLightGrid with RIS's kLtRegular
+// form): a sample is a point of light i's parallelogram at the fractions (a, b) of its two RIS draws, its colour mixed
+// at a and b -- a function of (i, a, b).  The handle is one float4 plane, (W, bits(M | i << 19), a, b): 16 B per pixel
+// instead of the reservoir's 32, index L the initial (0, 0) sample.
+constexpr uint32_t kHandleMG = 0x0007FFFFu;
+// the (position, colour) of grid sample (i, a, b), evaluated as kLtRegular's sample_reg (ris_pixel) does; col_tab = the
+// light colours (light_col or an LDS copy)
+__device__ __forceinline__ void grid_sample(const SceneDev& s, const float4* __restrict__ col_tab, uint32_t i, float a,
+                                            float b, v3& pos, v3& col) {
+    const bool zero = i >= s.num_lights;
+    const uint32_t j = zero ? 0u : i;
+    const float xl = (float)(j >> s.grid_ny_log2), yl = (float)(j & ((1u << s.grid_ny_log2) - 1u));
+    const v3 v0 = vadd(vadd(xyz(s.grid_start), vscale(xyz(s.grid_s01), xl)), vscale(xyz(s.grid_s02), yl));
+    const v3 p = vadd(vadd(v0, vscale(xyz(s.lights[1]), a)), vscale(xyz(s.lights[2]), b));
+    const v3 gc = xyz(col_tab[j]);
+    const v3 m = vmix(gc, gc, a);
+    const v3 c = vmix(m, m, b);
+    pos = zero ? mk(0.0f, 0.0f, 0.0f) : p;
+    col = zero ? mk(0.0f, 0.0f, 0.0f) : c;
+}
+
 #ifndef ROMIS_TAB_DMA
 #define ROMIS_TAB_DMA 1   // the biased passes stage powf's tables by LDS-DMA behind their own loads (gl_stage_tables_dma)
 #endif
@@ -835,18 +860,28 @@ __device__ __forceinline__ void ntl_stage_window(const Region& rg, const float4*
     }
 }
 
-template <bool DBG, uint32_t TH = 1>
+// GH (k_spatial1g_t2, a regular light grid): the input reservoirs arrive as grid handles (hg_in; ia / ib unused), one
+// 16-byte gather per accepted neighbour instead of two, the sample rebuilt by grid_sample from the light colours the
+// block stages in LDS behind the window; the output is written as a handle too (hg_out) and, unless odead (a later
+// handle pass is its only reader), as the reservoir planes.
+template <bool DBG, uint32_t TH = 1, bool GH = false>
 __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
                                                   v3 origin, const float4* __restrict__ n_t,
                                                   const float4* __restrict__ p_mat, const float4* __restrict__ ia,
                                                   const float4* __restrict__ ib, float4* __restrict__ oa,
                                                   float4* __restrict__ ob, float2* __restrict__ odbg,
                                                   const float* __restrict__ rp_in, float* __restrict__ rp_out,
-                                                  MissTiles mt) {
+                                                  MissTiles mt, const float4* __restrict__ hg_in = nullptr,
+                                                  float4* __restrict__ hg_out = nullptr, uint32_t odead = 0u) {
 #if !ROMIS_TAB_DMA
     const GlTabs tb = gl_stage_tables<false>();   // made visible by the window's barrier below
 #endif
     float4* const l_nt = g_lds;
+    float4* const l_col = g_lds + apron_max(TH);   // GH: the L light colours
+    const uint32_t L = s.num_lights;
+    auto put_handle = [&](uint32_t ofs, float W, uint32_t M, uint32_t li, float a, float b) {
+        if (GH && hg_out) st_at(hg_out, ofs, make_float4(W, __uint_as_float(M | (li << 19)), a, b));
+    };
     uint32_t tile;
     constexpr uint32_t kTH = kTileH * TH;   // tile rows
     const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
@@ -862,10 +897,13 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
             const int mx = tx0 + (int)((mw & 3u) * 8u + (ml & 7u)), my = ty0 + (int)((mw >> 2) * 8u + (ml >> 3));
             if (mx <= x1 && my <= y1) {
                 const uint32_t mo = ((uint32_t)(my - (int)rg.vy0) * rg.vw + (uint32_t)(mx - (int)rg.vx0)) << 4;
-                st_at(oa, mo, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-                st_at(ob, mo, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(mt.m)));
+                if (!odead) {
+                    st_at(oa, mo, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+                    st_at(ob, mo, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(mt.m)));
+                }
                 if (DBG) st_at(odbg, mo >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
                 if (rp_out) st_at(rp_out, mo >> 2, 0.0f);
+                put_handle(mo, 0.0f, mt.m, L, 0.0f, 0.0f);
             }
             return;   // block-uniform, before the window's barrier
         }
@@ -883,6 +921,7 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     const uint32_t pofs = ((uint32_t)(y - (int)rg.vy0) * rg.vw + (uint32_t)(x - (int)rg.vx0)) << 4;
     // the pixel's own records (coalesced), issued first
     float4 cpm = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ca = cpm, cb = cpm;
+    float4 ch = make_float4(0.0f, __uint_as_float(L << 19), 0.0f, 0.0f);   // GH: the own handle
     float pd_cached = 0.0f;
     if (live) {
         // a pixel of a background tile holds the known (0, W = 0), (0, M = mt.m) and pdf 0: RIS may not have stored
@@ -891,14 +930,26 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
         if (mixed && tile_flag_at(mt, rg, x, y) == 0u) {
             cpm = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(s.num_materials - 1u));
             cb.w = __uint_as_float(mt.m);
+            ch.y = __uint_as_float(mt.m | (L << 19));
         } else {
             cpm = ld_at(p_mat, pofs);
-            ca = ld_at(ia, pofs);
-            cb = ld_at(ib, pofs);
+            if (GH) {
+                ch = ld_at(hg_in, pofs);
+            } else {
+                ca = ld_at(ia, pofs);
+                cb = ld_at(ib, pofs);
+            }
             if (rp_in) pd_cached = ld_at(rp_in, pofs >> 2);
         }
     }
     ntl_stage_window<TH>(rg, n_t, l_nt, ax0, ay0, AW, n_apron);
+    if (GH) {   // the light colours behind the window (LDS-DMA, the same wait and barrier)
+        const uint32_t w64 = (threadIdx.x >> 6) << 6;
+        for (uint32_t d0 = 0; d0 < L; d0 += 256u * TH)
+            if (d0 + threadIdx.x < L)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(s.light_col + d0 + threadIdx.x),
+                                                 (__attribute__((address_space(3))) void*)(l_col + d0 + w64), 16, 0, 0);
+    }
 #if ROMIS_TAB_DMA
     const GlTabs tb = gl_stage_tables_dma();   // behind the block's own loads; made visible by the window's barrier
 #endif
@@ -941,6 +992,13 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     __syncthreads();
     if (!live) return;   // no barrier follows
     const float4 cn = l_nt[(uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0)];
+    const uint32_t cli = __float_as_uint(ch.y) >> 19;
+    if (GH) {   // the own reservoir from its handle
+        v3 p, c;
+        grid_sample(s, l_col, cli, ch.z, ch.w, p, c);
+        ca = make_float4(p.x, p.y, p.z, ch.x);
+        cb = make_float4(c.x, c.y, c.z, __uint_as_float(__float_as_uint(ch.y) & kHandleMG));
+    }
     const Px cur = make_px(s, cn, cpm, origin, pofs >> 4);
     // A primary-ray miss (value-initialised HitInfo: material kd = ks = 0, normal 0, P not NaN): its zero normal
     // rejects every neighbour (finite neighbour normals, s.normals_bounded: dot = +-0 < 0.906), and the target pdf of
@@ -948,10 +1006,13 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
     // with w = (0 * W) * M = +-0 (W finite): nothing is accepted, wSum stays FLT_MIN, M = M_own, W = 0.
     if (cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z) &&
         __builtin_isfinite(ca.w) && __builtin_isfinite(cb.x + cb.y + cb.z)) {
-        st_at(oa, pofs, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-        st_at(ob, pofs, make_float4(0.0f, 0.0f, 0.0f, cb.w));
+        if (!odead) {
+            st_at(oa, pofs, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+            st_at(ob, pofs, make_float4(0.0f, 0.0f, 0.0f, cb.w));
+        }
         if (DBG) st_at(odbg, pofs >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
         if (rp_out) st_at(rp_out, pofs >> 2, 0.0f);
+        put_handle(pofs, 0.0f, __float_as_uint(cb.w), L, 0.0f, 0.0f);
         return;
     }
     // depth / normal heuristic (render_utils.cpp:114-118), one shared reciprocal of the pixel's depth; both tests
@@ -974,29 +1035,47 @@ __device__ __forceinline__ void spatial1_ntl_body(const SceneDev& s, const Regio
             ok[n] = !(nd < 0.90630778703f) && !(fabsf(1.0f - q) > 0.1f);
         }
     }
-    float4 na[kLeanK], nb[kLeanK];
-    if (ok[0]) { na[0] = ld_at(ia, qo[0]); nb[0] = ld_at(ib, qo[0]); }
+    float4 na[kLeanK], nb[kLeanK];   // GH: na = the neighbour's handle
+    auto gather = [&](uint32_t n) {
+        if (GH) { na[n] = ld_at(hg_in, qo[n]); }
+        else { na[n] = ld_at(ia, qo[n]); nb[n] = ld_at(ib, qo[n]); }
+    };
+    if (ok[0]) gather(0);
     const float pd_cur = rp_in ? pd_cached : target_pdf(s, f, cur, xyz(ca), xyz(cb), tb);
     Comb1 cmb;
     cmb.pos = mk(0.0f, 0.0f, 0.0f); cmb.col = mk(0.0f, 0.0f, 0.0f);
     cmb.wsum = ROMIS_FLT_MIN; cmb.chosen = 0.0f; cmb.pd = 0.0f; cmb.macc = 0u; cmb.has_pd = false;
     cmb.h = ps + 2u * K * 0x9E3779B9u;
+    uint32_t hli = L;          // GH: the held sample's handle fields
+    float hfa = 0.0f, hfb = 0.0f;
 #pragma unroll
     for (uint32_t n = 0; n < kLeanK; n++) {
-        if (n + 1 < kLeanK && ok[n + 1]) { na[n + 1] = ld_at(ia, qo[n + 1]); nb[n + 1] = ld_at(ib, qo[n + 1]); }
+        if (n + 1 < kLeanK && ok[n + 1]) gather(n + 1);
         if (ok[n]) {
-            const v3 p = xyz(na[n]), c = xyz(nb[n]);
-            cmb.take(target_pdf(s, f, cur, p, c, tb), na[n].w, __float_as_uint(nb[n].w), p, c);
+            if (GH) {
+                const uint32_t hm = __float_as_uint(na[n].y), li = hm >> 19;
+                v3 p, c;
+                grid_sample(s, l_col, li, na[n].z, na[n].w, p, c);
+                if (cmb.take(target_pdf(s, f, cur, p, c, tb), na[n].x, hm & kHandleMG, p, c)) {
+                    hli = li; hfa = na[n].z; hfb = na[n].w;
+                }
+            } else {
+                const v3 p = xyz(na[n]), c = xyz(nb[n]);
+                cmb.take(target_pdf(s, f, cur, p, c, tb), na[n].w, __float_as_uint(nb[n].w), p, c);
+            }
         }
     }
-    cmb.take(pd_cur, ca.w, __float_as_uint(cb.w), xyz(ca), xyz(cb));
+    if (cmb.take(pd_cur, ca.w, __float_as_uint(cb.w), xyz(ca), xyz(cb))) { hli = cli; hfa = ch.z; hfb = ch.w; }
     float p = cmb.pd;
     if (!cmb.has_pd) p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z)) ? 0.0f : target_pdf(s, f, cur, cmb.pos, cmb.col, tb);
     const float W = contribution_weight(p, cmb.macc, cmb.wsum);
-    st_at(oa, pofs, make_float4(cmb.pos.x, cmb.pos.y, cmb.pos.z, W));
-    st_at(ob, pofs, make_float4(cmb.col.x, cmb.col.y, cmb.col.z, __uint_as_float(cmb.macc)));
+    if (!odead) {
+        st_at(oa, pofs, make_float4(cmb.pos.x, cmb.pos.y, cmb.pos.z, W));
+        st_at(ob, pofs, make_float4(cmb.col.x, cmb.col.y, cmb.col.z, __uint_as_float(cmb.macc)));
+    }
     if (DBG) st_at(odbg, pofs >> 1, make_float2(cmb.wsum, cmb.chosen));
     if (rp_out) st_at(rp_out, pofs >> 2, p);
+    put_handle(pofs, W, cmb.macc, hli, hfa, hfb);
 }
 
 #ifndef ROMIS_SPATIAL1_NTL_WPE
@@ -1027,6 +1106,17 @@ ROMIS_SPATIAL1_NTL_KERNEL(true, k_spatial1_ntl_dbg)
     }
 ROMIS_SPATIAL1_T2_KERNEL(false, k_spatial1_ntl_t2)
 ROMIS_SPATIAL1_T2_KERNEL(true, k_spatial1_ntl_t2_dbg)
+// k_spatial1g_t2: k_spatial1_ntl_t2 over light-grid handles (GH)
+#define ROMIS_SPATIAL1G_T2_KERNEL(DBG, NAME)                                                                          \
+    extern "C" __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL1_T2_WPE))) void     \
+    NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
+         const float4* p_mat, float4* oa, float4* ob, float2* odbg, const float* rp_in, float* rp_out, MissTiles mt,  \
+         const float4* hg_in, float4* hg_out, uint32_t odead) {                                                       \
+        spatial1_ntl_body<DBG, 2, true>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, nullptr, nullptr, oa, ob, odbg, rp_in, \
+                                        rp_out, mt, hg_in, hg_out, odead);                                             \
+    }
+ROMIS_SPATIAL1G_T2_KERNEL(false, k_spatial1g_t2)
+ROMIS_SPATIAL1G_T2_KERNEL(true, k_spatial1g_t2_dbg)
 
 // ---------------------------------------------------------------------------------------------------------
 // k_spatial1h[_t2]: the N = 1 biased pass over sample handles (round 5).  In a point-light scene
@@ -2074,21 +2164,33 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
                         : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
     ROMIS_LAUNCH(k, dim3(items_of(rg)), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
                  cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr, tu.ris_late, tmiss,
-                 tmiss ? skip_res : 0u, lt == kLtPoint && f.N == 1 ? h.w : nullptr, lt == kLtPoint && f.N == 1 ? h.m : nullptr,
-                 h.res_dead);
+                 tmiss ? skip_res : 0u, (lt == kLtPoint || lt == kLtRegular) && f.N == 1 ? h.w : nullptr,
+                 lt == kLtPoint && f.N == 1 ? h.m : nullptr, h.w && (lt == kLtPoint || lt == kLtRegular) ? h.res_dead : 0u);
     return hipGetLastError();
 }
 
 bool primary_ris_fits(const SceneDev& s) { return bvh_lds_bytes(s) <= kLdsBudget; }
 
-bool spatial_handles_ok(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes) {
-    if (!tu.spatial_handles || passes == 0 || f.N != 1 || f.unbiased || f.K > kLeanK || f.R > kLdsSpatialR) return false;
-    if (!tu.spatial_lean || !tu.ris_compact) return false;
-    if (s.light_types != 1u || s.num_lights == 0 || s.num_lights > 254u) return false;   // point lights; index L = zero
+int spatial_handle_kind(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes) {
+    if (!tu.spatial_handles || passes == 0 || f.N != 1 || f.unbiased || f.K > kLeanK || f.R > kLdsSpatialR) return -1;
+    if (!tu.spatial_lean || !tu.ris_compact || s.num_lights == 0) return -1;
+    int hk;
+    uint32_t mmax;
+    if (s.light_types == 1u && s.num_lights <= 254u) {   // point lights (k_spatial1h); index L = the zero sample
+        hk = 0; mmax = kHandleM;
+    } else if (ris_light_form(s, f, tu) == kLtRegular && tu.spatial_th != 1u && s.num_lights <= 1024u) {
+        // a regular light grid (RIS's kLtRegular form; k_spatial1g_t2, 32 x 16 tiles, <= 16 KB of colours in LDS)
+        hk = 1; mmax = kHandleMG;
+    } else {
+        return -1;
+    }
     // every M: RIS M, then each biased pass sums at most K + 1 inputs
     uint64_t m = f.M;
-    for (uint32_t p = 0; p < passes && m <= kHandleM; p++) m *= (uint64_t)(f.K + 1u);
-    return m <= kHandleM;
+    for (uint32_t p = 0; p < passes && m <= mmax; p++) m *= (uint64_t)(f.K + 1u);
+    return m <= mmax ? hk : -1;
+}
+bool spatial_handles_ok(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes) {
+    return spatial_handle_kind(s, f, tu, passes) >= 0;
 }
 
 // launch_spatial's N = 1 pass reads background tiles through MissTiles (k_spatial1_ntl / _t2 biased, k_spatial1u[_vis]
@@ -2176,7 +2278,21 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         // 32x16 tiles (k_spatial1_ntl_t2) where the auto XCD chunk is at most 2 tile rows (wide images): C4 222 ->
         // 203 us, C2 76.8 -> 79.0 (cfg_kbench, profiles/r3/r3k); spatial.th = 1 / 2 forces either
         const uint32_t th = tu.spatial_th ? tu.spatial_th : (8192u / std::max(rg.rw, 1u) <= 2u ? 2u : 1u);
-        if (hin.w) {
+        if (hin.w && s.light_types != 1u) {
+            // light-grid handles (spatial_handle_kind 1): k_spatial1_ntl_t2's grid, the colours behind the window
+            if (tu.spatial_th == 1u) return hipErrorInvalidValue;
+            const uint32_t nty2 = (rg.rh + 2u * kTileH - 1) / (2u * kTileH);
+            if (rg.xcd_rows) {
+                if (tu.spatial_xcd_rows == kXcdRowsAuto) rg.xcd_rows = std::max(1u, rg.xcd_rows / 2u);
+                grid = xcd_grid(rg, ntx, nty2);
+            } else {
+                grid = ntx * nty2;
+            }
+            ROMIS_LAUNCH(odbg ? k_spatial1g_t2_dbg : k_spatial1g_t2, dim3(grid), dim3(2u * kBlock),
+                         apron_max(2) * 16u + s.num_lights * 16u, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, oa,
+                         ob, odbg, rp_in, rp_out, mt, reinterpret_cast<const float4*>(hin.w),
+                         reinterpret_cast<float4*>(hout.w), hout.res_dead);
+        } else if (hin.w) {
             // sample handles (k_spatial1h[_t2]): 32 x 8 TH tiles, TH = spatial.th (auto: 2 -- C2 66.9 us against 76.2 for
             // 32 x 8, 70.6 / 68.4 for 32 x 24 / 32 x 32, kbench, profiles/r5); the XCD chunks hold xcd_rows tile rows
             // (the automatic count divided by TH)

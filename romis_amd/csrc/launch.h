@@ -24,6 +24,8 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg, const CameraD
 // restir_render's N = 1 biased passes over sample handles (k_spatial1h): the scene, features and knobs allow them and
 // every M `passes` passes can produce fits the handle's 24 bits
 bool spatial_handles_ok(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes);
+// which: 0 point-light handles (8 B per pixel), 1 light-grid handles (16 B), -1 none
+int spatial_handle_kind(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes);
 bool primary_ris_fits(const SceneDev& s);
 // the N = 1 spatial pass reads background tiles through MissTiles for this scene / features / knobs (SoA planes)
 bool spatial_reads_flags(const SceneDev& s, const FeaturesDev& f, const Tuning& tu);

@@ -1306,11 +1306,15 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     uint32_t skip_mode = skip_res ? (1u | (gbuf_ok ? 2u : 0u)) : 0u;
     // sample handles (k_spatial1h): N = 1 biased passes over a point-light scene, written by the fused RIS kernel and by
     // every pass but the last; 4 + 4 B per pixel and 16 B of slack (the planes are read a word at a time)
-    const bool handles = fused && !temporal && !fb.records && spatial_handles_ok(s, f, c->tuning, passes) &&
+    // (point lights: two 4-byte planes; a regular light grid: one float4 plane, k_spatial1g)
+    const int hkind = spatial_handle_kind(s, f, c->tuning, passes);
+    const bool handles = fused && !temporal && !fb.records && hkind >= 0 &&
                          (size_t)t.gwidth * t.gheight * 16u <= 0xFFFFFFFFull;
     if (handles)
-        for (int i = 0; i < 2; i++) ST_TRY(fb.hnd_()[i].ensure((size_t)t.gwidth * t.gheight * 8u + 16u));
-    // the handle passes read RIS's samples through the handles alone (the last pass writes the returned grid)
+        for (int i = 0; i < 2; i++) ST_TRY(fb.hnd_()[i].ensure((size_t)t.gwidth * t.gheight * (hkind ? 16u : 8u) + 16u));
+    // the handle passes read RIS's samples through the handles alone, and a pass's output is read by the next pass's
+    // handles alone: their reservoir planes are dead (the last pass writes the returned grid's owned rect; a tile's
+    // ghost ring holds intermediate values, include/restir_c.h)
     Handles ris_handles = fb.h(cur);
     ris_handles.res_dead = 1u;
     if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)

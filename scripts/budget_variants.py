@@ -44,6 +44,9 @@ VARIANTS = {
     # no neighbour reservoir loads at all (the pixel's own records stand in): gather latency and traffic removed
     "no_gather": [(r"na\[(n \+ 1|0)\] = ld_at\(ia, qo\[(n \+ 1|0)\]\);", r"na[\1] = ca;"),
                   (r"nb\[(n \+ 1|0)\] = ld_at\(ib, qo\[(n \+ 1|0)\]\);", r"nb[\1] = cb;")],
+    # round 5 (C4f): only the position / W half of each accepted neighbour's reservoir gathered (colour / M from the
+    # pixel's own): the upper bound of a 16-byte sample record for the light-grid scenes
+    "half_gather": [(r"nb\[(n \+ 1|0)\] = ld_at\(ib, qo\[(n \+ 1|0)\]\);", r"nb[\1] = cb;")],
     # everything after the window barrier replaced by a copy of the pixel's own records (the skeleton: own loads,
     # window DMA, barrier, stores), and the same without the window DMA
     "skeleton": [(r"    const float4 cn = l_nt\[\(uint32_t\)\(y - ay0\) \* AW \+ \(uint32_t\)\(x - ax0\)\];",

@@ -416,18 +416,20 @@ def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased, M, 
     assert_grid(grid, res, name)
 
 
+@pytest.mark.parametrize("name,framing", [("nightclub_128pt", None), ("cornell_1024", "framed")])
 @pytest.mark.parametrize("th", [1, 2])
 @pytest.mark.parametrize("w,h,passes,M", [(96, 64, 1, 32), (37, 23, 2, 32), (130, 70, 2, 1), (64, 1, 1, 16)])
-def test_spatial_handles_frames_match_oracle(gpu, oracle, th, w, h, passes, M):
+def test_spatial_handles_frames_match_oracle(gpu, oracle, name, framing, th, w, h, passes, M):
     """The biased passes over sample handles (k_spatial1h[_tN], round 5: W and M | light index planes staged in LDS
     beside the n_t window, point lights) at every tile height, ragged sizes, 1 and 2 passes: RGB and the returned grid
     bit-exact with the oracle (render_utils.cpp:87-140, reservoir.cpp:40-66); a pass before the last writes only its
-    handles.  The RGB without a returned grid (bench.py's render) too."""
-    name = "nightclub_128pt"
+    handles.  The RGB without a returned grid (bench.py's render) too.  cornell_1024 (C4's regular light grid, camera
+    into the box): the grid handles (W, M | i, a, b) of k_spatial1g_t2, whose samples are rebuilt from RIS's draws of
+    the light's fractions (32 x 16 tiles only: th = 1 runs the n_t-window pass instead)."""
     s = get_scene(name)
     gpu.set_scene(s)
     osc = oracle.OracleScene(s)
-    cam = scene.camera_for(name, w, h)
+    cam = scene.camera_for(name, w, h, framing)
     f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=passes, temporal_reuse=0,
                               initial_light_samples=M)
     gpu.set_tuning("spatial.th", th)
@@ -898,6 +900,8 @@ def test_full_size_c3_sequence_band_parity(gpu, oracle, N):
     ("cornell_1024", 1, 0, 0, 0, {}), ("cornell_1024", 2, 0, 0, 0, {}), ("cornell_4096", 1, 1, 1, 0, {}),
     ("cornell_4096", 2, 1, 1, 0, {}), ("cornell_4096", 1, 1, 0, 0, {}), ("nightclub_128pt", 1, 0, 0, 0, {}),
     ("cornell_1024", 2, 0, 0, 1, {}), ("cornell_4096", 2, 1, 1, 1, {}),
+    # sample-handle passes (point lights / the light grid) on a ghost-zoned tile: the returned ring keeps RIS's reservoirs
+    ("nightclub_128pt", 2, 0, 0, 1, {}), ("cornell_1024", 3, 0, 0, 1, {}),
     # biased passes with the G-buffer stores skipped too (miss.gbuf = 1; the default does so only from 2048 px wide):
     # the window fix-up, on 32 x 8 and on 32 x 16 tiles
     ("cornell_1024", 1, 0, 0, 0, {"miss.gbuf": 1}), ("cornell_1024", 2, 0, 0, 0, {"miss.gbuf": 1}),
@@ -942,5 +946,8 @@ def test_miss_tiles_match_full_reads(gpu, oracle, name, passes, unbiased, vis, t
         want, _, _ = oracle.render_frame(oracle.OracleScene(s), cam, f, w, h, SEED, 0, threads=16)
         assert_bits(on_rgb, want, f"{name} rgb against the oracle")
     assert_bits(on_rgb, off_rgb, f"{name} rgb")
+    # a tiled frame's grid is defined on the owned rect (the ghost ring holds intermediate values, include/restir_c.h)
+    own = (slice(None), slice(tile.y0 - tile.gy0, tile.y0 - tile.gy0 + tile.height),
+           slice(tile.x0 - tile.gx0, tile.x0 - tile.gx0 + tile.width)) if tile is not None else (slice(None),)
     for a, b in zip(off_grid, on_grid):
-        assert np.array_equal(np.asarray(a).view(np.uint32), np.asarray(b).view(np.uint32)), f"{name} grid"
+        assert np.array_equal(np.asarray(a)[own].view(np.uint32), np.asarray(b)[own].view(np.uint32)), f"{name} grid"

@@ -2,7 +2,7 @@
 # HBM traffic of the spatial pass (FETCH_SIZE / WRITE_SIZE, separate --pmc passes) and its kernel time, per config:
 # C2 (1080p headline: k_spatial1h_t2 over sample handles; "ntl": the n_t-window pass with reservoir gathers,
 # spatial.handles = 0), C4 (4K, TOML camera: 87 % background), C4f / C5f (4K / 8K looking into the box: the passes on
-# geometry, past the Infinity Cache).   scripts/traffic_study.sh <tag>
+# geometry, past the Infinity Cache; C4f's default k_spatial1g_t2 over light-grid handles, "ntl" its reservoir form).   scripts/traffic_study.sh <tag>
 set -o pipefail
 TAG=${1:-traffic}
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -12,7 +12,7 @@ cd "$REPO" || exit 1
 export TMPDIR=/tmp
 for CFG in c2 c4 c4f c5f; do
     VARS=("chunks:spatial.xcd_rows=255")
-    [ $CFG = c2 ] && VARS+=("ntl:spatial.xcd_rows=255,spatial.handles=0")
+    [ $CFG = c2 ] || [ $CFG = c4f ] && VARS+=("ntl:spatial.xcd_rows=255,spatial.handles=0")
     FR=3; [ $CFG = c5f ] && FR=1
     for V in "${VARS[@]}"; do
         NAME=${V%%:*}

@@ -118,6 +118,31 @@ __device__ __forceinline__ float rand01(uint32_t d) {
     return scaled + 0.0f;
 }
 __device__ __forceinline__ uint32_t uniform_index(uint32_t d, uint32_t n) { return __umulhi(d, n); }
+
+// Reservoir::update's acceptance `u < w / wSum` (reservoir.cpp:24-28) for a u of rand01 (a multiple of 2^-31 in [0, 1))
+// without the correctly rounded division where the answer is already known: the exact residual e = w - u wSum (one
+// fma, its sign exact) gives w / wSum <= u (e <= 0: RN(w / wSum) <= u, false) and w / wSum > u + ulp(u) / 2
+// (RN(e) > ulp(u) wSum: RN(w / wSum) >= the float after u, true).  Only the band in between (probability ~2^-24 per
+// draw), u = 0, wSum outside [2^-60, 2^60] (where ulp(u) wSum could leave the normal range) and NaN operands take the
+// division, under a wave-uniform branch.  tests/test_fast_accept.py checks the rule against the division on the CPU.
+#ifndef ROMIS_FAST_ACCEPT
+#define ROMIS_FAST_ACCEPT 1
+#endif
+__device__ __forceinline__ bool accept_u(float u, float w, float ws) {
+#if ROMIS_FAST_ACCEPT
+    const float e = __builtin_fmaf(-u, ws, w);
+    const float ulp = __uint_as_float(__float_as_uint(u) + 1u) - u;
+    const bool t = e > ulp * ws;
+    const bool known = (t || e <= 0.0f) && u != 0.0f && ws >= 0x1p-60f && ws <= 0x1p60f;
+    bool acc = t;
+    if (__builtin_expect(__any(!known), 0)) {
+        if (!known) acc = u < (w / ws);
+    }
+    return acc;
+#else
+    return u < (w / ws);
+#endif
+}
 __device__ __forceinline__ int uniform_offset(uint32_t d, uint32_t r) { return (int)__umulhi(d, 2u * r + 1u) - (int)r; }
 
 // ---- powf / expf: glibc 2.35's flt-32 algorithms, FMA objects (oracle/portable_math.h is the CPU side) -------

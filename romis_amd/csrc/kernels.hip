@@ -214,7 +214,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                     const float w = weight(pd);
                     r[0].M += 1u;
                     r[0].wsum += w;
-                    if (rand01(draw(ps, 4u * c + 3u)) < (w / r[0].wsum)) { best = c; r[0].chosen = w; r[0].pd = pd; }
+                    if (accept_u(rand01(draw(ps, 4u * c + 3u)), w, r[0].wsum)) { best = c; r[0].chosen = w; r[0].pd = pd; }
                 }
                 if (best != 0xFFFFFFFFu) {
                     sample(best, r[0].pos, r[0].col);
@@ -717,7 +717,7 @@ struct Comb1 {
         wsum += w;
         const float u = rand01(mix32(h));
         h += 0x9E3779B9u;
-        const bool acc = u < (w / wsum);
+        const bool acc = accept_u(u, w, wsum);
         if (acc) { pos = p; col = c; chosen = w; pd = pd_in; has_pd = true; }
         return acc;
     }
@@ -1143,7 +1143,7 @@ struct Comb1h {
         wsum += w;
         const float u = rand01(mix32(h));
         h += 0x9E3779B9u;
-        if (u < (w / wsum)) { li = l; chosen = w; pd = pd_in; has_pd = true; }
+        if (accept_u(u, w, wsum)) { li = l; chosen = w; pd = pd_in; has_pd = true; }
     }
 };
 
@@ -1392,7 +1392,7 @@ struct CombN {
             if ((uint32_t)j == k) {
                 macc[j] += M;
                 wsum[j] += w;
-                if (u < (w / wsum[j])) { pos[j] = p; col[j] = c; chosen[j] = w; pd[j] = pd_in; has_pd[j] = true; }
+                if (accept_u(u, w, wsum[j])) { pos[j] = p; col[j] = c; chosen[j] = w; pd[j] = pd_in; has_pd[j] = true; }
             }
         }
     }

@@ -449,7 +449,7 @@ __device__ __forceinline__ void sub_init(Sub& r) {
 __device__ __forceinline__ void sub_take(Sub& r, v3 pos, v3 col, float w, float u, float pd) {
     r.M += 1u;
     r.wsum += w;
-    if (u < (w / r.wsum)) { r.pos = pos; r.col = col; r.chosen = w; r.pd = pd; r.has_pd = true; }
+    if (accept_u(u, w, r.wsum)) { r.pos = pos; r.col = col; r.chosen = w; r.pd = pd; r.has_pd = true; }
 }
 
 template <int NT>
@@ -471,7 +471,7 @@ __device__ __forceinline__ uint32_t res_update(Sub* r, uint32_t N, v3 pos, v3 co
 #pragma unroll
         for (uint32_t j = 1; j < (uint32_t)(NT > 0 ? NT : 1); j++) ws = (j == k) ? r[j].wsum : ws;
         ws += w;                            // sub_take's wsum += w on the routed one
-        const bool acc = u < (w / ws);      // ... and its acceptance test
+        const bool acc = accept_u(u, w, ws);      // ... and its acceptance test
 #pragma unroll
         for (uint32_t j = 0; j < (uint32_t)(NT > 0 ? NT : 1); j++) {
             const bool sel = j == k, take = sel && acc;

@@ -2294,13 +2294,14 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
                          reinterpret_cast<float4*>(hout.w), hout.res_dead);
         } else if (hin.w) {
             // sample handles (k_spatial1h[_t2]): 32 x 8 TH tiles, TH = spatial.th (auto: 2 -- C2 66.9 us against 76.2 for
-            // 32 x 8, 70.6 / 68.4 for 32 x 24 / 32 x 32, kbench, profiles/r5); the XCD chunks hold xcd_rows tile rows
-            // (the automatic count divided by TH)
+            // 32 x 8, 70.6 / 68.4 for 32 x 24 / 32 x 32, kbench, profiles/r5); the XCD chunks hold xcd_rows tile rows,
+            // automatically one 32 x 16 row (C2: 66.1 / 65.7 us against 66.7 / 66.3 with two, 72.9 / 72.5 with four;
+            // profiles/r5/probes/r5p23)
             const uint32_t hth = tu.spatial_th ? tu.spatial_th : 2u;
             if (hth > 1u) {
                 const uint32_t ntyh = (rg.rh + hth * kTileH - 1) / (hth * kTileH);
                 if (rg.xcd_rows) {
-                    if (tu.spatial_xcd_rows == kXcdRowsAuto) rg.xcd_rows = std::max(1u, rg.xcd_rows / hth);
+                    if (tu.spatial_xcd_rows == kXcdRowsAuto) rg.xcd_rows = 1u;
                     grid = xcd_grid(rg, ntx, ntyh);
                 } else {
                     grid = ntx * ntyh;

@@ -34,7 +34,7 @@ def main():
     dst = os.path.join(ROOT, args.profile)
     os.makedirs(dst, exist_ok=True)
     entries = []
-    orders_of = {"c2": [("chunks", 255), ("ntl", 255)], "c4": [("chunks", 255)], "c4f": [("chunks", 255)],
+    orders_of = {"c2": [("chunks", 255), ("ntl", 255)], "c4": [("chunks", 255)], "c4f": [("chunks", 255), ("ntl", 255)],
                  "c5f": [("chunks", 255)]}
     for cfgname, orders in orders_of.items():
         cf = bench.CONFIGS[cfgname]

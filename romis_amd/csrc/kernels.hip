@@ -222,6 +222,35 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                     if (LT == kLtPoint || LT == kLtRegular) hidx = uniform_index(draw(ps, 4u * best), L);
                     if (LT == kLtRegular) { ha = rand01(draw(ps, 4u * best + 1u)); hb = rand01(draw(ps, 4u * best + 2u)); }
                 }
+            } else if (NT == 2) {
+                // res_update<2> (Reservoir::update routed to the smaller wSum -- argmin from FLT_MAX, strict <, first
+                // index) keeping each sub-reservoir's accepted candidate index, as the N = 1 loop does: the samples
+                // are drawn again after the loop
+                uint32_t best[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+                for (uint32_t c = 0; c < c_end; c++) {
+                    v3 pos, col;
+                    sample(c, pos, col);
+                    const float pd = target_pdf(s, f, px, pos, col, tb);
+                    const float w = weight(pd);
+                    const float b0 = r[0].wsum < ROMIS_FLT_MAX ? r[0].wsum : ROMIS_FLT_MAX;
+                    const bool k1 = r[1].wsum < b0;
+                    const float ws = (k1 ? r[1].wsum : r[0].wsum) + w;
+                    const bool acc = accept_u(rand01(draw(ps, 4u * c + 3u)), w, ws);
+                    r[0].M += k1 ? 0u : 1u;
+                    r[1].M += k1 ? 1u : 0u;
+                    r[0].wsum = k1 ? r[0].wsum : ws;
+                    r[1].wsum = k1 ? ws : r[1].wsum;
+                    if (acc) {
+                        if (k1) { best[1] = c; r[1].chosen = w; r[1].pd = pd; }
+                        else { best[0] = c; r[0].chosen = w; r[0].pd = pd; }
+                    }
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < 2u; j++)
+                    if (best[j] != 0xFFFFFFFFu) {
+                        sample(best[j], r[j].pos, r[j].col);
+                        r[j].has_pd = true;
+                    }
             } else {
                 for (uint32_t c = 0; c < c_end; c++) {
                     v3 pos, col;
@@ -2345,6 +2374,7 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         if (rp_written) *rp_written = rp_out != nullptr;
         return hipGetLastError();
     }
+    if (hin.w) return hipErrorInvalidValue;   // handles without a handle pass: the producer skipped the reservoirs
     auto k = f.unbiased ? (f.N == 1 ? k_spatial_n1_unbiased : (f.N == 2 ? k_spatial_n2_unbiased : k_spatial_n0_unbiased))
                         : (f.N == 1 ? k_spatial_n1_biased : (f.N == 2 ? k_spatial_n2_biased : k_spatial_n0_biased));
     const uint32_t bvh_lds = (f.unbiased && f.spatial_vis && bvh_bytes <= kLdsBudget) ? 1u : 0u;

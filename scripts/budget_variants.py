@@ -22,6 +22,7 @@ SPANS = {   # the function each variant patches: (first line, the text that foll
     "spatial": ("__device__ __forceinline__ void spatial1_ntl_body(", "#ifndef ROMIS_SPATIAL1_NTL_WPE"),
     "ris": ("__device__ __forceinline__ void ris_pixel(", "// k_ris: genCanonicalSamples per pixel."),
     "spatialu": ("__device__ __forceinline__ void spatial1u_body(", "#define ROMIS_SPATIAL1U_KERNEL"),
+    "spatialn": ("__device__ __forceinline__ void spatialn_ntl_body(", "#ifndef ROMIS_SPATIAL2_NTL_WPE"),
 }
 
 
@@ -47,6 +48,9 @@ VARIANTS = {
     # round 5 (C4f): only the position / W half of each accepted neighbour's reservoir gathered (colour / M from the
     # pixel's own): the upper bound of a 16-byte sample record for the light-grid scenes
     "half_gather": [(r"nb\[(n \+ 1|0)\] = ld_at\(ib, qo\[(n \+ 1|0)\]\);", r"nb[\1] = cb;")],
+    # round 5 (C2 at N = 2, k_spatial2_ntl): no neighbour reservoir gathers (the pixel's own sub-reservoirs stand in)
+    "n2_no_gather": [(r"na\[j\] = ld_at\(ia, qo\[n\] \+ \(uint32_t\)j \* jofs\); nb\[j\] = ld_at\(ib, qo\[n\] \+ \(uint32_t\)j \* jofs\);",
+                      "na[j] = ca[j]; nb[j] = cb[j];")],
     # everything after the window barrier replaced by a copy of the pixel's own records (the skeleton: own loads,
     # window DMA, barrier, stores), and the same without the window DMA
     "skeleton": [(r"    const float4 cn = l_nt\[\(uint32_t\)\(y - ay0\) \* AW \+ \(uint32_t\)\(x - ax0\)\];",
@@ -132,7 +136,8 @@ def main():
         if name.startswith("risg_"):
             a, b = 0, len(src)
         else:
-            a, b = body_span(src, "ris" if name.startswith("ris_") else "spatialu" if name.startswith("u_") else "spatial")
+            a, b = body_span(src, "ris" if name.startswith("ris_") else "spatialu" if name.startswith("u_")
+                             else "spatialn" if name.startswith("n2_") else "spatial")
         body = src[a:b]
         for pat, rep in subs:
             body, n = re.subn(pat, rep, body)

@@ -23,6 +23,7 @@ SPANS = {   # the function each variant patches: (first line, the text that foll
     "ris": ("__device__ __forceinline__ void ris_pixel(", "// k_ris: genCanonicalSamples per pixel."),
     "spatialu": ("__device__ __forceinline__ void spatial1u_body(", "#define ROMIS_SPATIAL1U_KERNEL"),
     "spatialn": ("__device__ __forceinline__ void spatialn_ntl_body(", "#ifndef ROMIS_SPATIAL2_NTL_WPE"),
+    "final": ("__device__ __forceinline__ void final_sorted_body(", "extern \"C\" __global__ __launch_bounds__(256) void k_final_n1_sorted("),
 }
 
 
@@ -51,6 +52,13 @@ VARIANTS = {
     # round 5 (C2 at N = 2, k_spatial2_ntl): no neighbour reservoir gathers (the pixel's own sub-reservoirs stand in)
     "n2_no_gather": [(r"na\[j\] = ld_at\(ia, qo\[n\] \+ \(uint32_t\)j \* jofs\); nb\[j\] = ld_at\(ib, qo\[n\] \+ \(uint32_t\)j \* jofs\);",
                       "na[j] = ca[j]; nb[j] = cb[j];")],
+    # round 5: final shading (k_final_n1_sorted at C2) -- the shadow rays, the shading, the tone map, the binning
+    "fin_no_trace": [(r"s_vis\[__float_as_uint\(a\.w\)\] = visible\(bvh, xyz\(a\), xyz\(b\)\) \? 1u : 0u;",
+                      "s_vis[__float_as_uint(a.w)] = (a.x < b.x) ? 1u : 0u;")],
+    "fin_no_shade": [(r"sc\[j\] = shade\(s, f, px, r\[j\]\.pos, r\[j\]\.col, tb\);",
+                      "sc[j] = vadd(vscale(r[j].col, px.N.x), vscale(r[j].pos, px.P.y));")],
+    "fin_no_tonemap": [(r"color = tone_map_rgb\(f, vdivs\(color, \(float\)NT\), tb\);", "color = vscale(color, 0.5f);")],
+    "fin_no_sort": [(r"bin\[j\] = need\[j\] \? target_bin\(bvh, r\[j\]\.pos\) : 0u;", "bin[j] = 0u;")],
     # everything after the window barrier replaced by a copy of the pixel's own records (the skeleton: own loads,
     # window DMA, barrier, stores), and the same without the window DMA
     "skeleton": [(r"    const float4 cn = l_nt\[\(uint32_t\)\(y - ay0\) \* AW \+ \(uint32_t\)\(x - ax0\)\];",
@@ -137,7 +145,7 @@ def main():
             a, b = 0, len(src)
         else:
             a, b = body_span(src, "ris" if name.startswith("ris_") else "spatialu" if name.startswith("u_")
-                             else "spatialn" if name.startswith("n2_") else "spatial")
+                             else "spatialn" if name.startswith("n2_") else "final" if name.startswith("fin_") else "spatial")
         body = src[a:b]
         for pat, rep in subs:
             body, n = re.subn(pat, rep, body)

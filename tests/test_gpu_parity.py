@@ -416,7 +416,7 @@ def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased, M, 
     assert_grid(grid, res, name)
 
 
-@pytest.mark.parametrize("name,framing", [("nightclub_128pt", None), ("cornell_1024", "framed")])
+@pytest.mark.parametrize("name,framing", [("nightclub_128pt", None), ("cornell_1024", "framed"), ("cornell_4096", "framed")])
 @pytest.mark.parametrize("th", [1, 2])
 @pytest.mark.parametrize("w,h,passes,M", [(96, 64, 1, 32), (37, 23, 2, 32), (130, 70, 2, 1), (64, 1, 1, 16)])
 def test_spatial_handles_frames_match_oracle(gpu, oracle, name, framing, th, w, h, passes, M):
@@ -425,7 +425,8 @@ def test_spatial_handles_frames_match_oracle(gpu, oracle, name, framing, th, w, 
     bit-exact with the oracle (render_utils.cpp:87-140, reservoir.cpp:40-66); a pass before the last writes only its
     handles.  The RGB without a returned grid (bench.py's render) too.  cornell_1024 (C4's regular light grid, camera
     into the box): the grid handles (W, M | i, a, b) of k_spatial1g_t2, whose samples are rebuilt from RIS's draws of
-    the light's fractions (32 x 16 tiles only: th = 1 runs the n_t-window pass instead)."""
+    the light's fractions (32 x 16 tiles only: th = 1 runs the n_t-window pass instead); cornell_4096 (4,096 lights, past
+    the handle pass's 1,024-colour table): the reservoir form, as the host falls back."""
     s = get_scene(name)
     gpu.set_scene(s)
     osc = oracle.OracleScene(s)

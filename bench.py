@@ -443,13 +443,15 @@ def select_halo(torch, world, local, backend, transport, make, check):
     return hf, rec, bad
 
 
-def halo_frames(torch, r, rank, world, local, f, cam, GW, GH, tx, ty, passes, args, transport, check_on):
+def halo_frames(torch, r, rank, world, local, f, cam, GW, GH, tx, ty, passes, args, transport, check_on, fatal=True):
     """N > 1 with spatial passes: this rank's tile rendered through the reservoir halo exchange (HaloFrames: interior
     launched while the border reservoirs move, border strips after) must equal, bit for bit, the same tile rendered
     with a ghost zone (restir_render on tile + passes * r) -- exits 3 on any mismatch (check_on).  Then the halo-mode
     frame and the exchange alone are timed.  Temporal reuse is off in the check (one frame from no predecessor).
     Returns (hf, rec): the verified HaloFrames -- the halo-mode main loop (c4 / c5, --mode halo) times this instance,
-    so the run never times a transport other than the one it checked -- and the JSON record."""
+    so the run never times a transport other than the one it checked -- and the JSON record.  fatal = False (the halo
+    is only checked, as with c2's ghost-zone frames at N > 1): a mismatch, or a render error that every rank sees as one,
+    is recorded and the run goes on (returns hf None) -- the timed frames do not use the halo."""
     from romis_amd import _abi, distributed, restir
     fc = _abi.Features.from_buffer_copy(f)
     fc.temporal_reuse = 0
@@ -470,13 +472,24 @@ def halo_frames(torch, r, rank, world, local, f, cam, GW, GH, tx, ty, passes, ar
         hf.f = fc
         try:
             rgb, _ = hf.render(None, cam, want_rgb=True, want_grid=False)
+        except _abi.RestirError as e:   # this rank's frame failed: counted as mismatching, so every rank sees it
+            rec_err["render_error"] = str(e)[:200]
+            rgb = None
         finally:
             hf.f = f0
+        if rgb is None:
+            import numpy as np
+            rgb = np.full_like(ghost["rgb"], np.nan)
         return distributed.tile_mismatches(rgb, ghost["rgb"])   # summed over ranks: every rank decides alike
 
+    rec_err = {}
     hf, rec, bad = select_halo(torch, world, local, args.dist_backend, transport, make, check)
+    rec.update(rec_err)
     rec["check"] = ("bit-exact" if bad == 0 else f"{bad} mismatching values") if check_on else "off"
     if bad:
+        if not fatal:   # the run's timed frames are the ghost-zone ones: record the failed check and go on
+            rec["timed"] = False
+            return None, rec
         if rank == 0:
             print(json.dumps({"error": "halo tile differs from the ghost-zone tile", "halo": rec}), flush=True)
         torch.distributed.barrier()
@@ -548,7 +561,7 @@ def main():
     if halo or check_on:
         # one HaloFrames per run, chosen and verified by halo_frames (select_halo); the halo-mode loop times it
         hf_checked, halo_rec = halo_frames(torch, r, rank, world, local, f, cam, GW, GH, tx, ty, passes, args, transport,
-                                           check_on)
+                                           check_on, fatal=halo)
         r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
         if halo:
             hf = hf_checked

@@ -488,7 +488,8 @@ typedef enum restir_kernel {
 } restir_kernel;
 restir_status restir_enable_timing(restir_ctx* ctx, int enable);
 /* Launch-shape knobs (never change results): "primary.lds", "ris.lds", "final.lds" (stage the BVH / light table in
- * LDS when it fits), "fuse.primary_ris" (restir_render runs primary rays + RIS as one kernel), "spatial.lean" (the
+ * LDS when it fits), "fuse.primary_ris" (restir_render runs primary rays + RIS as one kernel), "fuse.temporal" (with a predecessor
+ * grid, temporal reuse runs inside that kernel: N = 1 / 2, point lights, the light table in LDS; default 1), "spatial.lean" (the
  * lean N = 1 / 2 passes; 0: the general kernels), "timing.mask": the kernels (bit 1 << RESTIR_K_*) restir_enable_timing
  * brackets with HIP events (default all).  "bvh.max_leaf": triangles per BVH leaf for the next restir_set_scene
  * (default 2).  "layout.records": restir_render's buffers as per-pixel records [n_t, res_a, res_b] (1) or SoA planes

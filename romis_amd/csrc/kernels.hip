@@ -83,6 +83,42 @@ extern "C" __global__ __launch_bounds__(256) void k_primary_lds(SceneDev s, Regi
 }
 
 // ---------------------------------------------------------------------------------------------------------
+// Combine state shared by temporal and spatial: out[] (Reservoir(N) of the current pixel) + routed M sums.
+template <int NT>
+struct Combiner {
+    Sub out[NT > 0 ? NT : RESTIR_MAX_N_DEV];
+    uint32_t macc[NT > 0 ? NT : RESTIR_MAX_N_DEV];
+    uint32_t N_;
+    uint32_t t;      // update counter (RNG slot offset)
+    // compile-time trip count when N is a template constant (keeps out[] / macc[] in registers)
+    __device__ __forceinline__ uint32_t n() const { return NT > 0 ? (uint32_t)NT : N_; }
+    __device__ __forceinline__ void init(uint32_t nn) {
+        N_ = nn;
+        for (uint32_t j = 0; j < n(); j++) { sub_init(out[j]); macc[j] = 0u; }
+        t = 0;
+    }
+    // combine one input sub-reservoir (reservoir.cpp:47-54 / :75-82)
+    __device__ __forceinline__ void consume(const SceneDev& s, const FeaturesDev& f, const Px& cur, const Sub& in, uint32_t ps, uint32_t slot0) {
+        consume_pd(target_pdf(s, f, cur, in.pos, in.col), in, ps, slot0);
+    }
+    // the same with the input's target pdf at the combining pixel already known (the rp cache)
+    __device__ __forceinline__ void consume_pd(float pd, const Sub& in, uint32_t ps, uint32_t slot0) {
+        float w = (pd * in.W) * (float)in.M;
+        uint32_t k = res_update<NT>(out, n(), in.pos, in.col, w, rand01(draw(ps, slot0 + t)), pd);
+        t++;
+        macc_add<NT>(macc, k, in.M);
+    }
+    __device__ __forceinline__ void finish_biased(const SceneDev& s, const FeaturesDev& f, const Px& cur, float* pd_out = nullptr) {
+        for (uint32_t j = 0; j < n(); j++) out[j].M = macc[j];
+        for (uint32_t j = 0; j < n(); j++) {
+            const float pj = out[j].has_pd ? out[j].pd : target_pdf(s, f, cur, out[j].pos, out[j].col);
+            out[j].W = contribution_weight(pj, out[j].M, out[j].wsum);
+            if (pd_out) pd_out[j] = pj;
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------------------------------------
 // genCanonicalSamples for one pixel whose G-buffer records are (nt, pm); lights = the light table (global or
 // the block's LDS copy), bvh = the traversal arrays for the initial visibility rays.
 // LT: the light table's form (host-detected scene properties; genCanonicalSamples' switch, light.cpp:55-78, reduces
@@ -108,13 +144,13 @@ constexpr int kLtGeneral = 0, kLtPoint = 1, kLtGrid = 2, kLtPgram = 3, kLtRegula
 __host__ __device__ constexpr uint32_t lt_stride(int lt) {
     return lt == kLtGeneral ? 7u : lt == kLtPgram ? 4u : lt == kLtRegular ? 1u : 2u;
 }
-template <int NT, int LT = kLtGeneral>
+template <int NT, int LT = kLtGeneral, bool TEMP = false>
 __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key, v3 origin,
                                           const float4* lights, const Bvh& bvh, float4 nt, float4 pm, uint32_t x,
                                           uint32_t y, size_t p, float4* __restrict__ ra, float4* __restrict__ rb,
                                           float2* __restrict__ rdbg, float* __restrict__ rp, const GlTabs& tb,
                                           float* __restrict__ hw = nullptr, uint32_t* __restrict__ hm = nullptr,
-                                          bool store_res = true) {
+                                          bool store_res = true, TemporalIn tin = TemporalIn{nullptr, nullptr, 0u}) {
     const uint32_t L = s.num_lights;
     uint32_t hidx = L;   // the held sample's light index for the handle planes (k_spatial1h; L = the zero sample)
     float ha = 0.0f, hb = 0.0f;   // kLtRegular: its fractions (grid handles, k_spatial1g_t2)
@@ -222,7 +258,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                     if (LT == kLtPoint || LT == kLtRegular) hidx = uniform_index(draw(ps, 4u * best), L);
                     if (LT == kLtRegular) { ha = rand01(draw(ps, 4u * best + 1u)); hb = rand01(draw(ps, 4u * best + 2u)); }
                 }
-            } else if (NT == 2) {
+            } else if constexpr (NT == 2) {
                 // res_update<2> (Reservoir::update routed to the smaller wSum -- argmin from FLT_MAX, strict <, first
                 // index) keeping each sub-reservoir's accepted candidate index, as the N = 1 loop does: the samples
                 // are drawn again after the loop
@@ -259,12 +295,44 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                     res_update<NT>(r, N, pos, col, weight(pd), rand01(draw(ps, 4u * c + 3u)), pd);
                 }
             }
+            float pj0 = 0.0f;
             for (uint32_t j = 0; j < N; j++) {
                 // the held sample's target pdf: W's p-hat (light.cpp:90-93) and, N = 1, the pdf cache rp
                 const float pj = r[j].has_pd ? r[j].pd : target_pdf(s, f, px, r[j].pos, r[j].col, tb);
                 if (f.initial_vis && !visible(bvh, px.P, r[j].pos)) r[j].W = 0.0f;
                 else r[j].W = contribution_weight(pj, r[j].M, r[j].wsum);
-                if (NT == 1 && rp) rp[p] = pj;
+                if (j == 0) pj0 = pj;
+                if (NT == 1 && rp && !TEMP) rp[p] = pj;
+            }
+            if (TEMP) {
+                // temporalReuse (render_utils.cpp:142-177) fused: temporal_body's steps on the RIS reservoirs still in
+                // registers -- the predecessor's M clamped to clampM * M_current + 1, the current reservoir (its
+                // target pdf here: pj0 for N = 1, the pdf cache's value) then the predecessor's combined biased
+                Sub prev[NT > 0 ? NT : 1];
+                unsigned long long mcur = 0, mprev = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < (uint32_t)NT; j++) {
+                    sub_load(prev[j], tin.pa, tin.pb, ridx(rg, j, p));
+                    mcur += r[j].M;
+                    mprev += prev[j].M;
+                }
+                const unsigned long long C = (unsigned long long)f.clamp_m * mcur + 1ull;
+                if (mprev > C) {
+#pragma unroll
+                    for (uint32_t j = 0; j < (uint32_t)NT; j++)
+                        if (prev[j].M != 0u) prev[j].M = (uint32_t)C;
+                }
+                const uint32_t pst = pix_state(tin.key, y * rg.W + x);
+                Combiner<NT> cmb;
+                cmb.init(N);
+                if (NT == 1) cmb.consume_pd(pj0, r[0], pst, 0u);
+                else for (uint32_t j = 0; j < N; j++) cmb.consume(s, f, px, r[j], pst, 0u);
+                for (uint32_t j = 0; j < N; j++) cmb.consume(s, f, px, prev[j], pst, 0u);
+                float pd_out[NT > 0 ? NT : 1];
+                cmb.finish_biased(s, f, px, NT == 1 ? pd_out : nullptr);
+#pragma unroll
+                for (uint32_t j = 0; j < (uint32_t)NT; j++) r[j] = cmb.out[j];
+                if (NT == 1 && rp) rp[p] = pd_out[0];
             }
         } else if (NT == 1 && rp) {
             rp[p] = target_pdf(s, f, make_px(s, nt, pm, origin, p), r[0].pos, r[0].col, tb);   // no lights: the initial sample
@@ -320,14 +388,14 @@ __device__ __forceinline__ void ris_body(const SceneDev& s, const Region& rg, co
 // the G-buffer records go to memory for the later passes and straight into the pixel's RIS, and the primary
 // ray's latency-bound BVH traversal runs beside other waves' VALU-bound candidate loops.  The block stages the
 // BVH and, when it fits beside it, the light table in LDS.
-template <int NT, bool LDS_LIGHTS, int LT = kLtGeneral>
+template <int NT, bool LDS_LIGHTS, int LT = kLtGeneral, bool TEMP = false>
 __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region& rg, const CameraDev& cam,
                                                  const FeaturesDev& f, uint32_t key, float4* __restrict__ n_t,
                                                  float4* __restrict__ p_mat, float4* __restrict__ n_t2,
                                                  float4* __restrict__ ra, float4* __restrict__ rb, float2* __restrict__ rdbg,
                                                  float* __restrict__ rp, uint32_t late_ok, uint8_t* __restrict__ tmiss,
                                                  uint32_t skip_res, float* __restrict__ hw, uint32_t* __restrict__ hm,
-                                                 uint32_t res_dead) {
+                                                 uint32_t res_dead, TemporalIn tin = TemporalIn{nullptr, nullptr, 0u}) {
     const uint32_t bvh_f4 = 2u * s.num_nodes + 3u * s.num_tris;
     const float4* lights = global_lights<LT>(s);
     const uint32_t items = work_items(rg);
@@ -371,8 +439,8 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         // pdfs are not stored -- the first spatial pass substitutes them from the flag; bit 1 (above), nor its G-buffer
         // records (a single unbiased pass, which substitutes those too)
         if (live && (any || !tmiss || !(skip_res & 1u)))
-            ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb, hw, hm,
-                              !(hw && res_dead));
+            ris_pixel<NT, LT, TEMP>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb, hw, hm,
+                                    !(hw && res_dead), tin);
         return;
     }
     for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {
@@ -381,8 +449,8 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         if (!work_pixel(rg, item, x, y, p)) continue;
         float4 nt, pm;
         primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, nt, pm);
-        ris_pixel<NT, LT>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb, hw, hm,
-                          !(hw && res_dead));
+        ris_pixel<NT, LT, TEMP>(s, rg, f, key, origin, lights, bvh, nt, pm, x, y, p, ra, rb, rdbg, rp, tb, hw, hm,
+                                !(hw && res_dead), tin);
     }
 }
 
@@ -438,6 +506,15 @@ ROMIS_RIS_KERNEL_LT(2, false, kLtPgram, k_ris_n2_pg, ROMIS_RIS_ATTR)
                                       hw, hm, res_dead);                                                               \
     }
 #define ROMIS_PRIMARY_RIS_KERNEL(NT, LDS, NAME, ATTR) ROMIS_PRIMARY_RIS_KERNEL_LT(NT, LDS, kLtGeneral, NAME, ATTR)
+// primary rays + RIS + temporal reuse in one kernel (point lights, the table in LDS): restir_render with a predecessor
+#define ROMIS_PRIMARY_RIS_TEMPORAL_KERNEL(NT, NAME, ATTR)                                                              \
+    extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, CameraDev cam, FeaturesDev f,   \
+                                                          uint32_t key, float4* n_t, float4* p_mat, float4* n_t2,      \
+                                                          float4* ra, float4* rb, float2* rdbg, float* rp,             \
+                                                          uint32_t late_ok, TemporalIn tin) {                          \
+        primary_ris_body<NT, true, kLtPoint, true>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp, late_ok,    \
+                                                   nullptr, 0u, nullptr, nullptr, 0u, tin);                            \
+    }
 ROMIS_PRIMARY_RIS_KERNEL(1, true, k_primary_ris_n1_lds, ROMIS_RIS1_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(1, false, k_primary_ris_n1, ROMIS_RIS1_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(2, true, k_primary_ris_n2_lds, ROMIS_RIS_ATTR)
@@ -458,42 +535,8 @@ ROMIS_PRIMARY_RIS_KERNEL_LT(1, true, kLtPgram, k_primary_ris_n1_lds_pg, ROMIS_RI
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, true, kLtPgram, k_primary_ris_n2_lds_pg, ROMIS_RIS_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(1, false, kLtPgram, k_primary_ris_n1_pg, ROMIS_RIS1_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL_LT(2, false, kLtPgram, k_primary_ris_n2_pg, ROMIS_RIS_ATTR)
-
-// ---------------------------------------------------------------------------------------------------------
-// Combine state shared by temporal and spatial: out[] (Reservoir(N) of the current pixel) + routed M sums.
-template <int NT>
-struct Combiner {
-    Sub out[NT > 0 ? NT : RESTIR_MAX_N_DEV];
-    uint32_t macc[NT > 0 ? NT : RESTIR_MAX_N_DEV];
-    uint32_t N_;
-    uint32_t t;      // update counter (RNG slot offset)
-    // compile-time trip count when N is a template constant (keeps out[] / macc[] in registers)
-    __device__ __forceinline__ uint32_t n() const { return NT > 0 ? (uint32_t)NT : N_; }
-    __device__ __forceinline__ void init(uint32_t nn) {
-        N_ = nn;
-        for (uint32_t j = 0; j < n(); j++) { sub_init(out[j]); macc[j] = 0u; }
-        t = 0;
-    }
-    // combine one input sub-reservoir (reservoir.cpp:47-54 / :75-82)
-    __device__ __forceinline__ void consume(const SceneDev& s, const FeaturesDev& f, const Px& cur, const Sub& in, uint32_t ps, uint32_t slot0) {
-        consume_pd(target_pdf(s, f, cur, in.pos, in.col), in, ps, slot0);
-    }
-    // the same with the input's target pdf at the combining pixel already known (the rp cache)
-    __device__ __forceinline__ void consume_pd(float pd, const Sub& in, uint32_t ps, uint32_t slot0) {
-        float w = (pd * in.W) * (float)in.M;
-        uint32_t k = res_update<NT>(out, n(), in.pos, in.col, w, rand01(draw(ps, slot0 + t)), pd);
-        t++;
-        macc_add<NT>(macc, k, in.M);
-    }
-    __device__ __forceinline__ void finish_biased(const SceneDev& s, const FeaturesDev& f, const Px& cur, float* pd_out = nullptr) {
-        for (uint32_t j = 0; j < n(); j++) out[j].M = macc[j];
-        for (uint32_t j = 0; j < n(); j++) {
-            const float pj = out[j].has_pd ? out[j].pd : target_pdf(s, f, cur, out[j].pos, out[j].col);
-            out[j].W = contribution_weight(pj, out[j].M, out[j].wsum);
-            if (pd_out) pd_out[j] = pj;
-        }
-    }
-};
+ROMIS_PRIMARY_RIS_TEMPORAL_KERNEL(1, k_primary_ris_n1_lds_pt_temporal, ROMIS_RIS1_ATTR)
+ROMIS_PRIMARY_RIS_TEMPORAL_KERNEL(2, k_primary_ris_n2_lds_pt_temporal, ROMIS_RIS_ATTR)
 
 // k_temporal: temporalReuse (render_utils.cpp:142-177).  cur = (ca, cb), prev = (pa, pb); writes (oa, ob).
 template <int NT>
@@ -2195,6 +2238,25 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
                  cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr, tu.ris_late, tmiss,
                  tmiss ? skip_res : 0u, (lt == kLtPoint || lt == kLtRegular) && f.N == 1 ? h.w : nullptr,
                  lt == kLtPoint && f.N == 1 ? h.m : nullptr, h.w && (lt == kLtPoint || lt == kLtRegular) ? h.res_dead : 0u);
+    return hipGetLastError();
+}
+
+bool primary_ris_temporal_fits(const SceneDev& s, const FeaturesDev& f, const Tuning& tu) {
+    const int lt = ris_light_form(s, f, tu);
+    return tu.fuse_temporal && (f.N == 1 || f.N == 2) && lt == kLtPoint && tu.ris_lds && s.num_lights > 0 &&
+           bvh_lds_bytes(s) + ris_lights_lds_bytes(s, lt) <= kLdsBudget;
+}
+
+hipError_t launch_primary_ris_temporal(const SceneDev& s, const Region& rg0, const CameraDev& cam, const FeaturesDev& f,
+                                       uint32_t key, float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb,
+                                       float2* rdbg, float* rp, const Tuning& tu, hipStream_t stream, TemporalIn tin) {
+    if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
+    if (!primary_ris_temporal_fits(s, f, tu)) return hipErrorInvalidValue;   // the caller checks
+    const Region rg = with_map(rg0, 1u);
+    const size_t lds = bvh_lds_bytes(s) + ris_lights_lds_bytes(s, kLtPoint);
+    auto k = f.N == 1 ? k_primary_ris_n1_lds_pt_temporal : k_primary_ris_n2_lds_pt_temporal;
+    ROMIS_LAUNCH(k, dim3(items_of(rg)), dim3(kBlock), lds, stream, s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg,
+                 f.N == 1 ? rp : nullptr, tu.ris_late, tin);
     return hipGetLastError();
 }
 

@@ -27,6 +27,11 @@ bool spatial_handles_ok(const SceneDev& s, const FeaturesDev& f, const Tuning& t
 // which: 0 point-light handles (8 B per pixel), 1 light-grid handles (16 B), -1 none
 int spatial_handle_kind(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes);
 bool primary_ris_fits(const SceneDev& s);
+// primary rays + RIS + temporal reuse in one kernel (N = 1 / 2, point lights, the light table in LDS; fuse.temporal)
+bool primary_ris_temporal_fits(const SceneDev& s, const FeaturesDev& f, const Tuning& tu);
+hipError_t launch_primary_ris_temporal(const SceneDev& s, const Region& rg, const CameraDev& cam, const FeaturesDev& f,
+                                       uint32_t key, float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb,
+                                       float2* rdbg, float* rp, const Tuning& tu, hipStream_t stream, TemporalIn tin);
 // the N = 1 spatial pass reads background tiles through MissTiles for this scene / features / knobs (SoA planes)
 bool spatial_reads_flags(const SceneDev& s, const FeaturesDev& f, const Tuning& tu);
 // final shading writes background tiles from MissTiles without reading them (k_final_n1_sorted)

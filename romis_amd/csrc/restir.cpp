@@ -1317,7 +1317,18 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     // ghost ring holds intermediate values, include/restir_c.h)
     Handles ris_handles = fb.h(cur);
     ris_handles.res_dead = 1u;
-    if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)
+    // temporal reuse inside the fused kernel (k_primary_ris_n{1,2}_lds_pt_temporal): the predecessor's reservoirs are
+    // combined while the RIS reservoirs are still in registers (no store / reload, no G-buffer re-read, one launch less)
+    const bool temporal_fused = temporal && fused && !handles && primary_ris_temporal_fits(s, f, c->tuning);
+    if (temporal_fused) {
+        ST_TRY(use_prev(prev, c->device, st));   // the predecessor's records are complete (its producer's stream)
+        TIMED(c, RESTIR_K_PRIMARY_RIS,
+              launch_primary_ris_temporal(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur), fb.rb(cur), nullptr,
+                                          fb.rp(cur), c->tuning, st,
+                                          TemporalIn{fb.pa(prev), fb.pb(prev),
+                                                     restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0)}));
+        used_prev(prev, st);
+    } else if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)
         bool written = false;
         TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),
                                                           fb.rb(cur), nullptr, fb.rp(cur), c->tuning, st, tmiss, skip_mode,
@@ -1331,7 +1342,7 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
         TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, ris_key, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), nullptr,
                                           fb.rp(cur), c->tuning, st));
     }
-    if (temporal) {
+    if (temporal && !temporal_fused) {
         ST_TRY(use_prev(prev, c->device, st));   // the predecessor's records are complete (its producer's stream)
         TIMED(c, RESTIR_K_TEMPORAL,
               launch_temporal(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0), camd.origin, fb.nt(cur), pm,
@@ -2306,6 +2317,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.th")) { if (v > 2) return fail(RESTIR_ERR_INVALID, "spatial.th: 0 (auto), 1 or 2"); t.spatial_th = v; }
     else if (!std::strcmp(key, "spatial.handles")) t.spatial_handles = v;
     else if (!std::strcmp(key, "fuse.primary_ris")) t.fuse_primary_ris = v;
+    else if (!std::strcmp(key, "fuse.temporal")) t.fuse_temporal = v;
     else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;
     else if (!std::strcmp(key, "timing.every")) { t.timing_every = v ? v : 1u; for (auto& q : c->timing_seq) q = 0; }
     else if (!std::strcmp(key, "timing.fence")) {

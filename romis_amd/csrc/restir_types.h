@@ -114,6 +114,13 @@ struct MissTiles {
 
 // Sample handles (N = 1, point-light scenes, kernels.hip k_spatial1h): per view pixel the held sample's W (w) and
 // M | light index << 24 (m; index L = the initial zero sample), written beside the reservoir planes by the producer.
+// The predecessor grid of a temporal pass fused into primary rays + RIS (launch_primary_ris_temporal)
+struct TemporalIn {
+    const float4* pa;
+    const float4* pb;
+    uint32_t key;   // the temporal stage's RNG key
+};
+
 struct Handles {
     float* w;
     uint32_t* m;
@@ -144,6 +151,7 @@ struct Tuning {
     uint32_t fuse_primary_ris = 1; // restir_render: k_primary_ris instead of k_primary + k_ris when the BVH fits LDS
     uint32_t spatial_lean = 1;     // the lean N = 1 / 2 passes (0: the general kernels)
     uint32_t spatial_th = 0;       // N = 1 biased ntl pass: tile height in 8-row units (1: 32x8, 2: 32x16 k_spatial1_ntl_t2; 0: by width)
+    uint32_t fuse_temporal = 1;    // restir_render with a predecessor: temporal reuse inside the fused RIS kernel
     uint32_t spatial_handles = 1;  // restir_render, N = 1 biased, point lights: the passes read sample handles (k_spatial1h)
     uint32_t timing_mask = 0xFFFFFFFFu;   // kernels (bit = RESTIR_K_*) bracketed by HIP events when timing is on
     uint32_t timing_every = 1;     // events on every n-th launch of a timed kernel (the others launch plain)

@@ -59,16 +59,23 @@ def main():
             if any(k.startswith("bvh.") for k in keys):   # BVH knobs apply at the next set_scene
                 r.set_scene(scene.bench_scene(cf["scene"]))
             r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
-            rgb, _ = r.render_restir(None, cam, W, H, f, want_grid=False)
+            # temporal configs (c3): the second frame reuses the first's grid, so its image checks the temporal path
+            rgb, g = r.render_restir(None, cam, W, H, f, want_grid=bool(cf["temporal"]))
+            if cf["temporal"]:
+                rgb, g = r.render_restir(g, cam, W, H, f, want_grid=True)
             if ref is None:
                 ref = rgb
             elif not np.array_equal(rgb.view(np.uint32), ref.view(np.uint32)):
                 raise SystemExit(f"variant {name} changed the image")
             r.reset_timings()
             r.enable_timing(True)
-            for _ in range(args.frames):
-                r.render_restir(None, cam, W, H, f, want_rgb=False, want_grid=False)
+            for _ in range(args.frames):   # temporal configs thread the previous frame's grid (main.cpp:165)
+                if cf["temporal"]:
+                    _, g = r.render_restir(g, cam, W, H, f, want_rgb=False, want_grid=True)
+                else:
+                    r.render_restir(None, cam, W, H, f, want_rgb=False, want_grid=False)
             r.synchronize()
+            g = None
             r.enable_timing(False)
             for k, (ms, n) in r.timings().items():
                 if n:

@@ -469,24 +469,27 @@ def test_odd_sizes_and_extremes_match_oracle(gpu, oracle, w, h, N, passes, M):
         prev_gpu, prev_or = grid, res
 
 
-@pytest.mark.parametrize("records", [0, 1])
-def test_temporal_sequence_matches_oracle(gpu, oracle, records):
+@pytest.mark.parametrize("records,fuse,N", [(0, 1, 1), (1, 1, 1), (0, 0, 1), (0, 1, 2), (0, 0, 2)])
+def test_temporal_sequence_matches_oracle(gpu, oracle, records, fuse, N):
     """C3-style: 4 static frames, temporal reuse threading the previous frame's grid (main.cpp:165); both frame
-    buffer layouts (SoA planes, per-pixel records)."""
+    buffer layouts (SoA planes, per-pixel records); temporal reuse fused into the primary + RIS kernel (fuse.temporal,
+    the default for point lights) and as its own pass; N = 1 and 2."""
     gpu.set_tuning("layout.records", records)
+    gpu.set_tuning("fuse.temporal", fuse)
     try:
-        _temporal_sequence(gpu, oracle)
+        _temporal_sequence(gpu, oracle, N)
     finally:
         gpu.set_tuning("layout.records", 0)
+        gpu.set_tuning("fuse.temporal", 1)
 
 
-def _temporal_sequence(gpu, oracle):
+def _temporal_sequence(gpu, oracle, N=1):
     name = "nightclub_128pt"
     s = get_scene(name)
     gpu.set_scene(s)
     osc = oracle.OracleScene(s)
     cam = scene.camera_for(name, W, H)
-    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=2, temporal_reuse=1)
+    f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=2, temporal_reuse=1)
     gpu.set_seed(SEED, 0)
     prev_gpu, prev_or = None, None
     for frame in range(4):

@@ -310,9 +310,21 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 // target pdf here: pj0 for N = 1, the pdf cache's value) then the predecessor's combined biased
                 Sub prev[NT > 0 ? NT : 1];
                 unsigned long long mcur = 0, mprev = 0;
+                uint32_t phidx = L;   // the predecessor's light index (frame handles)
 #pragma unroll
                 for (uint32_t j = 0; j < (uint32_t)NT; j++) {
-                    sub_load(prev[j], tin.pa, tin.pb, ridx(rg, j, p));
+                    if (NT == 1 && LT == kLtPoint && tin.hw) {
+                        // the predecessor from its handle: the same W, M, position and colour the reservoir planes
+                        // hold (index L: the zero sample)
+                        const uint32_t hv = tin.hm[p];
+                        sub_init(prev[j]);
+                        phidx = hv >> 24;
+                        prev[j].W = tin.hw[p];
+                        prev[j].M = hv & 0x00FFFFFFu;
+                        if (phidx < L) { prev[j].pos = xyz(lights[phidx]); prev[j].col = xyz(lights[L + phidx]); }
+                    } else {
+                        sub_load(prev[j], tin.pa, tin.pb, ridx(rg, j, p));
+                    }
                     mcur += r[j].M;
                     mprev += prev[j].M;
                 }
@@ -330,6 +342,17 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 for (uint32_t j = 0; j < N; j++) cmb.consume(s, f, px, prev[j], pst, 0u);
                 float pd_out[NT > 0 ? NT : 1];
                 cmb.finish_biased(s, f, px, NT == 1 ? pd_out : nullptr);
+                // the held sample's light index: the predecessor's when the output holds its sample (bit for bit --
+                // a light with the current sample's position and colour rebuilds the same sample either way)
+                if (NT == 1 && LT == kLtPoint && hw) {
+                    const bool same = __float_as_uint(cmb.out[0].pos.x) == __float_as_uint(prev[0].pos.x) &&
+                                      __float_as_uint(cmb.out[0].pos.y) == __float_as_uint(prev[0].pos.y) &&
+                                      __float_as_uint(cmb.out[0].pos.z) == __float_as_uint(prev[0].pos.z) &&
+                                      __float_as_uint(cmb.out[0].col.x) == __float_as_uint(prev[0].col.x) &&
+                                      __float_as_uint(cmb.out[0].col.y) == __float_as_uint(prev[0].col.y) &&
+                                      __float_as_uint(cmb.out[0].col.z) == __float_as_uint(prev[0].col.z);
+                    if (same) hidx = phidx;
+                }
 #pragma unroll
                 for (uint32_t j = 0; j < (uint32_t)NT; j++) r[j] = cmb.out[j];
                 if (NT == 1 && rp) rp[p] = pd_out[0];
@@ -511,9 +534,10 @@ ROMIS_RIS_KERNEL_LT(2, false, kLtPgram, k_ris_n2_pg, ROMIS_RIS_ATTR)
     extern "C" __global__ __launch_bounds__(256) ATTR void NAME(SceneDev s, Region rg, CameraDev cam, FeaturesDev f,   \
                                                           uint32_t key, float4* n_t, float4* p_mat, float4* n_t2,      \
                                                           float4* ra, float4* rb, float2* rdbg, float* rp,             \
-                                                          uint32_t late_ok, TemporalIn tin) {                          \
+                                                          uint32_t late_ok, TemporalIn tin, float* hw, uint32_t* hm,   \
+                                                          uint32_t res_dead) {                                         \
         primary_ris_body<NT, true, kLtPoint, true>(s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, rp, late_ok,    \
-                                                   nullptr, 0u, nullptr, nullptr, 0u, tin);                            \
+                                                   nullptr, 0u, hw, hm, res_dead, tin);                                \
     }
 ROMIS_PRIMARY_RIS_KERNEL(1, true, k_primary_ris_n1_lds, ROMIS_RIS1_ATTR)
 ROMIS_PRIMARY_RIS_KERNEL(1, false, k_primary_ris_n1, ROMIS_RIS1_ATTR)
@@ -2249,20 +2273,22 @@ bool primary_ris_temporal_fits(const SceneDev& s, const FeaturesDev& f, const Tu
 
 hipError_t launch_primary_ris_temporal(const SceneDev& s, const Region& rg0, const CameraDev& cam, const FeaturesDev& f,
                                        uint32_t key, float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb,
-                                       float2* rdbg, float* rp, const Tuning& tu, hipStream_t stream, TemporalIn tin) {
+                                       float2* rdbg, float* rp, const Tuning& tu, hipStream_t stream, TemporalIn tin,
+                                       Handles h) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     if (!primary_ris_temporal_fits(s, f, tu)) return hipErrorInvalidValue;   // the caller checks
+    if (f.N != 1 && (h.w || tin.hw)) return hipErrorInvalidValue;          // handles: N = 1
     const Region rg = with_map(rg0, 1u);
     const size_t lds = bvh_lds_bytes(s) + ris_lights_lds_bytes(s, kLtPoint);
     auto k = f.N == 1 ? k_primary_ris_n1_lds_pt_temporal : k_primary_ris_n2_lds_pt_temporal;
     ROMIS_LAUNCH(k, dim3(items_of(rg)), dim3(kBlock), lds, stream, s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg,
-                 f.N == 1 ? rp : nullptr, tu.ris_late, tin);
+                 f.N == 1 ? rp : nullptr, tu.ris_late, tin, h.w, h.m, h.w ? h.res_dead : 0u);
     return hipGetLastError();
 }
 
 bool primary_ris_fits(const SceneDev& s) { return bvh_lds_bytes(s) <= kLdsBudget; }
 
-int spatial_handle_kind(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes) {
+int spatial_handle_kind(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes, uint64_t m0) {
     if (!tu.spatial_handles || passes == 0 || f.N != 1 || f.unbiased || f.K > kLeanK || f.R > kLdsSpatialR) return -1;
     if (!tu.spatial_lean || !tu.ris_compact || s.num_lights == 0) return -1;
     int hk;
@@ -2275,8 +2301,9 @@ int spatial_handle_kind(const SceneDev& s, const FeaturesDev& f, const Tuning& t
     } else {
         return -1;
     }
-    // every M: RIS M, then each biased pass sums at most K + 1 inputs
-    uint64_t m = f.M;
+    // every M: RIS M (or m0: after temporal reuse), then each biased pass sums at most K + 1 inputs
+    uint64_t m = m0 ? m0 : f.M;
+    if (m > mmax) return -1;
     for (uint32_t p = 0; p < passes && m <= mmax; p++) m *= (uint64_t)(f.K + 1u);
     return m <= mmax ? hk : -1;
 }

@@ -25,13 +25,15 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg, const CameraD
 // every M `passes` passes can produce fits the handle's 24 bits
 bool spatial_handles_ok(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes);
 // which: 0 point-light handles (8 B per pixel), 1 light-grid handles (16 B), -1 none
-int spatial_handle_kind(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes);
+// m0: the largest M entering the passes when it exceeds RIS's f.M (temporal reuse); 0 = f.M
+int spatial_handle_kind(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes, uint64_t m0 = 0);
 bool primary_ris_fits(const SceneDev& s);
 // primary rays + RIS + temporal reuse in one kernel (N = 1 / 2, point lights, the light table in LDS; fuse.temporal)
 bool primary_ris_temporal_fits(const SceneDev& s, const FeaturesDev& f, const Tuning& tu);
 hipError_t launch_primary_ris_temporal(const SceneDev& s, const Region& rg, const CameraDev& cam, const FeaturesDev& f,
                                        uint32_t key, float4* n_t, float4* p_mat, float4* n_t2, float4* ra, float4* rb,
-                                       float2* rdbg, float* rp, const Tuning& tu, hipStream_t stream, TemporalIn tin);
+                                       float2* rdbg, float* rp, const Tuning& tu, hipStream_t stream, TemporalIn tin,
+                                       Handles h);   // h: the output's sample handles (N = 1; as launch_primary_ris)
 // the N = 1 spatial pass reads background tiles through MissTiles for this scene / features / knobs (SoA planes)
 bool spatial_reads_flags(const SceneDev& s, const FeaturesDev& f, const Tuning& tu);
 // final shading writes background tiles from MissTiles without reading them (k_final_n1_sorted)

@@ -162,6 +162,9 @@ struct restir_frame {
     DevBuf rec;   // the frame's reservoirs over its view: per-pixel records [n_t, a_0, b_0, ...] or [a planes | b planes]
     bool records = true;
     uint32_t W = 0, H = 0, vx0 = 0, vy0 = 0, vw = 0, vh = 0, N = 0;
+    // frame handles: the scene upload (restir_ctx::scene_gen) whose light table the sample handles at rec's tail
+    // (W, M | light index << 24, after the reservoir planes) index; 0 = none written
+    uint64_t hgen = 0;
     std::shared_ptr<FramePool> pool;   // where rec goes back on release (the producing context's)
     std::mutex mu;
     hipEvent_t ready = nullptr;        // recorded on the producer's stream after its last kernel touching rec
@@ -210,6 +213,7 @@ struct restir_ctx {
         tex_dims, tri_uv;
     SceneDev sdev{};
     bool has_scene = false;
+    uint64_t scene_gen = 0;   // unique per scene upload (frame handles name the light table they index)
 
     // work buffers for one view
     uint32_t vw = 0, vh = 0, N = 0;
@@ -705,6 +709,15 @@ struct FrameBufs {
         float* w = hnd_()[i].as<float>();
         return w ? Handles{w, reinterpret_cast<uint32_t*>(w + npx), 0u} : Handles{nullptr, nullptr, 0u};
     }
+    // frame handles: the same planes at the tail of rec[i] (N = 1, planes layout, ensure_records), handed on with the
+    // records to the frame restir_render returns -- the next frame's fused temporal reuse reads them (8 B / px, not 32)
+    Handles fh(int i) const {
+        if (records || N != 1) return Handles{nullptr, nullptr, 0u};
+        float* w = reinterpret_cast<float*>(rec_()[i].as<float4>() + 2 * npx);
+        return Handles{w, reinterpret_cast<uint32_t*>(w + npx), 0u};
+    }
+    const float* fhw(const restir_frame* f) const { return reinterpret_cast<const float*>(f->rec.as<float4>() + 2 * npx); }
+    const uint32_t* fhm(const restir_frame* f) const { return reinterpret_cast<const uint32_t*>(fhw(f) + npx); }
     float4* nt(int i) const { return records ? rec_()[i].as<float4>() : n_t_().as<float4>(); }
     float4* ra(int i) const { return rec_()[i].as<float4>() + (records ? 1 : 0); }
     float4* rb(int i) const { return rec_()[i].as<float4>() + (records ? 2 : npx * N); }
@@ -722,7 +735,8 @@ restir_status ensure_records(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N
     const hipStream_t st = c->stream;
     ST_TRY(c->p_mat.ensure(npx * 16));
     if (!fb.records) ST_TRY(fb.n_t_().ensure(npx * 16));
-    const size_t rec_bytes = npx * (fb.records ? 1u + 2u * N : 2u * N) * 16;
+    // (N = 1 planes: + the frame handles' two 4-byte planes and 16 B of slack, FrameBufs::fh)
+    const size_t rec_bytes = npx * (fb.records ? 1u + 2u * N : 2u * N) * 16 + (!fb.records && N == 1 ? npx * 8 + 16 : 0);
     DevBuf* rec = fb.rec_();
     for (int i = 0; i < 2; i++) {
         // a buffer handed to a frame comes back through the pool (stream-ordered against its past users)
@@ -1129,6 +1143,8 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     for (const std::vector<float>* nv : {&n0, &n1, &n2})
         for (size_t i = 0; i < nv->size(); i++)
             if ((i % 4) != 3 && !(std::fabs((*nv)[i]) <= 0x1p125f)) s.normals_bounded = 0u;
+    static std::atomic<uint64_t> scene_gens{0};
+    c->scene_gen = ++scene_gens;
     c->has_scene = true;
     return RESTIR_OK;
 }
@@ -1307,9 +1323,19 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     // sample handles (k_spatial1h): N = 1 biased passes over a point-light scene, written by the fused RIS kernel and by
     // every pass but the last; 4 + 4 B per pixel and 16 B of slack (the planes are read a word at a time)
     // (point lights: two 4-byte planes; a regular light grid: one float4 plane, k_spatial1g)
-    const int hkind = spatial_handle_kind(s, f, c->tuning, passes);
-    const bool handles = fused && !temporal && !fb.records && hkind >= 0 &&
+    // With temporal reuse the passes read handles when the fused temporal kernel can rebuild the predecessor from its
+    // frame handles (point lights, the same scene upload): every M then bounded by RIS's plus the clamp's
+    const bool no_ghost = t.gwidth == t.width && t.gheight == t.height;
+    const bool temporal_handles = temporal && fused && !fb.records && N == 1 && no_ghost && prev->hgen != 0 &&
+                                  prev->hgen == c->scene_gen && primary_ris_temporal_fits(s, f, c->tuning);
+    const uint64_t m_in = temporal ? (uint64_t)f.M + (uint64_t)f.clamp_m * f.M + 1u : 0u;
+    const int hkind = (temporal && !temporal_handles) ? -1 : spatial_handle_kind(s, f, c->tuning, passes, m_in);
+    const bool handles = fused && !fb.records && hkind >= 0 && (!temporal || hkind == 0) &&
                          (size_t)t.gwidth * t.gheight * 16u <= 0xFFFFFFFFull;
+    // the last pass also writes the returned grid's handles (point lights, no ghost ring) for the next frame, bounded as
+    // if that frame's temporal reuse had run (its M bound)
+    const bool frame_handles = handles && hkind == 0 && out_next && no_ghost &&
+                               spatial_handle_kind(s, f, c->tuning, passes, (uint64_t)f.M + (uint64_t)f.clamp_m * f.M + 1u) == 0;
     if (handles)
         for (int i = 0; i < 2; i++) ST_TRY(fb.hnd_()[i].ensure((size_t)t.gwidth * t.gheight * (hkind ? 16u : 8u) + 16u));
     // the handle passes read RIS's samples through the handles alone, and a pass's output is read by the next pass's
@@ -1319,14 +1345,16 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     ris_handles.res_dead = 1u;
     // temporal reuse inside the fused kernel (k_primary_ris_n{1,2}_lds_pt_temporal): the predecessor's reservoirs are
     // combined while the RIS reservoirs are still in registers (no store / reload, no G-buffer re-read, one launch less)
-    const bool temporal_fused = temporal && fused && !handles && primary_ris_temporal_fits(s, f, c->tuning);
+    const bool temporal_fused = temporal && fused && primary_ris_temporal_fits(s, f, c->tuning);
     if (temporal_fused) {
         ST_TRY(use_prev(prev, c->device, st));   // the predecessor's records are complete (its producer's stream)
         TIMED(c, RESTIR_K_PRIMARY_RIS,
               launch_primary_ris_temporal(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur), fb.rb(cur), nullptr,
                                           fb.rp(cur), c->tuning, st,
                                           TemporalIn{fb.pa(prev), fb.pb(prev),
-                                                     restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0)}));
+                                                     restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0),
+                                                     handles ? fb.fhw(prev) : nullptr, handles ? fb.fhm(prev) : nullptr},
+                                          handles ? ris_handles : Handles{nullptr, nullptr, 0u}));
         used_prev(prev, st);
     } else if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)
         bool written = false;
@@ -1377,6 +1405,7 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                              handles ? fb.h(cur) : Handles{nullptr, nullptr, 0u},
                              // a pass before the last is read by the next one's handles alone: no reservoir planes
                              handles && pass + 1 < passes ? Handles{fb.h(nxt).w, fb.h(nxt).m, 1u}
+                             : frame_handles              ? fb.fh(nxt)
                                                           : Handles{nullptr, nullptr, 0u}));
         cur = nxt;
     }
@@ -1390,6 +1419,7 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
         // hand the final grid's records to the frame (no copy); the context re-allocates lazily
         std::swap(fr->rec, fb.rec_()[cur]);
         fr->records = fb.records;
+        fr->hgen = frame_handles ? c->scene_gen : 0u;
         *out_next = fr;
     }
     if (out_rgb) {

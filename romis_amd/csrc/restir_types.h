@@ -119,6 +119,10 @@ struct TemporalIn {
     const float4* pa;
     const float4* pb;
     uint32_t key;   // the temporal stage's RNG key
+    // N = 1 point lights: the predecessor's sample handles (W, M | light index << 24), read instead of (pa, pb) -- the
+    // light table rebuilds the sample (restir_render's frame handles; nullptr: the reservoir planes)
+    const float* hw;
+    const uint32_t* hm;
 };
 
 struct Handles {

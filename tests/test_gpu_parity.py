@@ -469,21 +469,27 @@ def test_odd_sizes_and_extremes_match_oracle(gpu, oracle, w, h, N, passes, M):
         prev_gpu, prev_or = grid, res
 
 
-@pytest.mark.parametrize("records,fuse,N", [(0, 1, 1), (1, 1, 1), (0, 0, 1), (0, 1, 2), (0, 0, 2)])
-def test_temporal_sequence_matches_oracle(gpu, oracle, records, fuse, N):
+@pytest.mark.parametrize("records,fuse,N,variant", [(0, 1, 1, ""), (0, 1, 1, "rescene"), (0, 1, 1, "nohandles"),
+                                                    (1, 1, 1, ""), (0, 0, 1, ""), (0, 1, 2, ""), (0, 0, 2, "")])
+def test_temporal_sequence_matches_oracle(gpu, oracle, records, fuse, N, variant):
     """C3-style: 4 static frames, temporal reuse threading the previous frame's grid (main.cpp:165); both frame
     buffer layouts (SoA planes, per-pixel records); temporal reuse fused into the primary + RIS kernel (fuse.temporal,
-    the default for point lights) and as its own pass; N = 1 and 2."""
+    the default for point lights) and as its own pass; N = 1 and 2.  N = 1 fused: the predecessor is rebuilt from the
+    frame handles its last pass wrote and the passes read sample handles; "rescene" re-uploads the scene mid-sequence
+    (the handles' light table is stale: the reservoir planes are read), "nohandles" turns the handle passes off."""
     gpu.set_tuning("layout.records", records)
     gpu.set_tuning("fuse.temporal", fuse)
+    if variant == "nohandles":
+        gpu.set_tuning("spatial.handles", 0)
     try:
-        _temporal_sequence(gpu, oracle, N)
+        _temporal_sequence(gpu, oracle, N, rescene=variant == "rescene")
     finally:
         gpu.set_tuning("layout.records", 0)
         gpu.set_tuning("fuse.temporal", 1)
+        gpu.set_tuning("spatial.handles", 1)
 
 
-def _temporal_sequence(gpu, oracle, N=1):
+def _temporal_sequence(gpu, oracle, N=1, rescene=False):
     name = "nightclub_128pt"
     s = get_scene(name)
     gpu.set_scene(s)
@@ -493,6 +499,8 @@ def _temporal_sequence(gpu, oracle, N=1):
     gpu.set_seed(SEED, 0)
     prev_gpu, prev_or = None, None
     for frame in range(4):
+        if rescene and frame == 2:
+            gpu.set_scene(s)   # a new upload: the predecessor's frame handles name the old one (reservoir planes read)
         rgb, grid = gpu.render_restir(prev_gpu, cam, W, H, f)
         want, res, _ = oracle.render_frame(osc, cam, f, W, H, SEED, frame, prev=prev_or)
         assert_bits(rgb, want, f"frame {frame} rgb")

@@ -497,7 +497,8 @@ restir_status restir_enable_timing(restir_ctx* ctx, int enable);
  * lights only, a light grid, one-colour parallelograms -- instead of the 7-float4 records (default 1; restir_set_scene
  * detects the form bit for bit).  "spatial.xcd_rows|xcd_cols" (the spatial pass's XCD chunk shape; 255 = automatic),
  * "spatial.th" (0: auto, 1: 32x8, 2: 32x16 tiles), "spatial.handles" (N = 1 biased passes over a point-light scene read
- * sample handles, k_spatial1h; default 1), "ris.late" (stage the light table after the primary rays, only for tiles that
+ * sample handles, k_spatial1h; with temporal reuse when the predecessor frame carries the handles its last pass wrote
+ * -- N = 1 point lights, no ghost ring, the same scene upload -- else its reservoir planes are read; default 1), "ris.late" (stage the light table after the primary rays, only for tiles that
  * need it), "final.sort" (bin each tile's shadow rays by target), "final.miss" (final shading reads only p_mat and
  * (pos, W) for a primary-ray miss), "miss.tiles" (background-tile flags from RIS to the spatial passes and final
  * shading, N <= 2 without temporal reuse), "miss.gbuf" (0 / 1 / 2 = auto: RIS also skips background tiles' G-buffer

@@ -142,10 +142,17 @@ struct FramePool {
         }
         return false;
     }
-    void give(DevBuf buf, std::vector<hipEvent_t> busy) {
+    // own: an event recorded on the owning context's own stream (the frame's `ready`): the next taker, on that stream,
+    // is ordered after it already -- no wait packet (a 5-10 us gap between kernels); only a drain needs it
+    void give(DevBuf buf, std::vector<hipEvent_t> busy, hipEvent_t own = nullptr) {
         Entry e{buf, std::move(busy)};
         std::lock_guard<std::mutex> lk(mu);
-        if (closed || free.size() >= 4) { drain(e); return; }
+        if (closed || free.size() >= 4) {
+            if (own) e.busy.push_back(own);
+            drain(e);
+            return;
+        }
+        if (own) (void)hipEventDestroy(own);   // released when the recorded work completes
         free.push_back(std::move(e));
     }
     void close() {
@@ -186,15 +193,18 @@ restir_frame* make_frame(const std::shared_ptr<FramePool>& pool, int device, hip
     fr->ready = record_event(s);
     return fr;
 }
-// the consumer of a predecessor frame: its stream waits for the producer's kernels (another context / stream)
-restir_status use_prev(const restir_frame* prev, int device, hipStream_t s) {
+// the consumer of a predecessor frame: its stream waits for the producer's kernels (another context / stream; a frame
+// of this context -- own, its pool, which the frame keeps alive -- was produced on this stream: ordered already)
+restir_status use_prev(const restir_frame* prev, int device, hipStream_t s, const FramePool* own) {
     if (prev->device != device)
         return fail(RESTIR_ERR_INVALID, "temporal predecessor lives on device %d, this context on %d", prev->device, device);
-    if (prev->ready) HIP_TRY(hipStreamWaitEvent(s, prev->ready, 0));
+    if (prev->ready && prev->pool.get() != own) HIP_TRY(hipStreamWaitEvent(s, prev->ready, 0));
     return RESTIR_OK;
 }
-// ... and records that it read it, so the records are not recycled under the read
-void used_prev(const restir_frame* prev, hipStream_t s) {
+// ... and records that it read it, so the records are not recycled under the read (the pool's taker is its own
+// context, on this stream when the reader is that context: ordered already)
+void used_prev(const restir_frame* prev, hipStream_t s, const FramePool* own) {
+    if (prev->pool.get() == own) return;
     restir_frame* fr = const_cast<restir_frame*>(prev);
     hipEvent_t ev = record_event(s);
     if (!ev) { (void)hipStreamSynchronize(s); return; }
@@ -1347,7 +1357,7 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     // combined while the RIS reservoirs are still in registers (no store / reload, no G-buffer re-read, one launch less)
     const bool temporal_fused = temporal && fused && primary_ris_temporal_fits(s, f, c->tuning);
     if (temporal_fused) {
-        ST_TRY(use_prev(prev, c->device, st));   // the predecessor's records are complete (its producer's stream)
+        ST_TRY(use_prev(prev, c->device, st, c->pool.get()));   // the predecessor's records are complete (its producer's stream)
         TIMED(c, RESTIR_K_PRIMARY_RIS,
               launch_primary_ris_temporal(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur), fb.rb(cur), nullptr,
                                           fb.rp(cur), c->tuning, st,
@@ -1355,7 +1365,7 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                                                      restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0),
                                                      handles ? fb.fhw(prev) : nullptr, handles ? fb.fhm(prev) : nullptr},
                                           handles ? ris_handles : Handles{nullptr, nullptr, 0u}));
-        used_prev(prev, st);
+        used_prev(prev, st, c->pool.get());
     } else if (fused) {   // same region: one kernel (kernels.hip k_primary_ris)
         bool written = false;
         TIMED(c, RESTIR_K_PRIMARY_RIS, launch_primary_ris(s, view, camd, f, ris_key, fb.nt(0), pm, fb.nt2(), fb.ra(cur),
@@ -1371,12 +1381,12 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
                                           fb.rp(cur), c->tuning, st));
     }
     if (temporal && !temporal_fused) {
-        ST_TRY(use_prev(prev, c->device, st));   // the predecessor's records are complete (its producer's stream)
+        ST_TRY(use_prev(prev, c->device, st, c->pool.get()));   // the predecessor's records are complete (its producer's stream)
         TIMED(c, RESTIR_K_TEMPORAL,
               launch_temporal(s, view, f, restir_rng_key(c->seed, frame, RESTIR_STAGE_TEMPORAL, 0), camd.origin, fb.nt(cur), pm,
                               fb.ra(cur), fb.rb(cur), fb.pa(prev), fb.pb(prev), fb.ra(cur), fb.rb(cur), nullptr,
                               fb.rp(cur), fb.rp(cur), c->tuning, st));
-        used_prev(prev, st);
+        used_prev(prev, st, c->pool.get());
     }
     bool rp_ok = fb.rp(cur) != nullptr;   // the current grid's target-pdf cache holds its samples' pdfs
     // the last pass's own-pixel shadow rays (unbiased + visibility reuse, N = 1) go on to final shading
@@ -1442,10 +1452,10 @@ void restir_frame_release(restir_frame* fr) {
         // touched them (the next user waits on those on its own stream); no device-wide synchronisation
         (void)hipSetDevice(fr->device);
         std::vector<hipEvent_t> busy = std::move(fr->reads);
-        if (fr->ready) busy.push_back(fr->ready);
         if (fr->pool) {
-            fr->pool->give(fr->rec, std::move(busy));
+            fr->pool->give(fr->rec, std::move(busy), fr->ready);   // ready: on the pool owner's stream
         } else {
+            if (fr->ready) busy.push_back(fr->ready);
             FramePool::Entry e{fr->rec, std::move(busy)};
             FramePool::drain(e);
         }
@@ -1852,7 +1862,7 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
             return fail(RESTIR_ERR_INVALID, "temporal predecessor grid does not match this tile's view / N");
         if (prev->records != (c->tuning.records != 0))
             return fail(RESTIR_ERR_INVALID, "temporal predecessor grid was rendered with the other buffer layout");
-        ST_TRY(use_prev(prev, c->device, c->stream));
+        ST_TRY(use_prev(prev, c->device, c->stream, c->pool.get()));
     }
     auto& h = c->halo;
     h.active = false;
@@ -1891,7 +1901,7 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
               launch_temporal(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_TEMPORAL, 0), h.camd.origin, fb.nt(0),
                               pm, fb.ra(0), fb.rb(0), fb.pa(prev), fb.pb(prev), fb.ra(0), fb.rb(0), nullptr, fb.rp(0),
                               fb.rp(0), c->tuning, c->stream));
-    if (temporal) used_prev(prev, c->stream);
+    if (temporal) used_prev(prev, c->stream, c->pool.get());
     h.rp_ok = fb.rp(0) != nullptr;
     h.active = true;
     if (send_bytes) *send_bytes = h.send_bytes;

@@ -612,6 +612,7 @@ def main():
     r.synchronize()
     r.enable_timing(False)
     kt_all = r.timings()
+    bg_info = r.background_pixels()
     state["grid"] = None
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -644,6 +645,17 @@ def main():
                     "traffic": traffic, "traffic_source": traffic_src, "bytes_per_launch": bytes_per_launch,
                     "avg_launch_us": round(avg_s * 1e6, 2),
                     "read_only_frac": round(sp_px * (32 + 32 * args.N) / avg_s / 1e9 / HBM_PEAK_GBS, 4)}
+        # the compulsory-byte figure beside the contract's: a pixel of a RIS-flagged background tile is
+        # written from the flag without reading anything (32 N B), the rest moves the contract's bytes; the last frame's
+        # flag count (restir_background_pixels) -- ghost-zone frames apply the computed region's share to the pass
+        if not halo and bg_info is not None and bg_info[1]:
+            share = bg_info[0] / bg_info[1]
+            comp = sp_px * ((1.0 - share) * (32 + 64 * args.N) + share * 32 * args.N)
+            roofline["background_share"] = round(share, 4)
+            roofline["compulsory_bytes_per_launch"] = int(comp)
+            roofline["frac_compulsory"] = round(comp / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+            # the survey's read-only bar (§8d: 64 B/px, <= 41.5 us at 1080p for 0.40)
+            roofline["read_only_bar_us"] = round(sp_px * (32 + 32 * args.N) / (0.40 * HBM_PEAK_GBS * 1e9) * 1e6, 2)
         # the practical ceiling next to the spec: a streaming-read kernel over 4 GiB (past the Infinity Cache), run
         # before the warm-up frames
         roofline["measured_read_peak"] = round(measured, 1)
@@ -708,6 +720,8 @@ def main():
                          "note": "ray slots = (k+1) N per pixel, an upper bound on the shadow rays cast; final = 1 per "
                                  "pixel and sub-reservoir (also an upper bound: no ray where the shaded value is 0)"}
     kernels["note"] = "separate run after the timed region, every kernel's dispatch recording HIP events"
+    # every rank computed the same mismatch count (select_halo sums it over ranks): all exit alike
+    halo_failed = halo_rec is not None and halo_rec.get("check") not in ("bit-exact", "off")
     if rank == 0:
         out = {
             "metric": "Mpixel-reservoirs/s at 1080p, M=32, k=5 spatial; 1/2/4/8 GPU",
@@ -731,10 +745,14 @@ def main():
         }
         if halo_rec is not None:
             out["halo"] = halo_rec
+        if halo_failed:   # a non-fatal halo check that failed still fails the run (after the record)
+            out["error"] = "halo tile differs from the ghost-zone tile (halo.check)"
         print(json.dumps(out), flush=True)
     r.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+    if halo_failed:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

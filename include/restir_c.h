@@ -214,6 +214,38 @@ restir_status restir_halo_plan(uint32_t global_width, uint32_t global_height, ui
                                uint32_t rank, uint32_t radius, uint32_t N, restir_halo_segment* send,
                                restir_halo_segment* recv, uint32_t* count);
 
+/* Uneven screen tiles (cost-balanced plans for frames whose geometry is not spread evenly).  A layout
+ * cuts the image into tiles_x columns at x_cuts (x_cuts[0] = 0 < x_cuts[1] < ... < x_cuts[tiles_x] = width) and
+ * each column c into tiles_y rows at its own y_cuts[c] (0 = y_cuts[c][0] < ... < y_cuts[c][tiles_y] = height); rank
+ * ty * tiles_x + tx owns [x_cuts[tx], x_cuts[tx + 1]) x [y_cuts[tx][ty], y_cuts[tx][ty + 1]).  One rectangle per rank,
+ * every pixel owned once; with tiles_y <= 4 a rank has at most 2 + 2 tiles_y halo partners (<= 8 segments).  Any
+ * layout renders bit-identically to one GPU: the spatial clamp is global (render_utils.cpp:109-110) and the RNG is
+ * keyed by global pixel.  restir_layout_even is restir_tile_plan's split; restir_tile_plan / restir_halo_plan /
+ * restir_halo_ops / restir_halo_begin are the _layout functions over it. */
+#define RESTIR_MAX_TILES_X 16u
+#define RESTIR_MAX_TILES_Y 16u
+typedef struct restir_tile_layout {
+    uint32_t global_width, global_height, tiles_x, tiles_y;
+    uint32_t x_cuts[RESTIR_MAX_TILES_X + 1];
+    uint32_t y_cuts[RESTIR_MAX_TILES_X][RESTIR_MAX_TILES_Y + 1];
+} restir_tile_layout;
+restir_status restir_layout_even(uint32_t global_width, uint32_t global_height, uint32_t tiles_x, uint32_t tiles_y,
+                                 restir_tile_layout* out);
+/* A layout balancing `cost` -- a cost_w x cost_h grid of per-cell work over the image (row-major, row 0 = the bottom
+ * row, cell (i, j) = the pixels x with floor(x cost_w / width) = i and y with floor(y cost_h / height) = j, the cell's
+ * cost spread evenly over them): the x cuts split the column totals into equal shares, then each column's y cuts
+ * split its own row totals.  Cuts are rounded to multiples of align_x / align_y (0: 1) and keep every tile at least
+ * one alignment unit wide / high.  *efficiency (may be NULL) = mean over ranks of a rank's cost / the largest. */
+restir_status restir_layout_balanced(uint32_t global_width, uint32_t global_height, uint32_t tiles_x, uint32_t tiles_y,
+                                     const float* cost, uint32_t cost_w, uint32_t cost_h, uint32_t align_x,
+                                     uint32_t align_y, restir_tile_layout* out, double* efficiency);
+/* The cost share a layout gives each rank (out[rank], summing to 1) under the same cost grid. */
+restir_status restir_layout_shares(const restir_tile_layout* layout, const float* cost, uint32_t cost_w, uint32_t cost_h,
+                                   double* out);
+restir_status restir_layout_tile(const restir_tile_layout* layout, uint32_t rank, uint32_t ghost, restir_tile* out);
+restir_status restir_layout_halo_plan(const restir_tile_layout* layout, uint32_t rank, uint32_t radius, uint32_t N,
+                                      restir_halo_segment* send, restir_halo_segment* recv, uint32_t* count);
+
 /* ---- context ----------------------------------------------------------------------------------------- */
 /* (halo-mode frame functions: after the render / stage API below) */
 typedef struct restir_ctx   restir_ctx;
@@ -376,6 +408,10 @@ restir_status restir_debug_math(restir_ctx* ctx, const float* x, const float* y,
 restir_status restir_halo_begin(restir_ctx* ctx, const restir_camera* cam, const restir_features* features,
                                 uint32_t width, uint32_t height, uint32_t tiles_x, uint32_t tiles_y, uint32_t rank,
                                 const restir_frame* prev, uint64_t* send_bytes, uint64_t* recv_bytes);
+/* restir_halo_begin over an uneven layout (restir_tile_layout): rank `rank`'s tile of it */
+restir_status restir_halo_begin_layout(restir_ctx* ctx, const restir_camera* cam, const restir_features* features,
+                                       const restir_tile_layout* layout, uint32_t rank, const restir_frame* prev,
+                                       uint64_t* send_bytes, uint64_t* recv_bytes);
 restir_status restir_halo_pack(restir_ctx* ctx, void* send_buf, uint64_t bytes, int host_memory);
 restir_status restir_halo_unpack(restir_ctx* ctx, const void* recv_buf, uint64_t bytes, int host_memory);
 restir_status restir_halo_spatial(restir_ctx* ctx);
@@ -419,6 +455,8 @@ typedef struct restir_halo_op {
 } restir_halo_op;
 restir_status restir_halo_ops(uint32_t global_width, uint32_t global_height, uint32_t tiles_x, uint32_t tiles_y,
                               uint32_t rank, uint32_t radius, uint32_t N, restir_halo_op* ops, uint32_t* count);
+restir_status restir_layout_halo_ops(const restir_tile_layout* layout, uint32_t rank, uint32_t radius, uint32_t N,
+                                     restir_halo_op* ops, uint32_t* count);
 
 /* Record-only mode of restir_halo_pass: the native transport's plumbing checked without a second GPU.  With
  * restir_halo_record(ctx, 1) a pass needs no communicator and posts no RCCL operation; it appends every step it
@@ -476,6 +514,13 @@ restir_status restir_features_json(const restir_features* features, const restir
  * streaming-read kernel over `bytes` (rounded down to 16 B; pass >= 1 GiB to defeat the 256 MB Infinity
  * Cache), timed with HIP events over `iters` launches.  *out_gbps = bytes * iters / time / 1e9. */
 restir_status restir_measure_read_bandwidth(restir_ctx* ctx, uint64_t bytes, uint32_t iters, double* out_gbps);
+
+/* Background pixels of the last restir_render frame (the compulsory-byte roofline, bench.py roofline.frac_compulsory):
+ * the pixels of the RIS tiles (32 x 8 over the frame's computed region) whose every pixel missed the scene with the RIS
+ * result known -- the MissTiles flags from which the spatial passes and final shading write those tiles without reading
+ * them.  *computed = the region's pixels; *background = 0 when the frame kept no flags (temporal reuse, N > 2, knob
+ * "miss.tiles" off).  Synchronises the context's stream. */
+restir_status restir_background_pixels(restir_ctx* ctx, uint64_t* background, uint64_t* computed);
 
 /* ---- timing ----------------------------------------------------------------------------------------- */
 /* When enabled, every kernel of restir_render / restir_stage_* is bracketed by HIP events on the

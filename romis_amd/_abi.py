@@ -119,7 +119,36 @@ class Tile(C.Structure):
                 ("gx0", C.c_uint32), ("gy0", C.c_uint32), ("gwidth", C.c_uint32), ("gheight", C.c_uint32)]
 
 
+RESTIR_MAX_TILES_X = 16
+RESTIR_MAX_TILES_Y = 16
+
+
+class TileLayout(C.Structure):
+    """restir_tile_layout: column cuts x_cuts[0..tiles_x], per-column row cuts y_cuts[c][0..tiles_y]."""
+    _fields_ = [("global_width", C.c_uint32), ("global_height", C.c_uint32), ("tiles_x", C.c_uint32),
+                ("tiles_y", C.c_uint32), ("x_cuts", C.c_uint32 * (RESTIR_MAX_TILES_X + 1)),
+                ("y_cuts", (C.c_uint32 * (RESTIR_MAX_TILES_Y + 1)) * RESTIR_MAX_TILES_X)]
+
+    def cuts(self) -> dict:
+        """JSON form: {"x": [...], "y": [[...] per column]}."""
+        tx, ty = self.tiles_x, self.tiles_y
+        return {"x": list(self.x_cuts[:tx + 1]), "y": [list(self.y_cuts[c][:ty + 1]) for c in range(tx)]}
+
+    @classmethod
+    def from_cuts(cls, width: int, height: int, cuts: dict) -> "TileLayout":
+        L = cls()
+        L.global_width, L.global_height = width, height
+        L.tiles_x, L.tiles_y = len(cuts["x"]) - 1, len(cuts["y"][0]) - 1
+        for i, v in enumerate(cuts["x"]):
+            L.x_cuts[i] = v
+        for c, col in enumerate(cuts["y"]):
+            for i, v in enumerate(col):
+                L.y_cuts[c][i] = v
+        return L
+
+
 assert C.sizeof(HaloOp) == 40 and C.sizeof(HaloEvent) == 32
+assert C.sizeof(TileLayout) == 4 * (4 + 17 + 16 * 17)
 assert C.sizeof(Light) == 88
 assert C.sizeof(Material) == 36
 assert C.sizeof(Mesh) == 80 and C.sizeof(Texture) == 16
@@ -213,6 +242,20 @@ SIGNATURES = {
                                        C.POINTER(C.c_size_t)]),
     "restir_halo_end": (C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_float)]),
     "restir_measure_read_bandwidth": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
+    "restir_layout_even": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(TileLayout)]),
+    "restir_layout_balanced": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_float), C.c_uint32,
+                                         C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(TileLayout),
+                                         C.POINTER(C.c_double)]),
+    "restir_layout_shares": (C.c_int, [C.POINTER(TileLayout), C.POINTER(C.c_float), C.c_uint32, C.c_uint32,
+                                       C.POINTER(C.c_double)]),
+    "restir_layout_tile": (C.c_int, [C.POINTER(TileLayout), C.c_uint32, C.c_uint32, C.POINTER(Tile)]),
+    "restir_layout_halo_plan": (C.c_int, [C.POINTER(TileLayout), C.c_uint32, C.c_uint32, C.c_uint32,
+                                          C.POINTER(HaloSegment), C.POINTER(HaloSegment), C.POINTER(C.c_uint32)]),
+    "restir_layout_halo_ops": (C.c_int, [C.POINTER(TileLayout), C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(HaloOp),
+                                         C.POINTER(C.c_uint32)]),
+    "restir_halo_begin_layout": (C.c_int, [_P, C.POINTER(Camera), C.POINTER(Features), C.POINTER(TileLayout), C.c_uint32,
+                                           _P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "restir_background_pixels": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "restir_enable_timing": (C.c_int, [_P, C.c_int]),
     "restir_set_tuning": (C.c_int, [_P, C.c_char_p, C.c_int]),
     "restir_timings": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),

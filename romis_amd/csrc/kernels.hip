@@ -454,7 +454,9 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
             if (n_t2) n_t2[gidx(rg, p)] = nt;
             p_mat[p] = pm;
         }
-        if (late && any) {
+        // TEMP with frame handles: a pixel that misses now may hold a predecessor whose handle names a real light (the
+        // camera moved), rebuilt from this table -- staged for every tile then
+        if (late && (any || (TEMP && tin.hw != nullptr))) {
             stage_lights<LT>(s, g_lds + bvh_f4);
             __syncthreads();
         }

@@ -122,6 +122,9 @@ struct FramePool {
     std::vector<Entry> free;
     bool closed = false;   // the owning context is gone: returned buffers are freed
     int device = 0;
+    // the owning context's stream (null once closed): its own later frames read a predecessor's records on it without
+    // recording read events (used_prev), so a drain waits for that stream before the records are freed
+    hipStream_t owner = nullptr;
     static void drain(Entry& e) {
         for (hipEvent_t ev : e.busy) { (void)hipEventSynchronize(ev); (void)hipEventDestroy(ev); }
         e.busy.clear();
@@ -149,6 +152,9 @@ struct FramePool {
         std::lock_guard<std::mutex> lk(mu);
         if (closed || free.size() >= 4) {
             if (own) e.busy.push_back(own);
+            // a later frame of the owner may still be reading the buffer on its stream (no read event): wait for it
+            // rather than rely on hipFree's implicit synchronisation
+            if (!closed && owner) (void)hipStreamSynchronize(owner);
             drain(e);
             return;
         }
@@ -158,6 +164,7 @@ struct FramePool {
     void close() {
         std::lock_guard<std::mutex> lk(mu);
         closed = true;
+        owner = nullptr;   // the context synchronised its stream before closing the pool
         for (Entry& e : free) drain(e);
         free.clear();
     }
@@ -234,6 +241,8 @@ struct restir_ctx {
     DevBuf rp[2];                                   // their target-pdf cache planes (N = 1, planes layout)
     DevBuf vis;                                     // unbiased + visibility pass -> final shading: own-pixel ray
     DevBuf tmiss;                                   // RIS -> spatial passes / final shading: background tiles (MissTiles)
+    uint32_t tmiss_w = 0, tmiss_h = 0;              // the last frame's computed region when it kept the flags (else 0)
+    uint64_t last_px = 0;                           // the last frame's computed pixels
     DevBuf hnd[2];                                  // sample handles of rec[i] (N = 1 point lights, k_spatial1h)
     int cur = 0;
     uint32_t rgb_w = 0, rgb_h = 0;
@@ -372,24 +381,170 @@ void restir_camera_derive(const restir_camera* cam, restir_camera_frame* out) {
     out->half_h = hh;
 }
 
-restir_status restir_tile_plan(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t tiles_y, uint32_t rank, uint32_t ghost,
-                               restir_tile* out) {
-    if (!out || W == 0 || H == 0 || tiles_x == 0 || tiles_y == 0 || rank >= tiles_x * tiles_y || tiles_x > W ||
-        tiles_y > H)
-        return fail(RESTIR_ERR_INVALID, "restir_tile_plan: bad arguments (W=%u H=%u tiles=%ux%u rank=%u)", W, H, tiles_x,
-                    tiles_y, rank);
-    const uint32_t tx = rank % tiles_x, ty = rank / tiles_x;
+}  // extern "C"
+
+namespace {
+// a layout's cuts are well formed: every column and every row of a column at least one pixel, the ends at the image
+restir_status layout_check(const restir_tile_layout* L) {
+    if (!L) return fail(RESTIR_ERR_INVALID, "tile layout is NULL");
+    const uint32_t tx = L->tiles_x, ty = L->tiles_y;
+    if (L->global_width == 0 || L->global_height == 0 || tx == 0 || ty == 0 || tx > RESTIR_MAX_TILES_X ||
+        ty > RESTIR_MAX_TILES_Y)
+        return fail(RESTIR_ERR_INVALID, "tile layout: bad size (W=%u H=%u tiles=%ux%u, at most %ux%u)", L->global_width,
+                    L->global_height, tx, ty, RESTIR_MAX_TILES_X, RESTIR_MAX_TILES_Y);
+    if (L->x_cuts[0] != 0 || L->x_cuts[tx] != L->global_width)
+        return fail(RESTIR_ERR_INVALID, "tile layout: x cuts must run from 0 to the width");
+    for (uint32_t c = 0; c < tx; c++) {
+        if (L->x_cuts[c + 1] <= L->x_cuts[c]) return fail(RESTIR_ERR_INVALID, "tile layout: x cuts not increasing at %u", c);
+        if (L->y_cuts[c][0] != 0 || L->y_cuts[c][ty] != L->global_height)
+            return fail(RESTIR_ERR_INVALID, "tile layout: column %u's y cuts must run from 0 to the height", c);
+        for (uint32_t r = 0; r < ty; r++)
+            if (L->y_cuts[c][r + 1] <= L->y_cuts[c][r])
+                return fail(RESTIR_ERR_INVALID, "tile layout: column %u's y cuts not increasing at %u", c, r);
+    }
+    return RESTIR_OK;
+}
+// pixels of cost cell i along an axis of n pixels split into m cells: x belongs to cell floor(x m / n)
+inline uint32_t cell_of(uint32_t x, uint32_t m, uint32_t n) { return (uint32_t)((uint64_t)x * m / n); }
+inline uint32_t cell_begin(uint32_t i, uint32_t m, uint32_t n) { return (uint32_t)(((uint64_t)i * n + m - 1) / m); }
+// pixels of [a, b) in cell i
+inline uint32_t cell_overlap(uint32_t i, uint32_t m, uint32_t n, uint32_t a, uint32_t b) {
+    const uint32_t c0 = std::max(cell_begin(i, m, n), a), c1 = std::min(cell_begin(i + 1, m, n), b);
+    return c1 > c0 ? c1 - c0 : 0u;
+}
+// the cost the grid puts on the rectangle [xa, xb) x [ya, yb) (each cell's cost spread evenly over its pixels)
+double rect_cost(const float* cost, uint32_t cw, uint32_t ch, uint32_t W, uint32_t H, uint32_t xa, uint32_t xb,
+                 uint32_t ya, uint32_t yb) {
+    double sum = 0.0;
+    const uint32_t j0 = cell_of(ya, ch, H), j1 = cell_of(yb - 1, ch, H), i0 = cell_of(xa, cw, W), i1 = cell_of(xb - 1, cw, W);
+    for (uint32_t j = j0; j <= j1; j++) {
+        const double fy = (double)cell_overlap(j, ch, H, ya, yb) / (cell_begin(j + 1, ch, H) - cell_begin(j, ch, H));
+        for (uint32_t i = i0; i <= i1; i++) {
+            const double fx = (double)cell_overlap(i, cw, W, xa, xb) / (cell_begin(i + 1, cw, W) - cell_begin(i, cw, W));
+            sum += (double)cost[(size_t)j * cw + i] * fx * fy;
+        }
+    }
+    return sum;
+}
+// cuts c[1..parts-1] of [0, n) at the equal-share points of the per-pixel prefix cost P (P[x] = cost of [0, x)),
+// rounded to multiples of `align`, every part at least `align` wide (the last takes the remainder)
+void share_cuts(const std::vector<double>& P, uint32_t n, uint32_t parts, uint32_t align, uint32_t* c) {
+    c[0] = 0;
+    c[parts] = n;
+    const double total = P[n];
+    for (uint32_t k = 1; k < parts; k++) {
+        const double target = total * k / parts;
+        const uint32_t x = (uint32_t)(std::lower_bound(P.begin(), P.begin() + n + 1, target) - P.begin());
+        uint64_t q = ((uint64_t)x + align / 2) / align * align;
+        const uint64_t lo = (uint64_t)c[k - 1] + align, hi = (uint64_t)n - (uint64_t)(parts - k) * align;
+        q = std::min(std::max(q, lo), hi);
+        c[k] = (uint32_t)q;
+    }
+}
+void layout_rect(const restir_tile_layout& L, uint32_t rank, uint32_t& x0, uint32_t& y0, uint32_t& w, uint32_t& h) {
+    const uint32_t tx = rank % L.tiles_x, ty = rank / L.tiles_x;
+    x0 = L.x_cuts[tx]; w = L.x_cuts[tx + 1] - x0;
+    y0 = L.y_cuts[tx][ty]; h = L.y_cuts[tx][ty + 1] - y0;
+}
+}  // namespace
+
+extern "C" {
+
+restir_status restir_layout_even(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t tiles_y, restir_tile_layout* out) {
+    if (!out || W == 0 || H == 0 || tiles_x == 0 || tiles_y == 0 || tiles_x > W || tiles_y > H ||
+        tiles_x > RESTIR_MAX_TILES_X || tiles_y > RESTIR_MAX_TILES_Y)
+        return fail(RESTIR_ERR_INVALID, "restir_tile_plan: bad arguments (W=%u H=%u tiles=%ux%u)", W, H, tiles_x, tiles_y);
+    restir_tile_layout L{};
+    L.global_width = W; L.global_height = H; L.tiles_x = tiles_x; L.tiles_y = tiles_y;
     // even split, remainder to the first tiles (deterministic, every pixel owned exactly once)
-    auto span = [](uint32_t n, uint32_t parts, uint32_t i, uint32_t& s0, uint32_t& len) {
-        uint32_t base = n / parts, rem = n % parts;
-        s0 = i * base + std::min(i, rem);
-        len = base + (i < rem ? 1u : 0u);
-    };
+    auto start = [](uint32_t n, uint32_t parts, uint32_t i) { return i * (n / parts) + std::min(i, n % parts); };
+    for (uint32_t c = 0; c <= tiles_x; c++) L.x_cuts[c] = start(W, tiles_x, c);
+    for (uint32_t c = 0; c < tiles_x; c++)
+        for (uint32_t r = 0; r <= tiles_y; r++) L.y_cuts[c][r] = start(H, tiles_y, r);
+    *out = L;
+    return RESTIR_OK;
+}
+
+restir_status restir_layout_balanced(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t tiles_y, const float* cost,
+                                     uint32_t cw, uint32_t ch, uint32_t align_x, uint32_t align_y, restir_tile_layout* out,
+                                     double* efficiency) {
+    if (!out || !cost || cw == 0 || ch == 0 || cw > W || ch > H)
+        return fail(RESTIR_ERR_INVALID, "restir_layout_balanced: bad cost grid (%ux%u over %ux%u)", cw, ch, W, H);
+    restir_tile_layout L{};
+    ST_TRY(restir_layout_even(W, H, tiles_x, tiles_y, &L));
+    align_x = std::max(align_x, 1u);
+    align_y = std::max(align_y, 1u);
+    if ((uint64_t)tiles_x * align_x > W || (uint64_t)tiles_y * align_y > H)
+        return fail(RESTIR_ERR_INVALID, "restir_layout_balanced: %ux%u tiles of at least %ux%u px do not fit %ux%u", tiles_x,
+                    tiles_y, align_x, align_y, W, H);
+    for (size_t i = 0; i < (size_t)cw * ch; i++)
+        if (!(cost[i] >= 0.0f) || !std::isfinite(cost[i]))
+            return fail(RESTIR_ERR_INVALID, "restir_layout_balanced: cost cell %zu is negative or not finite", i);
+    // columns: the per-pixel-column cost (each cell's column total spread over its pixel columns), prefix-summed
+    std::vector<double> colsum(cw, 0.0);
+    for (uint32_t j = 0; j < ch; j++)
+        for (uint32_t i = 0; i < cw; i++) colsum[i] += cost[(size_t)j * cw + i];
+    std::vector<double> P(W + 1, 0.0);
+    for (uint32_t x = 0; x < W; x++) {
+        const uint32_t i = cell_of(x, cw, W);
+        P[x + 1] = P[x] + colsum[i] / (cell_begin(i + 1, cw, W) - cell_begin(i, cw, W));
+    }
+    share_cuts(P, W, tiles_x, align_x, L.x_cuts);
+    // each column: its own rows' cost, prefix-summed over pixel rows
+    std::vector<double> Q(H + 1, 0.0), rowsum(ch);
+    for (uint32_t c = 0; c < tiles_x; c++) {
+        const uint32_t xa = L.x_cuts[c], xb = L.x_cuts[c + 1];
+        for (uint32_t j = 0; j < ch; j++) {
+            double s = 0.0;
+            for (uint32_t i = cell_of(xa, cw, W); i <= cell_of(xb - 1, cw, W); i++)
+                s += (double)cost[(size_t)j * cw + i] * cell_overlap(i, cw, W, xa, xb) /
+                     (cell_begin(i + 1, cw, W) - cell_begin(i, cw, W));
+            rowsum[j] = s;
+        }
+        for (uint32_t y = 0; y < H; y++) {
+            const uint32_t j = cell_of(y, ch, H);
+            Q[y + 1] = Q[y] + rowsum[j] / (cell_begin(j + 1, ch, H) - cell_begin(j, ch, H));
+        }
+        share_cuts(Q, H, tiles_y, align_y, L.y_cuts[c]);
+    }
+    ST_TRY(layout_check(&L));
+    if (efficiency) {
+        std::vector<double> sh(tiles_x * tiles_y);
+        ST_TRY(restir_layout_shares(&L, cost, cw, ch, sh.data()));
+        double mx = 0.0, mean = 0.0;
+        for (double v : sh) { mx = std::max(mx, v); mean += v / sh.size(); }
+        *efficiency = mx > 0.0 ? mean / mx : 1.0;
+    }
+    *out = L;
+    return RESTIR_OK;
+}
+
+restir_status restir_layout_shares(const restir_tile_layout* L, const float* cost, uint32_t cw, uint32_t ch, double* out) {
+    ST_TRY(layout_check(L));
+    if (!cost || !out || cw == 0 || ch == 0 || cw > L->global_width || ch > L->global_height)
+        return fail(RESTIR_ERR_INVALID, "restir_layout_shares: bad cost grid");
+    const uint32_t n = L->tiles_x * L->tiles_y;
+    double total = 0.0;
+    for (uint32_t q = 0; q < n; q++) {
+        uint32_t x0, y0, w, h;
+        layout_rect(*L, q, x0, y0, w, h);
+        out[q] = rect_cost(cost, cw, ch, L->global_width, L->global_height, x0, x0 + w, y0, y0 + h);
+        total += out[q];
+    }
+    for (uint32_t q = 0; q < n; q++) out[q] = total > 0.0 ? out[q] / total : 1.0 / n;
+    return RESTIR_OK;
+}
+
+restir_status restir_layout_tile(const restir_tile_layout* L, uint32_t rank, uint32_t ghost, restir_tile* out) {
+    ST_TRY(layout_check(L));
+    if (!out || rank >= L->tiles_x * L->tiles_y)
+        return fail(RESTIR_ERR_INVALID, "restir_tile_plan: bad arguments (rank %u of %ux%u tiles)", rank, L->tiles_x,
+                    L->tiles_y);
+    const uint32_t W = L->global_width, H = L->global_height;
     restir_tile t{};
     t.global_width = W;
     t.global_height = H;
-    span(W, tiles_x, tx, t.x0, t.width);
-    span(H, tiles_y, ty, t.y0, t.height);
+    layout_rect(*L, rank, t.x0, t.y0, t.width, t.height);
     const uint32_t gx0 = t.x0 > ghost ? t.x0 - ghost : 0u;
     const uint32_t gy0 = t.y0 > ghost ? t.y0 - ghost : 0u;
     const uint32_t gx1 = std::min<uint64_t>((uint64_t)t.x0 + t.width + ghost, W);
@@ -399,11 +554,22 @@ restir_status restir_tile_plan(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_
     return RESTIR_OK;
 }
 
-restir_status restir_halo_plan(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t tiles_y, uint32_t rank, uint32_t radius,
-                               uint32_t N, restir_halo_segment* send, restir_halo_segment* recv, uint32_t* count) {
+restir_status restir_tile_plan(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t tiles_y, uint32_t rank, uint32_t ghost,
+                               restir_tile* out) {
+    restir_tile_layout L;
+    if (!out || rank >= tiles_x * tiles_y)
+        return fail(RESTIR_ERR_INVALID, "restir_tile_plan: bad arguments (W=%u H=%u tiles=%ux%u rank=%u)", W, H, tiles_x,
+                    tiles_y, rank);
+    ST_TRY(restir_layout_even(W, H, tiles_x, tiles_y, &L));
+    return restir_layout_tile(&L, rank, ghost, out);
+}
+
+restir_status restir_layout_halo_plan(const restir_tile_layout* L, uint32_t rank, uint32_t radius, uint32_t N,
+                                      restir_halo_segment* send, restir_halo_segment* recv, uint32_t* count) {
     if (!count || !send || !recv || N == 0) return fail(RESTIR_ERR_INVALID, "restir_halo_plan: null argument / N = 0");
+    const uint32_t W = L ? L->global_width : 0u, H = L ? L->global_height : 0u;
     restir_tile me{};
-    ST_TRY(restir_tile_plan(W, H, tiles_x, tiles_y, rank, 0, &me));
+    ST_TRY(restir_layout_tile(L, rank, 0, &me));
     struct R { uint64_t x0, y0, x1, y1; };
     auto grow = [&](const restir_tile& t) {
         return R{t.x0 > radius ? t.x0 - radius : 0u, t.y0 > radius ? t.y0 - radius : 0u,
@@ -418,10 +584,10 @@ restir_status restir_halo_plan(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_
     const uint32_t cap = *count;
     uint32_t n = 0;
     uint64_t so = 0, ro = 0;
-    for (uint32_t q = 0; q < tiles_x * tiles_y; q++) {
+    for (uint32_t q = 0; q < L->tiles_x * L->tiles_y; q++) {
         if (q == rank) continue;
         restir_tile tq{};
-        ST_TRY(restir_tile_plan(W, H, tiles_x, tiles_y, q, 0, &tq));
+        ST_TRY(restir_layout_tile(L, q, 0, &tq));
         const R s_ = meet(owned(me), grow(tq)), r_ = meet(owned(tq), grow(me));
         if (s_.x1 == 0 || r_.x1 == 0) continue;
         if (n >= cap) return fail(RESTIR_ERR_INVALID, "restir_halo_plan: more than %u segments", cap);
@@ -439,6 +605,13 @@ restir_status restir_halo_plan(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_
     }
     *count = n;
     return RESTIR_OK;
+}
+
+restir_status restir_halo_plan(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t tiles_y, uint32_t rank, uint32_t radius,
+                               uint32_t N, restir_halo_segment* send, restir_halo_segment* recv, uint32_t* count) {
+    restir_tile_layout L;
+    ST_TRY(restir_layout_even(W, H, tiles_x, tiles_y, &L));
+    return restir_layout_halo_plan(&L, rank, radius, N, send, recv, count);
 }
 
 }  // extern "C"
@@ -463,10 +636,17 @@ extern "C" {
 
 restir_status restir_halo_ops(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t tiles_y, uint32_t rank, uint32_t radius,
                               uint32_t N, restir_halo_op* ops, uint32_t* count) {
+    restir_tile_layout L;
+    ST_TRY(restir_layout_even(W, H, tiles_x, tiles_y, &L));
+    return restir_layout_halo_ops(&L, rank, radius, N, ops, count);
+}
+
+restir_status restir_layout_halo_ops(const restir_tile_layout* L, uint32_t rank, uint32_t radius, uint32_t N,
+                                     restir_halo_op* ops, uint32_t* count) {
     if (!count || !ops) return fail(RESTIR_ERR_INVALID, "restir_halo_ops: null argument");
     restir_halo_segment sg[RESTIR_MAX_HALO_SEGS], rg_[RESTIR_MAX_HALO_SEGS];
     uint32_t n = RESTIR_MAX_HALO_SEGS;
-    ST_TRY(restir_halo_plan(W, H, tiles_x, tiles_y, rank, radius, N, sg, rg_, &n));
+    ST_TRY(restir_layout_halo_plan(L, rank, radius, N, sg, rg_, &n));
     if (*count < 2 * n) {
         const uint32_t need = 2 * n;
         *count = need;
@@ -803,6 +983,7 @@ restir_status restir_create(int device, restir_ctx** out) {
     c->device = device;
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; return fail(RESTIR_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e)); }
+    c->pool->owner = c->stream;
     *out = c;
     return RESTIR_OK;
 }
@@ -1380,6 +1561,9 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
         TIMED(c, RESTIR_K_RIS, launch_ris(s, view, f, ris_key, camd.origin, fb.nt(cur), pm, fb.ra(cur), fb.rb(cur), nullptr,
                                           fb.rp(cur), c->tuning, st));
     }
+    c->last_px = (uint64_t)t.gwidth * t.gheight;   // restir_background_pixels
+    c->tmiss_w = tmiss ? t.gwidth : 0u;
+    c->tmiss_h = tmiss ? t.gheight : 0u;
     if (temporal && !temporal_fused) {
         ST_TRY(use_prev(prev, c->device, st, c->pool.get()));   // the predecessor's records are complete (its producer's stream)
         TIMED(c, RESTIR_K_TEMPORAL,
@@ -1782,6 +1966,26 @@ restir_status restir_debug_math(restir_ctx* c, const float* x, const float* y, f
     return RESTIR_OK;
 }
 
+restir_status restir_background_pixels(restir_ctx* c, uint64_t* background, uint64_t* computed) {
+    if (!c || !background || !computed) return fail(RESTIR_ERR_INVALID, "bad argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    *background = 0;
+    *computed = c->last_px;
+    if (!c->tmiss_w || !c->tmiss.p) return RESTIR_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const uint32_t ntx = (c->tmiss_w + 31u) / 32u, nty = (c->tmiss_h + 7u) / 8u;
+    std::vector<uint8_t> flags((size_t)ntx * nty);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(flags.data(), c->tmiss.p, flags.size(), hipMemcpyDeviceToHost));
+    uint64_t bg = 0;
+    for (uint32_t ty = 0; ty < nty; ty++)
+        for (uint32_t tx = 0; tx < ntx; tx++)
+            if (flags[(size_t)ty * ntx + tx] == 0u)   // flag 0: a background tile (kernels.hip primary_ris_body)
+                bg += (uint64_t)std::min(32u, c->tmiss_w - 32u * tx) * std::min(8u, c->tmiss_h - 8u * ty);
+    *background = bg;
+    return RESTIR_OK;
+}
+
 restir_status restir_measure_read_bandwidth(restir_ctx* c, uint64_t bytes, uint32_t iters, double* out_gbps) {
     if (!c || !out_gbps || iters == 0 || bytes < (1u << 20)) return fail(RESTIR_ERR_INVALID, "bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
@@ -1835,15 +2039,26 @@ restir_status to_segs(const restir_halo_segment* g, uint32_t n, HaloSegs& hs, ui
 restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const restir_features* features, uint32_t width,
                                 uint32_t height, uint32_t tiles_x, uint32_t tiles_y, uint32_t rank, const restir_frame* prev,
                                 uint64_t* send_bytes, uint64_t* recv_bytes) {
+    restir_tile_layout L;
+    ST_TRY(restir_layout_even(width, height, tiles_x, tiles_y, &L));
+    return restir_halo_begin_layout(c, cam, features, &L, rank, prev, send_bytes, recv_bytes);
+}
+
+restir_status restir_halo_begin_layout(restir_ctx* c, const restir_camera* cam, const restir_features* features,
+                                       const restir_tile_layout* layout, uint32_t rank, const restir_frame* prev,
+                                       uint64_t* send_bytes, uint64_t* recv_bytes) {
     if (!c || !cam) return fail(RESTIR_ERR_INVALID, "null argument");
     ST_TRY(check_features(features));
+    ST_TRY(layout_check(layout));
     std::lock_guard<std::mutex> lk(c->mu);
     if (!c->has_scene) return fail(RESTIR_ERR_STATE, "restir_halo_begin before restir_set_scene");
     HIP_TRY(hipSetDevice(c->device));
     const FeaturesDev f = to_dev(features);
     const uint32_t passes = features->spatial_reuse ? features->spatial_resampling_passes : 0u;
+    const uint32_t width = layout->global_width, height = layout->global_height;
+    const uint32_t tiles_x = layout->tiles_x, tiles_y = layout->tiles_y;
     restir_tile t{};
-    ST_TRY(restir_tile_plan(width, height, tiles_x, tiles_y, rank, passes ? f.R : 0u, &t));
+    ST_TRY(restir_layout_tile(layout, rank, passes ? f.R : 0u, &t));
     // plan into locals, validate everything, then commit to c->halo (a failure leaves no half-updated plan)
     restir_halo_segment sg[RESTIR_MAX_HALO_SEGS], rg_[RESTIR_MAX_HALO_SEGS];
     uint32_t n = 0;
@@ -1851,7 +2066,7 @@ restir_status restir_halo_begin(restir_ctx* c, const restir_camera* cam, const r
     uint64_t send_b = 0, recv_b = 0;
     if (passes) {   // no spatial pass, no exchange: skip the plan (and its segment cap)
         n = RESTIR_MAX_HALO_SEGS;
-        ST_TRY(restir_halo_plan(width, height, tiles_x, tiles_y, rank, f.R, f.N, sg, rg_, &n));
+        ST_TRY(restir_layout_halo_plan(layout, rank, f.R, f.N, sg, rg_, &n));
         ST_TRY(to_segs(sg, n, send, send_b));
         ST_TRY(to_segs(rg_, n, recv, recv_b));
     }

@@ -24,18 +24,22 @@ class HaloFrames:
     communicator's rank and size match the tile plan.  bench.py --mode halo --halo-transport native selects it."""
 
     def __init__(self, renderer: "restir.Renderer", width: int, height: int, tiles: tuple, rank: int, features,
-                 group=None, transport: str | None = None):
+                 group=None, transport: str | None = None, layout=None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
         self.r = renderer
         self.W, self.H, self.tiles, self.rank, self.f = width, height, tuple(tiles), rank, features
         self.group = group
+        # layout: an uneven tile layout (restir.layout_balanced; every rank must pass the same one), else the even split
+        if layout is not None and (layout.tiles_x, layout.tiles_y) != self.tiles:
+            raise ValueError(f"HaloFrames: a {layout.tiles_x}x{layout.tiles_y} layout for {tiles[0]}x{tiles[1]} tiles")
+        self.layout = layout
         self.passes = features.spatial_resampling_passes if features.spatial_reuse else 0
         radius = features.spatial_resample_radius
-        self.tile = restir.tile_plan(width, height, tiles[0], tiles[1], rank, radius if self.passes else 0)
+        self.tile = restir.tile_plan(width, height, tiles[0], tiles[1], rank, radius if self.passes else 0, layout=layout)
         self.send, self.recv = restir.halo_plan(width, height, tiles[0], tiles[1], rank, radius,
-                                                features.num_samples_in_reservoir)
+                                                features.num_samples_in_reservoir, layout=layout)
         if dist.get_rank(group) != rank or dist.get_world_size(group) != tiles[0] * tiles[1]:
             raise ValueError(f"HaloFrames: rank {rank} of a {tiles[0]}x{tiles[1]} tile plan, but the group's rank is "
                              f"{dist.get_rank(group)} of {dist.get_world_size(group)}: the halo peers are tile ranks")
@@ -103,7 +107,7 @@ class HaloFrames:
 
     def render(self, prev, camera, want_rgb: bool = True, want_grid: bool = True):
         """One frame: (rgb of the owned tile [h][w][3], row 0 = top, or None; ReservoirGrid for temporal reuse)."""
-        sb, rb = self.r.halo_begin(prev, camera, self.W, self.H, self.f, self.tiles, self.rank)
+        sb, rb = self.r.halo_begin(prev, camera, self.W, self.H, self.f, self.tiles, self.rank, layout=self.layout)
         if self.transport in ("native", "record"):
             for _ in range(self.passes):
                 self.r.halo_pass()

@@ -116,12 +116,18 @@ class Renderer:
         return rgb
 
     # ---- halo-mode frames (include/restir_c.h "halo-mode frames") -------------------------------------
-    def halo_begin(self, prev, camera, width, height, features, tiles, rank):
-        """Primary rays on the tile + ring, RIS / temporal on the owned tile.  Returns (send_bytes, recv_bytes)."""
+    def halo_begin(self, prev, camera, width, height, features, tiles, rank, layout=None):
+        """Primary rays on the tile + ring, RIS / temporal on the owned tile.  Returns (send_bytes, recv_bytes).
+        layout: an uneven restir_tile_layout (layout_balanced) instead of the even tiles split."""
         sb, rb_ = C.c_uint64(), C.c_uint64()
-        check(self.lib, self.lib.restir_halo_begin(self.ctx, C.byref(camera), C.byref(features), width, height, tiles[0],
-                                                   tiles[1], rank, prev.handle if prev is not None else None,
-                                                   C.byref(sb), C.byref(rb_)), "restir_halo_begin")
+        ph = prev.handle if prev is not None else None
+        if layout is not None:
+            check(self.lib, self.lib.restir_halo_begin_layout(self.ctx, C.byref(camera), C.byref(features), C.byref(layout),
+                                                              rank, ph, C.byref(sb), C.byref(rb_)), "restir_halo_begin_layout")
+        else:
+            check(self.lib, self.lib.restir_halo_begin(self.ctx, C.byref(camera), C.byref(features), width, height,
+                                                       tiles[0], tiles[1], rank, ph, C.byref(sb), C.byref(rb_)),
+                  "restir_halo_begin")
         return sb.value, rb_.value
 
     def halo_pack(self, buf_ptr: int, nbytes: int, host: bool) -> None:
@@ -180,6 +186,13 @@ class Renderer:
         check(self.lib, self.lib.restir_measure_read_bandwidth(self.ctx, int(nbytes), int(iters), C.byref(out)),
               "restir_measure_read_bandwidth")
         return out.value
+
+    def background_pixels(self) -> tuple[int, int]:
+        """(background, computed) pixels of the last render_restir frame (restir_background_pixels): the pixels of its
+        RIS tiles flagged all-miss, which the spatial passes and final shading write without reading."""
+        bg, px = C.c_uint64(), C.c_uint64()
+        check(self.lib, self.lib.restir_background_pixels(self.ctx, C.byref(bg), C.byref(px)), "restir_background_pixels")
+        return int(bg.value), int(px.value)
 
     # ---- timing ---------------------------------------------------------------------------------------
     def enable_timing(self, on: bool = True) -> None:
@@ -324,31 +337,79 @@ def rccl_unique_id() -> bytes:
     return buf.raw
 
 
-def halo_plan(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, radius: int, N: int):
-    """restir_halo_plan: ([send segments], [recv segments]) for `rank`, one pair per adjacent rank."""
+def halo_plan(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, radius: int, N: int, layout=None):
+    """restir_halo_plan: ([send segments], [recv segments]) for `rank`, one pair per adjacent rank (layout: an
+    uneven restir_tile_layout instead of the even tiles_x x tiles_y split)."""
     lib = _abi.load_library()
     send = (_abi.HaloSegment * 8)()
     recv = (_abi.HaloSegment * 8)()
     n = C.c_uint32(8)
-    check(lib, lib.restir_halo_plan(width, height, tiles_x, tiles_y, rank, radius, N, send, recv, C.byref(n)),
-          "restir_halo_plan")
+    if layout is not None:
+        check(lib, lib.restir_layout_halo_plan(C.byref(layout), rank, radius, N, send, recv, C.byref(n)),
+              "restir_layout_halo_plan")
+    else:
+        check(lib, lib.restir_halo_plan(width, height, tiles_x, tiles_y, rank, radius, N, send, recv, C.byref(n)),
+              "restir_halo_plan")
     return list(send[:n.value]), list(recv[:n.value])
 
 
-def halo_ops(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, radius: int, N: int) -> list:
+def halo_ops(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, radius: int, N: int, layout=None) -> list:
     """restir_halo_ops: the sends / receives restir_halo_pass posts per spatial pass, in posting order."""
     lib = _abi.load_library()
     ops = (_abi.HaloOp * 16)()
     n = C.c_uint32(16)
-    check(lib, lib.restir_halo_ops(width, height, tiles_x, tiles_y, rank, radius, N, ops, C.byref(n)), "restir_halo_ops")
+    if layout is not None:
+        check(lib, lib.restir_layout_halo_ops(C.byref(layout), rank, radius, N, ops, C.byref(n)), "restir_layout_halo_ops")
+    else:
+        check(lib, lib.restir_halo_ops(width, height, tiles_x, tiles_y, rank, radius, N, ops, C.byref(n)),
+              "restir_halo_ops")
     return list(ops[:n.value])
 
 
-def tile_plan(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, ghost: int) -> _abi.Tile:
+def tile_plan(width: int, height: int, tiles_x: int, tiles_y: int, rank: int, ghost: int, layout=None) -> _abi.Tile:
     lib = _abi.load_library()
     t = _abi.Tile()
-    check(lib, lib.restir_tile_plan(width, height, tiles_x, tiles_y, rank, ghost, C.byref(t)), "restir_tile_plan")
+    if layout is not None:
+        check(lib, lib.restir_layout_tile(C.byref(layout), rank, ghost, C.byref(t)), "restir_layout_tile")
+    else:
+        check(lib, lib.restir_tile_plan(width, height, tiles_x, tiles_y, rank, ghost, C.byref(t)), "restir_tile_plan")
     return t
+
+
+def layout_even(width: int, height: int, tiles_x: int, tiles_y: int) -> _abi.TileLayout:
+    """restir_layout_even: restir_tile_plan's even split as a layout."""
+    lib = _abi.load_library()
+    L = _abi.TileLayout()
+    check(lib, lib.restir_layout_even(width, height, tiles_x, tiles_y, C.byref(L)), "restir_layout_even")
+    return L
+
+
+def _cost_arg(cost):
+    c = np.ascontiguousarray(cost, dtype=np.float32)
+    if c.ndim != 2:
+        raise ValueError("cost grid must be 2-D [rows (row 0 = bottom)][columns]")
+    return c, c.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def layout_balanced(width: int, height: int, tiles_x: int, tiles_y: int, cost, align=(32, 8)):
+    """restir_layout_balanced: (layout, implied efficiency) balancing the cost grid [rows][cols] (row 0 = bottom)."""
+    lib = _abi.load_library()
+    c, ptr = _cost_arg(cost)
+    L = _abi.TileLayout()
+    eff = C.c_double()
+    check(lib, lib.restir_layout_balanced(width, height, tiles_x, tiles_y, ptr, c.shape[1], c.shape[0], align[0], align[1],
+                                          C.byref(L), C.byref(eff)), "restir_layout_balanced")
+    return L, eff.value
+
+
+def layout_shares(layout, cost) -> np.ndarray:
+    """restir_layout_shares: each rank's share of the cost grid under `layout` (sums to 1)."""
+    lib = _abi.load_library()
+    c, ptr = _cost_arg(cost)
+    out = np.zeros(layout.tiles_x * layout.tiles_y, np.float64)
+    check(lib, lib.restir_layout_shares(C.byref(layout), ptr, c.shape[1], c.shape[0],
+                                        out.ctypes.data_as(C.POINTER(C.c_double))), "restir_layout_shares")
+    return out
 
 
 def tile_grid(n: int) -> tuple:

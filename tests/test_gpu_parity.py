@@ -470,39 +470,60 @@ def test_odd_sizes_and_extremes_match_oracle(gpu, oracle, w, h, N, passes, M):
 
 
 @pytest.mark.parametrize("records,fuse,N,variant", [(0, 1, 1, ""), (0, 1, 1, "rescene"), (0, 1, 1, "nohandles"),
-                                                    (1, 1, 1, ""), (0, 0, 1, ""), (0, 1, 2, ""), (0, 0, 2, "")])
+                                                    (1, 1, 1, ""), (0, 0, 1, ""), (0, 1, 2, ""), (0, 0, 2, ""),
+                                                    (0, 1, 1, "moving"), (0, 1, 1, "moving_ragged"), (0, 1, 2, "moving_ragged"),
+                                                    (0, 1, 1, "mbound_in"), (0, 1, 1, "mbound_out")])
 def test_temporal_sequence_matches_oracle(gpu, oracle, records, fuse, N, variant):
     """C3-style: 4 static frames, temporal reuse threading the previous frame's grid (main.cpp:165); both frame
     buffer layouts (SoA planes, per-pixel records); temporal reuse fused into the primary + RIS kernel (fuse.temporal,
     the default for point lights) and as its own pass; N = 1 and 2.  N = 1 fused: the predecessor is rebuilt from the
     frame handles its last pass wrote and the passes read sample handles; "rescene" re-uploads the scene mid-sequence
-    (the handles' light table is stale: the reservoir planes are read), "nohandles" turns the handle passes off."""
+    (the handles' light table is stale: the reservoir planes are read), "nohandles" turns the handle passes off.
+    "moving" / "moving_ragged" pan the camera between frames (96 x 64 and a 37 x 23 frame that is no multiple of the 32 x 8
+    / 32 x 16 tiles, clampM = 1): RIS tiles whose every pixel misses now while the predecessor held real lights there, so
+    the fused kernel rebuilds those predecessors from its light table (the table must be staged for such
+    tiles too).  "mbound_in" / "mbound_out": 5 and 6 passes at clampM = 20, the last M bound (M + clampM M + 1)(K + 1)^P
+    that fits the handles' 24 bits and the first that does not (frame handles on / reservoir planes)."""
     gpu.set_tuning("layout.records", records)
     gpu.set_tuning("fuse.temporal", fuse)
     if variant == "nohandles":
         gpu.set_tuning("spatial.handles", 0)
     try:
-        _temporal_sequence(gpu, oracle, N, rescene=variant == "rescene")
+        if variant.startswith("moving"):
+            w, h = (37, 23) if variant == "moving_ragged" else (W, H)
+            _temporal_sequence(gpu, oracle, N, w=w, h=h, moving=True, clamp=1)
+        elif variant.startswith("mbound"):
+            _temporal_sequence(gpu, oracle, N, passes=5 if variant == "mbound_in" else 6, clamp=20)
+        else:
+            _temporal_sequence(gpu, oracle, N, rescene=variant == "rescene")
     finally:
         gpu.set_tuning("layout.records", 0)
         gpu.set_tuning("fuse.temporal", 1)
         gpu.set_tuning("spatial.handles", 1)
 
 
-def _temporal_sequence(gpu, oracle, N=1, rescene=False):
+# a camera panning across the nightclub (lookAt offsets per frame): 40-80 % of the pixels change from hit to miss or back
+_PAN = [(0.0, 0.0), (9.0, 4.0), (3.0, -2.0), (12.0, 6.0)]
+
+
+def _temporal_sequence(gpu, oracle, N=1, rescene=False, w=W, h=H, moving=False, clamp=20, passes=2):
     name = "nightclub_128pt"
     s = get_scene(name)
     gpu.set_scene(s)
     osc = oracle.OracleScene(s)
-    cam = scene.camera_for(name, W, H)
-    f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=2, temporal_reuse=1)
+    cam = scene.camera_for(name, w, h)
+    f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=passes, temporal_reuse=1,
+                              temporal_clamp_m=clamp)
     gpu.set_seed(SEED, 0)
     prev_gpu, prev_or = None, None
     for frame in range(4):
         if rescene and frame == 2:
             gpu.set_scene(s)   # a new upload: the predecessor's frame handles name the old one (reservoir planes read)
-        rgb, grid = gpu.render_restir(prev_gpu, cam, W, H, f)
-        want, res, _ = oracle.render_frame(osc, cam, f, W, H, SEED, frame, prev=prev_or)
+        if moving:
+            dx, dy = _PAN[frame]
+            cam = scene.make_camera(30.0, 25.0, (2.57 + dx, 1.23 + dy, -1.35), (10.3, 30.0, 0.0), w, h)
+        rgb, grid = gpu.render_restir(prev_gpu, cam, w, h, f)
+        want, res, _ = oracle.render_frame(osc, cam, f, w, h, SEED, frame, prev=prev_or)
         assert_bits(rgb, want, f"frame {frame} rgb")
         assert_grid(grid, res, f"frame {frame}")
         prev_gpu, prev_or = grid, res

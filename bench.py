@@ -74,6 +74,12 @@ def parse():
     ap.add_argument("--halo-transport", default="auto", choices=["auto", "native", "torch"],
                     help="halo transport: the library's own RCCL communicator (native), torch.distributed p2p (torch); "
                          "auto = native under nccl, torch under gloo")
+    ap.add_argument("--layout", default="auto", choices=["auto", "even", "balanced"],
+                    help="N > 1 tile layout: even cuts, or cost-balanced cuts from a low-resolution primary pass "
+                         "(restir_layout_balanced, broadcast from rank 0); auto = balanced for the strong-scaling "
+                         "configs (c4 / c5: one image split over the ranks), even for weak-scaling c2 / c3")
+    ap.add_argument("--layout-rounds", type=int, default=3,
+                    help="balanced layout: rounds of refinement from the ranks' measured tile frame times")
     ap.add_argument("--prewarm-gemm-ms", type=float, default=500.0,
                     help="GPU clock pre-warm before the warm-up frames (not frames, not timed): fp32 GEMMs through torch "
                          "for this long.  An idle box's first ~40 frames run up to 10 %% slower (profiles/r4/gap); 500 ms "
@@ -443,7 +449,8 @@ def select_halo(torch, world, local, backend, transport, make, check):
     return hf, rec, bad
 
 
-def halo_frames(torch, r, rank, world, local, f, cam, GW, GH, tx, ty, passes, args, transport, check_on, fatal=True):
+def halo_frames(torch, r, rank, world, local, f, cam, GW, GH, tx, ty, passes, args, transport, check_on, fatal=True,
+                layout=None):
     """N > 1 with spatial passes: this rank's tile rendered through the reservoir halo exchange (HaloFrames: interior
     launched while the border reservoirs move, border strips after) must equal, bit for bit, the same tile rendered
     with a ghost zone (restir_render on tile + passes * r) -- exits 3 on any mismatch (check_on).  Then the halo-mode
@@ -458,14 +465,14 @@ def halo_frames(torch, r, rank, world, local, f, cam, GW, GH, tx, ty, passes, ar
     ghost = {}
 
     def make(tr):
-        return distributed.HaloFrames(r, GW, GH, (tx, ty), rank, f, transport=tr)
+        return distributed.HaloFrames(r, GW, GH, (tx, ty), rank, f, transport=tr, layout=layout)
 
     def check(hf):
         if not check_on:
             return 0
         if "rgb" not in ghost:
             r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
-            ghost_tile = restir.tile_plan(GW, GH, tx, ty, rank, passes * args.r)
+            ghost_tile = restir.tile_plan(GW, GH, tx, ty, rank, passes * args.r, layout=layout)
             ghost["rgb"], _ = r.render_restir(None, cam, GW, GH, fc, tile=ghost_tile, want_grid=False)
         r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
         f0 = hf.f
@@ -543,13 +550,35 @@ def main():
                               temporal_reuse=cf["temporal"], unbiased_combination=cf["unbiased"],
                               spatial_reuse_visibility_check=cf["vis"])
     ghost = passes * args.r
-    tile = restir.tile_plan(GW, GH, tx, ty, rank, ghost)
 
     r = restir.Renderer(local)
     for kv in args.tune:
         key, val = kv.split("=", 1)
         r.set_tuning(key, int(val))
     r.set_scene(sc)
+    # the tile layout: a strong-scaling frame's geometry is not spread evenly (C4 / C5's TOML camera: the box fills the
+    # middle of the frame), so its cuts follow a cost grid measured once per camera on rank 0 and broadcast
+    layout, layout_rec = None, None
+    use_balanced = args.layout == "balanced" or (args.layout == "auto" and scaling == "strong")
+    if world > 1 and use_balanced:
+        from romis_amd import distributed
+
+        def time_tile(L):   # this rank's frame on its tile of L (ghost-zone frames: the tile's kernels, no exchange)
+            gt = restir.tile_plan(GW, GH, tx, ty, rank, ghost, layout=L)
+            fc = _abi.Features.from_buffer_copy(f)
+            fc.temporal_reuse = 0
+            r.render_restir(None, cam, GW, GH, fc, tile=gt, want_rgb=False, want_grid=False)
+            r.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                r.render_restir(None, cam, GW, GH, fc, tile=gt, want_rgb=False, want_grid=False)
+            r.synchronize()
+            return (time.perf_counter() - t0) / 3
+
+        layout, layout_rec = distributed.balanced_layout(
+            r, lambda w, h: scene.camera_for(cf["scene"], w, h, cf.get("camera")), GW, GH, (tx, ty),
+            time_tile=time_tile, rounds=args.layout_rounds)
+    tile = restir.tile_plan(GW, GH, tx, ty, rank, ghost, layout=layout)
     r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
     state = {"grid": None}
     transport = args.halo_transport
@@ -561,7 +590,7 @@ def main():
     if halo or check_on:
         # one HaloFrames per run, chosen and verified by halo_frames (select_halo); the halo-mode loop times it
         hf_checked, halo_rec = halo_frames(torch, r, rank, world, local, f, cam, GW, GH, tx, ty, passes, args, transport,
-                                           check_on, fatal=halo)
+                                           check_on, fatal=halo, layout=layout)
         r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
         if halo:
             hf = hf_checked
@@ -613,6 +642,16 @@ def main():
     r.enable_timing(False)
     kt_all = r.timings()
     bg_info = r.background_pixels()
+    # per-rank GPU kernel time per frame of that run (the balance of the tile layout, measured): gathered to rank 0
+    n_kf = max(1, min(args.steps, 20))
+    busy_ms = sum(v[0] for v in kt_all.values()) / n_kf
+    rank_busy = [busy_ms]
+    if world > 1:
+        on_gpu = torch.distributed.get_backend() == "nccl"
+        bt = torch.tensor([busy_ms], dtype=torch.float64, device=torch.device("cuda", local) if on_gpu else "cpu")
+        outs = [torch.zeros_like(bt) for _ in range(world)]
+        torch.distributed.all_gather(outs, bt)
+        rank_busy = [float(o.item()) for o in outs]
     state["grid"] = None
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -623,7 +662,12 @@ def main():
            "tile": [tile.width, tile.height] if scaling == "strong" else [GW // tx, GH // ty], "image": [GW, GH],
            "tiles": [tx, ty], "M": cf["M"], "N": args.N, "k": args.k, "r": args.r, "passes": passes,
            "temporal": cf["temporal"], "unbiased": cf["unbiased"], "spatial_visibility": cf["vis"],
-           "parallelism": f"screen tiles {tx}x{ty}, " + (f"RCCL reservoir halo {args.r}px" if halo else f"ghost {ghost}px")}
+           "parallelism": f"screen tiles {tx}x{ty}" + (" cost-balanced" if layout is not None else "") + ", " +
+                          (f"RCCL reservoir halo {args.r}px" if halo else f"ghost {ghost}px")}
+    if layout_rec is not None:
+        # this rank's share and the spread over ranks of the measured per-rank frame times (max over ranks is `value`)
+        layout_rec["owned"] = [tile.x0, tile.y0, tile.width, tile.height]
+        cfg["layout"] = layout_rec
     if cf.get("camera"):
         cfg["camera"] = camera_record(cf["camera"])
 
@@ -743,6 +787,11 @@ def main():
             "cpu_baseline": cpu,
             "kernels": kernels,
         }
+        if world > 1:
+            out["balance"] = {"kernel_ms_per_frame_per_rank": [round(v, 4) for v in rank_busy],
+                              "efficiency": round(float(np.mean(rank_busy) / max(rank_busy)), 4) if max(rank_busy) > 0 else None,
+                              "note": "GPU kernel time per frame on each rank (HIP events, the per-kernel run): mean / max "
+                                      "is the tile layout's balance, halo transfers excluded"}
         if halo_rec is not None:
             out["halo"] = halo_rec
         if halo_failed:   # a non-fatal halo check that failed still fails the run (after the record)

@@ -272,6 +272,7 @@ struct restir_ctx {
         bool rp_ok = false;          // the current grid's target-pdf cache is valid (restir_render's rp_ok)
         bool interior_done = false;  // the current pass's interior launch is issued (restir_halo_spatial_interior)
         bool part_rp = false;        // every launch of the current pass wrote the pdf cache
+        uint8_t* tmiss = nullptr;    // the view's background-tile flags (fused RIS over the view, no temporal reuse)
     } halo;
     DevBuf halo_scratch;
     // record-only restir_halo_pass (restir_halo_record): the steps it issues, no RCCL call
@@ -2106,11 +2107,32 @@ restir_status restir_halo_begin_layout(restir_ctx* c, const restir_camera* cam, 
     SceneDev s;
     ST_TRY(scene_for(c, f, (size_t)t.gwidth * t.gheight, s));
     float4* pm = c->p_mat.as<float4>();
-    // G-buffer on the whole view (the spatial passes read the neighbours' depth / normal / position),
-    // reservoirs only on the owned rectangle
-    TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, h.view, h.camd, fb.nt(0), pm, fb.nt2(), c->tuning, c->stream));
-    TIMED(c, RESTIR_K_RIS, launch_ris(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_RIS, 0), h.camd.origin,
-                                      fb.nt(0), pm, fb.ra(0), fb.rb(0), nullptr, fb.rp(0), c->tuning, c->stream));
+    // G-buffer on the whole view (the spatial passes read the neighbours' depth / normal / position).  Without temporal
+    // reuse: restir_render's fused primary + RIS kernel over the whole view, with its background-tile flags (the ring's
+    // RIS results are the ones its owner computes -- same G-buffer, same global-pixel keys -- and the exchange before
+    // the first pass overwrites them with those same values), so the passes and final shading write background tiles
+    // without reading them; the ring's RIS costs (ring / tile) of the RIS time.  Otherwise primary rays on the view
+    // and RIS / temporal reuse on the owned rectangle.
+    const bool fused = !temporal && c->tuning.fuse_primary_ris && primary_ris_fits(s);
+    h.tmiss = nullptr;
+    if (fused) {
+        uint8_t* tm = nullptr;
+        if (c->tuning.miss_tiles && f.N <= 2 && s.normals_bounded && !fb.records) {
+            const size_t tiles = (size_t)((t.gwidth + 31u) / 32u) * ((t.gheight + 7u) / 8u);
+            ST_TRY(c->tmiss.ensure((tiles + 3u) & ~(size_t)3u));   // whole words (the spatial pass reads its flag's word)
+            tm = c->tmiss.as<uint8_t>();
+        }
+        bool written = false;
+        TIMED(c, RESTIR_K_PRIMARY_RIS,
+              launch_primary_ris(s, h.view, h.camd, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_RIS, 0), fb.nt(0), pm,
+                                 fb.nt2(), fb.ra(0), fb.rb(0), nullptr, fb.rp(0), c->tuning, c->stream, tm, 0u, &written));
+        if (written) h.tmiss = tm;
+    } else {
+        TIMED(c, RESTIR_K_PRIMARY, launch_primary(s, h.view, h.camd, fb.nt(0), pm, fb.nt2(), c->tuning, c->stream));
+        TIMED(c, RESTIR_K_RIS, launch_ris(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_RIS, 0),
+                                          h.camd.origin, fb.nt(0), pm, fb.ra(0), fb.rb(0), nullptr, fb.rp(0), c->tuning,
+                                          c->stream));
+    }
     if (temporal)
         TIMED(c, RESTIR_K_TEMPORAL,
               launch_temporal(s, h.owned, f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_TEMPORAL, 0), h.camd.origin, fb.nt(0),
@@ -2203,7 +2225,10 @@ static restir_status halo_spatial_part(restir_ctx* c, const Region& rg, bool int
           launch_spatial(sd, rg, h.f, restir_rng_key(c->seed, h.frame, RESTIR_STAGE_SPATIAL, h.pass), h.camd.origin,
                          fb.nt(h.cur), c->p_mat.as<float4>(), fb.ra(h.cur), fb.rb(h.cur), fb.ra(nxt), fb.rb(nxt), nullptr,
                          h.rp_ok ? fb.rp(h.cur) : nullptr, h.rp_ok && interior ? fb.rp(h.cur) : nullptr, fb.rp(nxt),
-                         &wrote, c->tuning, c->stream));
+                         &wrote, c->tuning, c->stream, nullptr, nullptr,
+                         // background tiles (restir_render's MissTiles): every ring pixel holds its owner's value, which
+                         // for a background tile is the known one
+                         MissTiles{h.tmiss, (!h.f.unbiased || h.pass == 0) ? h.f.M : 0u, 0u}));
     rp_written = rp_written && wrote;
     return RESTIR_OK;
 }
@@ -2505,7 +2530,8 @@ restir_status restir_halo_end(restir_ctx* c, restir_frame** out_next, float* out
     SceneDev sd;
     ST_TRY(scene_for(c, h.f, (size_t)h.view.vw * h.view.vh, sd));
     TIMED(c, RESTIR_K_FINAL, launch_final(sd, h.owned, h.f, h.camd.origin, fb.nt(h.cur), c->p_mat.as<float4>(),
-                                          fb.ra(h.cur), fb.rb(h.cur), c->rgb.as<float>(), c->tuning, c->stream));
+                                          fb.ra(h.cur), fb.rb(h.cur), c->rgb.as<float>(), c->tuning, c->stream, nullptr,
+                                          MissTiles{h.tmiss, 0u, 0u}));
     c->cur = h.cur;
     h.active = false;
     if (out_next) {

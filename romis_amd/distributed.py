@@ -122,6 +122,130 @@ class HaloFrames:
         return self.r.halo_end(self.tile, want_rgb, want_grid)
 
 
+# Cost-balanced screen tiles.  A frame's time on a rank follows its geometry pixels (a background
+# pixel misses the scene: its RIS, spatial and shading work is a shortcut); the weight of a background pixel relative
+# to a geometry pixel in halo-mode frames is measured in profiles/r6/balance.json (scripts/balance_measure.py).
+COST_GRID = (480, 270)       # cost cells over the image (4K: 8 x 8 px, 8K: 16 x 16 px)
+BACKGROUND_WEIGHT = 0.1      # cost of a background pixel / a geometry pixel (profiles/r6/balance.json fit)
+LAYOUT_ALIGN = (32, 8)       # cut granularity: whole 32-px tile columns, 8-px tile rows
+
+
+def geometry_cost(renderer: "restir.Renderer", camera_fn, width: int, height: int, grid=COST_GRID,
+                  background=BACKGROUND_WEIGHT):
+    """The cost grid [rows (row 0 = bottom)][cols] of a width x height frame: one primary ray per cell through the
+    library's own primary-ray kernel (restir_stage_primary over a grid-sized image with the same camera framing,
+    camera_fn(w, h)), 1 where it hits the scene, `background` where it misses."""
+    import numpy as np
+    gw, gh = min(grid[0], width), min(grid[1], height)
+    renderer.stage_configure(gw, gh, 1)
+    renderer.stage_primary(camera_fn(gw, gh))
+    n_t = renderer.download(restir._abi.BUF_GBUF_N_T)
+    hit = (n_t[:, 3] < 1e30).reshape(gh, gw)   # t = FLT_MAX on a miss
+    return np.where(hit, np.float32(1.0), np.float32(background)).astype(np.float32)
+
+
+def cell_owners(layout, cost_shape):
+    """[rows][cols] rank owning each cost cell's centre under `layout` (cell (i, j) as restir_layout_balanced maps it)."""
+    import numpy as np
+    ch, cw = cost_shape
+    W, H = layout.global_width, layout.global_height
+    cx = ((np.arange(cw) + 0.5) * W / cw).astype(np.int64)
+    cy = ((np.arange(ch) + 0.5) * H / ch).astype(np.int64)
+    xc = np.asarray(list(layout.x_cuts[:layout.tiles_x + 1]))
+    col = np.clip(np.searchsorted(xc, cx, side="right") - 1, 0, layout.tiles_x - 1)
+    own = np.zeros((ch, cw), np.int64)
+    for i in range(cw):
+        yc = np.asarray(list(layout.y_cuts[col[i]][:layout.tiles_y + 1]))
+        row = np.clip(np.searchsorted(yc, cy, side="right") - 1, 0, layout.tiles_y - 1)
+        own[:, i] = row * layout.tiles_x + col[i]
+    return own
+
+
+def refine_cost(cost, layout, rank_seconds):
+    """The cost grid corrected by measured per-rank frame times under `layout`: every cell a rank owns is scaled by
+    (the rank's share of the measured time) / (its share of the modelled cost), so that a rank whose pixels proved
+    dearer than the model (specular materials, occluded lights, the visibility pass's rays) weighs more in the next
+    cut.  Results do not depend on the layout (any layout is bit-identical); only the balance does."""
+    import numpy as np
+    t = np.asarray(rank_seconds, np.float64)
+    share_t = t / t.sum()
+    share_c = restir.layout_shares(layout, cost)
+    scale = np.where(share_c > 0, share_t / np.maximum(share_c, 1e-12), 1.0)
+    out = cost.astype(np.float64) * scale[cell_owners(layout, cost.shape)]
+    return (out / out.mean()).astype(np.float32)
+
+
+def _layout_buf(L, eff):
+    import numpy as np
+    nx, ny = restir._abi.RESTIR_MAX_TILES_X + 1, restir._abi.RESTIR_MAX_TILES_Y + 1
+    buf = np.zeros(nx + restir._abi.RESTIR_MAX_TILES_X * ny + 1, np.int64)
+    buf[:nx] = list(L.x_cuts)
+    buf[nx:-1] = np.asarray([list(r) for r in L.y_cuts], np.int64).reshape(-1)
+    buf[-1] = int(round(eff * 1e6))
+    return buf
+
+
+def _layout_from_buf(buf, width, height, tiles):
+    nx, ny = restir._abi.RESTIR_MAX_TILES_X + 1, restir._abi.RESTIR_MAX_TILES_Y + 1
+    L = restir._abi.TileLayout()
+    L.global_width, L.global_height, L.tiles_x, L.tiles_y = width, height, tiles[0], tiles[1]
+    for i in range(nx):
+        L.x_cuts[i] = int(buf[i])
+    yc = buf[nx:-1].reshape(restir._abi.RESTIR_MAX_TILES_X, ny)
+    for c in range(restir._abi.RESTIR_MAX_TILES_X):
+        for i in range(ny):
+            L.y_cuts[c][i] = int(yc[c, i])
+    return L, float(buf[-1]) / 1e6
+
+
+def balanced_layout(renderer: "restir.Renderer", camera_fn, width: int, height: int, tiles: tuple, group=None,
+                    align=LAYOUT_ALIGN, time_tile=None, rounds: int = 3):
+    """(layout, record): rank 0 of the group measures the geometry (geometry_cost) and cuts the tiles
+    (restir_layout_balanced); the cuts are broadcast, so every rank holds the same layout (once per camera).
+    time_tile(layout) -> this rank's frame seconds on its tile of `layout`: then `rounds` rounds of measured
+    refinement follow (refine_cost on rank 0 from the gathered times, new cuts broadcast)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    multi = dist.is_initialized() and dist.get_world_size(group) > 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    dev = torch.device("cuda", torch.cuda.current_device()) if multi and dist.get_backend(group) == "nccl" else "cpu"
+    src = (dist.get_global_rank(group, 0) if group is not None else 0) if multi else 0
+
+    def share(buf):
+        if multi:
+            t = torch.from_numpy(buf).to(dev)
+            dist.broadcast(t, src=src, group=group)
+            buf = t.cpu().numpy()
+        return _layout_from_buf(buf, width, height, tiles)
+
+    cost = None
+    buf = np.zeros(restir._abi.RESTIR_MAX_TILES_X + 1 + restir._abi.RESTIR_MAX_TILES_X * (restir._abi.RESTIR_MAX_TILES_Y + 1)
+                   + 1, np.int64)
+    if rank == 0:
+        cost = geometry_cost(renderer, camera_fn, width, height)
+        buf = _layout_buf(*restir.layout_balanced(width, height, tiles[0], tiles[1], cost, align))
+    L, eff = share(buf)
+    rec = {"kind": "cost-balanced (restir_layout_balanced)", "model_efficiency": round(eff, 4),
+           "cost_grid": list(COST_GRID), "background_weight": BACKGROUND_WEIGHT, "align": list(align), "refinement": []}
+    for _ in range(rounds if time_tile is not None else 0):
+        mine = float(time_tile(L))
+        times = [mine]
+        if multi:
+            t = torch.tensor([mine], dtype=torch.float64, device=dev)
+            outs = [torch.zeros_like(t) for _ in range(dist.get_world_size(group))]
+            dist.all_gather(outs, t, group=group)
+            times = [float(o.item()) for o in outs]
+        rec["refinement"].append({"cuts": L.cuts(), "rank_ms": [round(v * 1e3, 4) for v in times],
+                                  "measured_efficiency": round(float(np.mean(times) / max(times)), 4)})
+        if rank == 0:
+            cost = refine_cost(cost, L, times)
+            buf = _layout_buf(*restir.layout_balanced(width, height, tiles[0], tiles[1], cost, align))
+        L, eff = share(buf)
+    rec["cuts"] = L.cuts()
+    return L, rec
+
+
 def tile_mismatches(mine, other, group=None) -> int:
     """Bit-for-bit comparison of two renderings of this rank's tile (float32 arrays of one shape), summed over the
     group's ranks: the number of 32-bit words that differ anywhere (a shape mismatch counts every word)."""

@@ -29,8 +29,14 @@ def _features(passes, N, unbiased=0, vis=0):
                                  unbiased_combination=unbiased, spatial_reuse_visibility_check=vis)
 
 
+# uneven layouts of the 96 x 64 frame (restir_tile_layout); "balanced": distributed.balanced_layout
+# -- the cost grid from the library's primary-ray kernel on rank 0, the cuts broadcast over the group
+UNEVEN = {(4, 2): {"x": [0, 36, 52, 68, 96], "y": [[0, 20, 64], [0, 36, 64], [0, 28, 64], [0, 44, 64]]},
+          (2, 4): {"x": [0, 56, 96], "y": [[0, 10, 30, 44, 64], [0, 18, 32, 50, 64]]}}
+
+
 def _worker(rank, world, port, tiles, passes, N, out_dir, name="nightclub_128pt", records=0, backend="gloo",
-            width=W, height=H, unbiased=0, vis=0):
+            width=W, height=H, unbiased=0, vis=0, layout_kind=None):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from romis_amd import _abi, distributed, restir, scene
@@ -43,7 +49,12 @@ def _worker(rank, world, port, tiles, passes, N, out_dir, name="nightclub_128pt"
     r.set_scene(sc)
     r.set_seed(_abi.RESTIR_DEFAULT_SEED, 0)
     cam = scene.camera_for(name, W, H)
-    hf = distributed.HaloFrames(r, W, H, tiles, rank, _features(passes, N, unbiased, vis))
+    layout = None
+    if layout_kind == "uneven":
+        layout = _abi.TileLayout.from_cuts(W, H, UNEVEN[tuple(tiles)])
+    elif layout_kind == "balanced":
+        layout, _ = distributed.balanced_layout(r, lambda w, h: scene.camera_for(name, w, h), W, H, tiles, align=(8, 8))
+    hf = distributed.HaloFrames(r, W, H, tiles, rank, _features(passes, N, unbiased, vis), layout=layout)
     prev = None
     for fr in range(FRAMES):
         rgb, prev = hf.render(prev, cam)
@@ -88,16 +99,19 @@ def _single_gpu_check(tmp_path, passes, N, name=_DEFAULT_SCENE, records=0, width
 # run the lean N = 1 unbiased pass (k_spatial1u[_vis]), whose Z term reads the pdf cache at neighbour pixels: in a
 # border strip those may lie in the exchanged ring, which carries no cache (restir.cpp halo_spatial_part).
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,tiles,passes,N,name,records,unbiased,vis", [
-    (2, (2, 1), 2, 1, _DEFAULT_SCENE, 0, 0, 0), (4, (2, 2), 2, 1, _DEFAULT_SCENE, 0, 0, 0),
-    (4, (2, 2), 1, 2, _DEFAULT_SCENE, 0, 0, 0),
-    (2, (2, 1), 2, 1, _DEFAULT_SCENE, 1, 0, 0), (4, (2, 2), 1, 2, _DEFAULT_SCENE, 1, 0, 0),
-    (8, (4, 2), 2, 1, "cornell_1024", 0, 0, 0), (8, (8, 1), 1, 1, _DEFAULT_SCENE, 0, 0, 0),
-    (2, (2, 1), 2, 1, _DEFAULT_SCENE, 0, 1, 0), (4, (2, 2), 1, 1, "cornell_1024", 0, 1, 1),
-    (8, (4, 2), 2, 1, "cornell_4096", 0, 1, 1), (4, (2, 2), 1, 2, _DEFAULT_SCENE, 0, 1, 1)])
-def test_halo_frames_match_single_gpu_sequence(tmp_path, world, tiles, passes, N, name, records, unbiased, vis):
+@pytest.mark.parametrize("world,tiles,passes,N,name,records,unbiased,vis,layout_kind", [
+    (2, (2, 1), 2, 1, _DEFAULT_SCENE, 0, 0, 0, None), (4, (2, 2), 2, 1, _DEFAULT_SCENE, 0, 0, 0, None),
+    (4, (2, 2), 1, 2, _DEFAULT_SCENE, 0, 0, 0, None),
+    (2, (2, 1), 2, 1, _DEFAULT_SCENE, 1, 0, 0, None), (4, (2, 2), 1, 2, _DEFAULT_SCENE, 1, 0, 0, None),
+    (8, (4, 2), 2, 1, "cornell_1024", 0, 0, 0, None), (8, (8, 1), 1, 1, _DEFAULT_SCENE, 0, 0, 0, None),
+    (2, (2, 1), 2, 1, _DEFAULT_SCENE, 0, 1, 0, None), (4, (2, 2), 1, 1, "cornell_1024", 0, 1, 1, None),
+    (8, (4, 2), 2, 1, "cornell_4096", 0, 1, 1, None), (4, (2, 2), 1, 2, _DEFAULT_SCENE, 0, 1, 1, None),
+    (8, (4, 2), 2, 1, _DEFAULT_SCENE, 0, 0, 0, "uneven"), (8, (2, 4), 1, 2, "cornell_1024", 0, 0, 0, "uneven"),
+    (8, (4, 2), 1, 1, "cornell_4096", 0, 1, 1, "balanced"), (8, (4, 2), 2, 1, "cornell_1024", 0, 0, 0, "balanced")])
+def test_halo_frames_match_single_gpu_sequence(tmp_path, world, tiles, passes, N, name, records, unbiased, vis,
+                                               layout_kind):
     mp.spawn(_worker, args=(world, _free_port(), tiles, passes, N, str(tmp_path), name, records, "gloo", W, H,
-                            unbiased, vis), nprocs=world, join=True)
+                            unbiased, vis, layout_kind), nprocs=world, join=True)
     _single_gpu_check(tmp_path, passes, N, name, records, unbiased=unbiased, vis=vis)
 
 

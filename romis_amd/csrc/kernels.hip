@@ -1248,7 +1248,7 @@ struct Comb1h {
 // LDS of a handle block: the n_t window, the two handle windows, then the light table (2 (L + 1) float4)
 __host__ __device__ constexpr uint32_t h_lds_f4(uint32_t TH) { return apron_max(TH) + apron_max(TH) / 2u; }
 
-template <uint32_t TH>
+template <uint32_t TH, bool HG = false>
 __device__ __forceinline__ void h_stage(const SceneDev& s, const Region& rg, const float4* __restrict__ n_t, HandlesIn hi,
                                         float4* l_nt, float* l_w, uint32_t* l_m, float4* l_lt, int ax0, int ay0, uint32_t AW,
                                         uint32_t n_apron) {
@@ -1265,10 +1265,12 @@ __device__ __forceinline__ void h_stage(const SceneDev& s, const Region& rg, con
             const uint32_t o = base + r * rg.vw + (i - r * AW);
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(n_t + o),
                                              (__attribute__((address_space(3))) void*)(l_nt + kThreads * k + w64), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(hi.w + o),
-                                             (__attribute__((address_space(3))) void*)(l_w + kThreads * k + w64), 4, 0, 0);
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(hi.m + o),
-                                             (__attribute__((address_space(3))) void*)(l_m + kThreads * k + w64), 4, 0, 0);
+            if (!HG) {
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(hi.w + o),
+                                                 (__attribute__((address_space(3))) void*)(l_w + kThreads * k + w64), 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(hi.m + o),
+                                                 (__attribute__((address_space(3))) void*)(l_m + kThreads * k + w64), 4, 0, 0);
+            }
         }
     }
     // light table: entries d = 0 .. L positions, L + 1 .. 2L + 1 colours (the light_c2 planes); d = L and 2L + 1 are
@@ -1285,7 +1287,10 @@ __device__ __forceinline__ void h_stage(const SceneDev& s, const Region& rg, con
     if (threadIdx.x < 2u) l_lt[threadIdx.x ? 2u * L + 1u : L] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
-template <bool DBG, uint32_t TH = 1>
+// HG (round 6 probe): the handles are gathered from global memory (the own pixel's coalesced, an accepted
+// neighbour's one 4 + 4 B gather) instead of staged in LDS: the block's LDS is the n_t window and the light table only
+// (34 KB at 32 x 16: four blocks of 8 waves per CU instead of three)
+template <bool DBG, uint32_t TH = 1, bool HG = false>
 __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
                                                v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                                HandlesIn hi, float4* __restrict__ oa, float4* __restrict__ ob,
@@ -1296,7 +1301,7 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
     float4* const l_nt = g_lds;
     float* const l_w = reinterpret_cast<float*>(g_lds + apron_max(TH));
     uint32_t* const l_m = reinterpret_cast<uint32_t*>(l_w + apron_max(TH));
-    float4* const l_lt = g_lds + h_lds_f4(TH);
+    float4* const l_lt = g_lds + (HG ? apron_max(TH) : h_lds_f4(TH));
     const uint32_t L = s.num_lights;
     uint32_t tile;
     const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
@@ -1333,6 +1338,8 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
     const uint32_t pix = (uint32_t)(y - (int)rg.vy0) * rg.vw + (uint32_t)(x - (int)rg.vx0);
     float4 cpm = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     float pd_cached = 0.0f;
+    float gw = 0.0f;
+    uint32_t gm = 0u;
     const bool own_bg = live && mixed && tile_flag_at(mt, rg, x, y) == 0u;   // a background RIS tile: known, unread
     if (live) {
         if (own_bg) {
@@ -1340,21 +1347,24 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
         } else {
             cpm = p_mat[pix];
             if (rp_in) pd_cached = rp_in[pix];
+            if (HG) { gw = hi.w[pix]; gm = hi.m[pix]; }
         }
     }
-    h_stage<TH>(s, rg, n_t, hi, l_nt, l_w, l_m, l_lt, ax0, ay0, AW, n_apron);
+    h_stage<TH, HG>(s, rg, n_t, hi, l_nt, l_w, l_m, l_lt, ax0, ay0, AW, n_apron);
     const GlTabs tb = gl_stage_tables_dma();
     const uint32_t K = f.K;   // <= kLeanK (host check)
     const uint32_t ps = pix_state(key, (uint32_t)y * rg.W + (uint32_t)x);
     const uint32_t span = 2u * f.R + 1u;
-    uint32_t qi[kLeanK];
+    uint32_t qi[kLeanK], qp[kLeanK];
 #pragma unroll
     for (uint32_t n = 0; n < kLeanK; n++) {
         qi[n] = 0u;
+        qp[n] = 0u;
         if (n < K) {
             const int nx = min(max(x - R + (int)__umulhi(draw(ps, 2u * n), span), xlo), xhi);
             const int ny = min(max(y - R + (int)__umulhi(draw(ps, 2u * n + 1u), span), ylo), yhi);
             qi[n] = (uint32_t)(ny - ay0) * AW + (uint32_t)(nx - ax0);
+            if (HG) qp[n] = (uint32_t)(ny - (int)rg.vy0) * rg.vw + (uint32_t)(nx - (int)rg.vx0);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's DMA before the barrier (spatial1_ntl_body)
@@ -1375,8 +1385,8 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
     if (!live) return;   // no barrier follows
     const uint32_t own = (uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0);
     const float4 cn = l_nt[own];
-    const float cw = own_bg ? 0.0f : l_w[own];
-    const uint32_t cm = own_bg ? (mt.m | (L << 24)) : l_m[own];
+    const float cw = own_bg ? 0.0f : (HG ? gw : l_w[own]);
+    const uint32_t cm = own_bg ? (mt.m | (L << 24)) : (HG ? gm : l_m[own]);
     const uint32_t cli = cm >> 24;
     const v3 cpos = xyz(l_lt[cli]), ccol = xyz(l_lt[L + 1u + cli]);
     const Px cur = make_px(s, cn, cpm, origin, pix);
@@ -1403,14 +1413,17 @@ __device__ __forceinline__ void spatial1h_body(const SceneDev& s, const Region& 
         qw[n] = 0.0f;
         if (n < K) {
             const float4 g = l_nt[qi[n]];
-            qm[n] = l_m[qi[n]];
-            qw[n] = l_w[qi[n]];
+            if (!HG) {
+                qm[n] = l_m[qi[n]];
+                qw[n] = l_w[qi[n]];
+            }
             const float nd = vdot(xyz(g), cur.N);
             float q = div_by_rcp_d(g.w, rt);
             if (__builtin_expect(!rt_all, 0)) {
                 if (!div_fast_ok(cur.t)) q = g.w / cur.t;
             }
             ok[n] = !(nd < 0.90630778703f) && !(fabsf(1.0f - q) > 0.1f);
+            if (HG && ok[n]) { qm[n] = hi.m[qp[n]]; qw[n] = hi.w[qp[n]]; }
         }
     }
     const float pd_cur = rp_in ? pd_cached : target_pdf(s, f, cur, cpos, ccol, tb);
@@ -1453,6 +1466,20 @@ ROMIS_SPATIAL1H_KERNEL(false, 1, k_spatial1h)
 ROMIS_SPATIAL1H_KERNEL(true, 1, k_spatial1h_dbg)
 ROMIS_SPATIAL1H_KERNEL(false, 2, k_spatial1h_t2)
 ROMIS_SPATIAL1H_KERNEL(true, 2, k_spatial1h_t2_dbg)
+#ifndef ROMIS_SPATIAL1HG_WPE
+#define ROMIS_SPATIAL1HG_WPE 8
+#endif
+#define ROMIS_SPATIAL1HG_KERNEL(DBG, NAME)                                                                             \
+    extern "C" __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL1HG_WPE))) void      \
+    NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
+         const float4* p_mat, HandlesIn hi, float4* oa, float4* ob, float2* odbg, const float* rp_in, float* rp_out,  \
+         float* how, uint32_t* hom, MissTiles mt, uint32_t odead) {                                                   \
+        spatial1h_body<DBG, 2, true>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, hi, oa, ob, odbg, rp_in, rp_out, how, \
+                                     hom, mt, odead);                                                                  \
+    }
+ROMIS_SPATIAL1HG_KERNEL(false, k_spatial1hg_t2)
+ROMIS_SPATIAL1HG_KERNEL(true, k_spatial1hg_t2_dbg)
+
 
 
 // k_spatial2_ntl: the biased pass for N = 2 sub-reservoirs (the reference's default, common.h:105), laid out like
@@ -2404,6 +2431,13 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
             const uint32_t nty2 = (rg.rh + 2u * kTileH - 1) / (2u * kTileH);
             if (rg.xcd_rows) {
                 if (tu.spatial_xcd_rows == kXcdRowsAuto) rg.xcd_rows = std::max(1u, rg.xcd_rows / 2u);
+                if (tu.spatial_xcd_rows == kXcdRowsAuto && tu.spatial_xcd_cols == kXcdColsAuto && ntx >= 64u) {
+                    // wide frames: 2-D chunks of 4 x 8 tiles (128 x 64 px), so the +-R window rows of vertically
+                    // adjacent tiles are re-read from one XCD's L2: C4f HBM traffic 1.30 -> 1.01x algorithmic (FETCH
+                    // 770 -> 541 MB a launch), spatial 404.5 -> 398.2 us (round 6, profiles/r6/probes/s4)
+                    rg.xcd_rows = 4u;
+                    rg.xcd_cols = 8u;
+                }
                 grid = xcd_grid(rg, ntx, nty2);
             } else {
                 grid = ntx * nty2;
@@ -2412,6 +2446,21 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
                          apron_max(2) * 16u + s.num_lights * 16u, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat, oa,
                          ob, odbg, rp_in, rp_out, mt, reinterpret_cast<const float4*>(hin.w),
                          reinterpret_cast<float4*>(hout.w), hout.res_dead);
+        } else if (hin.w && tu.spatial_gather && tu.spatial_th != 1u) {
+            // sample handles gathered instead of staged (k_spatial1hg_t2, spatial.gather; round 6): 32 x 16 tiles, the
+            // automatic XCD chunk one tile row as for k_spatial1h_t2
+            const uint32_t ntyh = (rg.rh + 2u * kTileH - 1) / (2u * kTileH);
+            if (rg.xcd_rows) {
+                if (tu.spatial_xcd_rows == kXcdRowsAuto) rg.xcd_rows = 1u;
+                grid = xcd_grid(rg, ntx, ntyh);
+            } else {
+                grid = ntx * ntyh;
+            }
+            const size_t lds = (size_t)apron_max(2) * 16u + (size_t)(2u * s.num_lights + 2u) * 16u;
+            const HandlesIn hi{hin.w, hin.m};
+            ROMIS_LAUNCH(odbg ? k_spatial1hg_t2_dbg : k_spatial1hg_t2, dim3(grid), dim3(2u * kBlock), lds, stream, s, rg, f,
+                         key, o[0], o[1], o[2], n_t, p_mat, hi, oa, ob, odbg, rp_in, rp_out, hout.w, hout.m, mt,
+                         hout.res_dead);
         } else if (hin.w) {
             // sample handles (k_spatial1h[_t2]): 32 x 8 TH tiles, TH = spatial.th (auto: 2 -- C2 66.9 us against 76.2 for
             // 32 x 8, 70.6 / 68.4 for 32 x 24 / 32 x 32, kbench, profiles/r5); the XCD chunks hold xcd_rows tile rows,

@@ -36,7 +36,7 @@ UNEVEN = {(4, 2): {"x": [0, 36, 52, 68, 96], "y": [[0, 20, 64], [0, 36, 64], [0,
 
 
 def _worker(rank, world, port, tiles, passes, N, out_dir, name="nightclub_128pt", records=0, backend="gloo",
-            width=W, height=H, unbiased=0, vis=0, layout_kind=None):
+            width=W, height=H, unbiased=0, vis=0, layout_kind=None, frames=FRAMES):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from romis_amd import _abi, distributed, restir, scene
@@ -56,7 +56,7 @@ def _worker(rank, world, port, tiles, passes, N, out_dir, name="nightclub_128pt"
         layout, _ = distributed.balanced_layout(r, lambda w, h: scene.camera_for(name, w, h), W, H, tiles, align=(8, 8))
     hf = distributed.HaloFrames(r, W, H, tiles, rank, _features(passes, N, unbiased, vis), layout=layout)
     prev = None
-    for fr in range(FRAMES):
+    for fr in range(frames):
         rgb, prev = hf.render(prev, cam)
         t = hf.tile
         full = np.zeros((H, W, 3), np.float32)
@@ -72,7 +72,8 @@ def _worker(rank, world, port, tiles, passes, N, out_dir, name="nightclub_128pt"
     dist.destroy_process_group()
 
 
-def _single_gpu_check(tmp_path, passes, N, name=_DEFAULT_SCENE, records=0, width=W, height=H, unbiased=0, vis=0):
+def _single_gpu_check(tmp_path, passes, N, name=_DEFAULT_SCENE, records=0, width=W, height=H, unbiased=0, vis=0,
+                      frames=FRAMES):
     from romis_amd import _abi, restir, scene
     W, H = width, height
     r = restir.Renderer(0)
@@ -83,7 +84,7 @@ def _single_gpu_check(tmp_path, passes, N, name=_DEFAULT_SCENE, records=0, width
         cam = scene.camera_for(name, W, H)
         f = _features(passes, N, unbiased, vis)
         prev = None
-        for fr in range(FRAMES):
+        for fr in range(frames):
             want, prev = r.render_restir(prev, cam, W, H, f)
             got = np.load(str(tmp_path / f"frame{fr}.npy"))
             bad = np.flatnonzero(got.view(np.uint32) != want.view(np.uint32))
@@ -113,6 +114,19 @@ def test_halo_frames_match_single_gpu_sequence(tmp_path, world, tiles, passes, N
     mp.spawn(_worker, args=(world, _free_port(), tiles, passes, N, str(tmp_path), name, records, "gloo", W, H,
                             unbiased, vis, layout_kind), nprocs=world, join=True)
     _single_gpu_check(tmp_path, passes, N, name, records, unbiased=unbiased, vis=vis)
+
+
+# The C4 / C5 strong-scaling split at full size: 8 processes on the box's GPU, each rendering its
+# rect of the 4K / 8K frame (the TOML camera: 87 % background) through the halo passes of a cost-balanced 4 x 2 layout
+# (distributed.balanced_layout: uneven per-column row cuts), halos over gloo; the stitched frame against restir_render's
+# single-GPU frame, which the full-size band tests pin to the oracle (test_full_size_frames_c4_c5_band_parity).
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,width,height,unbiased,vis", [("cornell_1024", 3840, 2160, 0, 0),
+                                                          ("cornell_4096", 7680, 4320, 1, 1)])
+def test_halo_full_size_balanced_split(tmp_path, name, width, height, unbiased, vis):
+    mp.spawn(_worker, args=(8, _free_port(), (4, 2), 1, 1, str(tmp_path), name, 0, "gloo", width, height, unbiased, vis,
+                            "balanced", 1), nprocs=8, join=True)
+    _single_gpu_check(tmp_path, 1, 1, name, 0, width, height, unbiased, vis, frames=1)
 
 
 # The native transport (restir_halo_pass: the library's own RCCL communicator, grouped ncclSend / ncclRecv on a

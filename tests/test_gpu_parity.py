@@ -13,6 +13,7 @@ pytestmark = pytest.mark.gpu
 
 W, H = 96, 64
 SEED = _abi.RESTIR_DEFAULT_SEED
+DEFAULT_GATHER = 1   # the library's spatial.gather default (restir_types.h Tuning::spatial_gather)
 
 
 @pytest.fixture(scope="module")
@@ -417,8 +418,9 @@ def test_render_frame_matches_oracle(gpu, oracle, name, N, passes, unbiased, M, 
 
 
 @pytest.mark.parametrize("name,framing", [("nightclub_128pt", None), ("cornell_1024", "framed"), ("cornell_4096", "framed")])
-@pytest.mark.parametrize("th", [1, 2])
-@pytest.mark.parametrize("w,h,passes,M", [(96, 64, 1, 32), (37, 23, 2, 32), (130, 70, 2, 1), (64, 1, 1, 16)])
+@pytest.mark.parametrize("th", [1, 2, "lds"])
+@pytest.mark.parametrize("w,h,passes,M", [(96, 64, 1, 32), (37, 23, 2, 32), (130, 70, 2, 1), (64, 1, 1, 16),
+                                          (70, 150, 1, 32)])
 def test_spatial_handles_frames_match_oracle(gpu, oracle, name, framing, th, w, h, passes, M):
     """The biased passes over sample handles (k_spatial1h[_tN], round 5: W and M | light index planes staged in LDS
     beside the n_t window, point lights) at every tile height, ragged sizes, 1 and 2 passes: RGB and the returned grid
@@ -426,14 +428,18 @@ def test_spatial_handles_frames_match_oracle(gpu, oracle, name, framing, th, w, 
     handles.  The RGB without a returned grid (bench.py's render) too.  cornell_1024 (C4's regular light grid, camera
     into the box): the grid handles (W, M | i, a, b) of k_spatial1g_t2, whose samples are rebuilt from RIS's draws of
     the light's fractions (32 x 16 tiles only: th = 1 runs the n_t-window pass instead); cornell_4096 (4,096 lights, past
-    the handle pass's 1,024-colour table): the reservoir form, as the host falls back."""
+    the handle pass's 1,024-colour table): the reservoir form, as the host falls back.  At 32 x 16 the point-light handle
+    pass gathers the neighbours' handles from global memory (k_spatial1hg_t2, the default since round 6); "lds": the
+    round-5 form with the handle windows staged in LDS beside the n_t window (k_spatial1h_t2)."""
     s = get_scene(name)
     gpu.set_scene(s)
     osc = oracle.OracleScene(s)
     cam = scene.camera_for(name, w, h, framing)
     f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=passes, temporal_reuse=0,
                               initial_light_samples=M)
-    gpu.set_tuning("spatial.th", th)
+    lds = th == "lds"   # 32 x 16 with the handle windows staged in LDS (k_spatial1h_t2) instead of gathered
+    gpu.set_tuning("spatial.th", 2 if lds else th)
+    gpu.set_tuning("spatial.gather", 0 if lds else DEFAULT_GATHER)
     try:
         gpu.set_seed(SEED, 0)
         rgb, grid = gpu.render_restir(None, cam, w, h, f)
@@ -441,6 +447,7 @@ def test_spatial_handles_frames_match_oracle(gpu, oracle, name, framing, th, w, 
         rgb_ng, _ = gpu.render_restir(None, cam, w, h, f, want_grid=False)
     finally:
         gpu.set_tuning("spatial.th", 0)
+        gpu.set_tuning("spatial.gather", DEFAULT_GATHER)
     want, res, _ = oracle.render_frame(osc, cam, f, w, h, SEED, 0)
     assert_bits(rgb, want, f"th={th} {w}x{h} passes={passes}")
     assert_grid(grid, res, f"th={th} {w}x{h} passes={passes}")
@@ -947,8 +954,8 @@ def test_miss_tiles_match_full_reads(gpu, oracle, name, passes, unbiased, vis, t
     spatial passes and final shading write those tiles' known results without reading them.  Frames at 640 x 360
     (the Cornell box fills the middle: most tiles, and most unbiased neighbourhoods, are background), whole and as a
     ghost-zoned screen tile (2 x 2 plan, rank 3: the RIS, spatial and final regions start at different offsets), must
-    equal the frames rendered with the flags off bit for bit -- RGB and the returned grid -- and, for whole frames, the
-    oracle's frame (RGB)."""
+    equal the frames rendered with the flags off bit for bit -- RGB and the returned grid -- and the oracle's frame (RGB;
+    a tile against the oracle's whole frame cropped to its owned rect)."""
     from romis_amd import restir
     tune = dict(tune)
     N = tune.pop("N", 1)
@@ -975,9 +982,11 @@ def test_miss_tiles_match_full_reads(gpu, oracle, name, passes, unbiased, vis, t
         gpu.set_tuning("miss.tiles", 1)
         gpu.set_tuning("miss.gbuf", 2)
         gpu.set_tuning("spatial.th", 0)
-    if tile is None:
-        want, _, _ = oracle.render_frame(oracle.OracleScene(s), cam, f, w, h, SEED, 0, threads=16)
-        assert_bits(on_rgb, want, f"{name} rgb against the oracle")
+    want, _, _ = oracle.render_frame(oracle.OracleScene(s), cam, f, w, h, SEED, 0, threads=16)
+    if tile is not None:   # the tile's rows (row 0 = its top) against the oracle's whole frame (row 0 = global y = h - 1)
+        r0 = h - (tile.y0 + tile.height)
+        want = np.ascontiguousarray(want[r0:r0 + tile.height, tile.x0:tile.x0 + tile.width])
+    assert_bits(on_rgb, want, f"{name} rgb against the oracle")
     assert_bits(on_rgb, off_rgb, f"{name} rgb")
     # a tiled frame's grid is defined on the owned rect (the ghost ring holds intermediate values, include/restir_c.h)
     own = (slice(None), slice(tile.y0 - tile.gy0, tile.y0 - tile.gy0 + tile.height),

@@ -153,6 +153,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                                           bool store_res = true, TemporalIn tin = TemporalIn{nullptr, nullptr, 0u}) {
     const uint32_t L = s.num_lights;
     uint32_t hidx = L;   // the held sample's light index for the handle planes (k_spatial1h; L = the zero sample)
+    uint32_t hidx1 = L;  // N = 2: sub-reservoir 1's (the handle record of k_spatial2hg)
     float ha = 0.0f, hb = 0.0f;   // kLtRegular: its fractions (grid handles, k_spatial1g_t2)
     const size_t npx = (size_t)rg.vw * rg.vh;
     const uint32_t N = NT > 0 ? (uint32_t)NT : f.N;
@@ -287,6 +288,10 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                         sample(best[j], r[j].pos, r[j].col);
                         r[j].has_pd = true;
                     }
+                if (LT == kLtPoint) {
+                    if (best[0] != 0xFFFFFFFFu) hidx = uniform_index(draw(ps, 4u * best[0]), L);
+                    if (best[1] != 0xFFFFFFFFu) hidx1 = uniform_index(draw(ps, 4u * best[1]), L);
+                }
             } else {
                 for (uint32_t c = 0; c < c_end; c++) {
                     v3 pos, col;
@@ -364,6 +369,9 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
         if (store_res || rdbg)
             for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, ridx(rg, j, p), j * npx + p);
         if (NT == 1 && LT == kLtPoint && hw) { hw[p] = r[0].W; hm[p] = r[0].M | (hidx << 24); }
+        if (NT == 2 && LT == kLtPoint && !TEMP && hw)   // N = 2 handle record (W_0, M_0 | i_0 << 24, W_1, M_1 | i_1 << 24)
+            reinterpret_cast<float4*>(hw)[p] = make_float4(r[0].W, __uint_as_float(r[0].M | (hidx << 24)), r[1].W,
+                                                           __uint_as_float(r[1].M | (hidx1 << 24)));
         if (NT == 1 && LT == kLtRegular && hw)   // grid handle: (W, M | i << 19, a, b) in one float4 plane
             reinterpret_cast<float4*>(hw)[p] = make_float4(r[0].W, __uint_as_float(r[0].M | (hidx << 19)), ha, hb);
     }
@@ -1664,6 +1672,237 @@ __device__ __forceinline__ void spatialn_ntl_body(const SceneDev& s, const Regio
     }
 }
 
+// k_spatial2hg[_t2]: the N = 2 biased pass over sample handles (round 6), point lights.  The producer
+// (k_primary_ris_n2*_pt, or this pass for the next) writes one 16-byte handle record per pixel, (W_0, M_0 | i_0 << 24,
+// W_1, M_1 | i_1 << 24) -- sub-reservoir j's W, M and light index (L = the zero sample) -- instead of the four 16-byte
+// reservoir records; an accepted neighbour is one 16-byte gather, its samples rebuilt from the light table the block
+// stages in LDS behind the n_t window (k_spatial2_ntl gathers 64 B).  The combine is spatialn_ntl_body's: each accepted
+// neighbour's two sub-reservoirs in order, then the pixel's own, each routed to the output with the smallest wSum
+// (strict <, first index: reservoir.cpp:10-32) and adding its M there (combineBiased, reservoir.cpp:40-66); the same
+// RNG slots and arithmetic on the same (position, colour, W, M) values.  The host enables it only while every M fits 24
+// bits and L <= 254.
+struct Comb2h {
+    float wsum[2], chosen[2], pd[2];
+    uint32_t macc[2], li[2];
+    bool has_pd[2];
+    uint32_t h;
+    __device__ __forceinline__ void init(uint32_t h0, uint32_t L) {
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            wsum[j] = ROMIS_FLT_MIN; chosen[j] = 0.0f; pd[j] = 0.0f; macc[j] = 0u; li[j] = L; has_pd[j] = false;
+        }
+        h = h0;
+    }
+    __device__ __forceinline__ void take(float pd_in, float W, uint32_t M, uint32_t l) {
+        const float w = (pd_in * W) * (float)M;          // reservoir.cpp:50
+        const bool k1 = wsum[1] < (wsum[0] < ROMIS_FLT_MAX ? wsum[0] : ROMIS_FLT_MAX);   // CombN's argmin, N = 2
+        const float u = rand01(mix32(h));
+        h += 0x9E3779B9u;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            if ((j == 1) == k1) {
+                macc[j] += M;
+                wsum[j] += w;
+                if (accept_u(u, w, wsum[j])) { li[j] = l; chosen[j] = w; pd[j] = pd_in; has_pd[j] = true; }
+            }
+        }
+    }
+};
+
+template <bool DBG, uint32_t TH>
+__device__ __forceinline__ void spatial2hg_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, uint32_t key,
+                                                v3 origin, const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
+                                                const float4* __restrict__ hin, float4* __restrict__ oa,
+                                                float4* __restrict__ ob, float2* __restrict__ odbg, float4* __restrict__ hout,
+                                                MissTiles mt, uint32_t odead) {
+    constexpr uint32_t kTH = kTileH * TH;
+    float4* const l_nt = g_lds;
+    float4* const l_lt = g_lds + apron_max(TH);
+    const uint32_t L = s.num_lights;
+    const uint32_t jofs = rg.js << 4;   // bytes between the sub-reservoir planes
+    uint32_t tile;
+    const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
+    if (!xcd_tile(rg, ntx * ((rg.rh + kTH - 1) / kTH), blockIdx.x, tile)) return;   // block-uniform
+    const int tx0 = (int)(rg.rx0 + (tile % ntx) * kTileW), ty0 = (int)(rg.ry0 + (tile / ntx) * kTH);
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;   // wave w: the 8x8 block (w % 4, w / 4)
+    auto put = [&](uint32_t pix, const float* W, const uint32_t* M, const uint32_t* li, const float* ws, const float* ch) {
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            if (!odead) {
+                const float4 pos = l_lt[li[j]], col = l_lt[L + 1u + li[j]];
+                st_at(oa, (pix << 4) + (uint32_t)j * jofs, make_float4(pos.x, pos.y, pos.z, W[j]));
+                st_at(ob, (pix << 4) + (uint32_t)j * jofs, make_float4(col.x, col.y, col.z, __uint_as_float(M[j])));
+            }
+            if (DBG) st_at(odbg, ((pix << 4) + (uint32_t)j * jofs) >> 1, make_float2(ws[j], ch[j]));
+        }
+        if (hout) hout[pix] = make_float4(W[0], __uint_as_float(M[0] | (li[0] << 24)), W[1], __uint_as_float(M[1] | (li[1] << 24)));
+    };
+    bool mixed = false;
+    if (mt.m) {
+        // a tile of background pixels: sub-reservoir 0 = (0, W = 0), (0, M = mt.m), sub-reservoir 1 = (0, W = 0), (0, M = 0)
+        // -- the miss shortcut's result below, written without reading the tile, its window or its neighbours.  The
+        // light table is not staged: the zero sample's (position, colour) are written as zeros
+        const int x1 = min(tx0 + (int)kTileW, (int)(rg.rx0 + rg.rw)) - 1, y1 = min(ty0 + (int)kTH, (int)(rg.ry0 + rg.rh)) - 1;
+        if (tiles_known_miss(mt, rg, tx0, x1, ty0, y1, &mixed)) {
+            const int mx = tx0 + (int)((w & 3u) * 8u + (l & 7u)), my = ty0 + (int)((w >> 2) * 8u + (l >> 3));
+            if (mx <= x1 && my <= y1) {
+                const uint32_t mp = (uint32_t)(my - (int)rg.vy0) * rg.vw + (uint32_t)(mx - (int)rg.vx0);
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    if (!odead) {
+                        st_at(oa, (mp << 4) + (uint32_t)j * jofs, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+                        st_at(ob, (mp << 4) + (uint32_t)j * jofs, make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(j == 0 ? mt.m : 0u)));
+                    }
+                    if (DBG) st_at(odbg, ((mp << 4) + (uint32_t)j * jofs) >> 1, make_float2(ROMIS_FLT_MIN, 0.0f));
+                }
+                if (hout) hout[mp] = make_float4(0.0f, __uint_as_float(mt.m | (L << 24)), 0.0f, __uint_as_float(L << 24));
+            }
+            return;   // block-uniform, before the window's barrier
+        }
+    }
+    const int xlo = max(0, (int)rg.vx0), xhi = min((int)rg.W, (int)(rg.vx0 + rg.vw)) - 1;
+    const int ylo = max(0, (int)rg.vy0), yhi = min((int)rg.H, (int)(rg.vy0 + rg.vh)) - 1;
+    const int R = (int)f.R;
+    const int ax0 = max(tx0 - R, xlo), ax1 = min(tx0 + (int)kTileW - 1 + R, xhi);
+    const int ay0 = max(ty0 - R, ylo), ay1 = min(ty0 + (int)kTH - 1 + R, yhi);
+    const uint32_t AW = (uint32_t)(ax1 - ax0 + 1), n_apron = AW * (uint32_t)(ay1 - ay0 + 1);
+    const int x = tx0 + (int)((w & 3u) * 8u + (l & 7u)), y = ty0 + (int)((w >> 2) * 8u + (l >> 3));
+    const bool live = x < (int)(rg.rx0 + rg.rw) && y < (int)(rg.ry0 + rg.rh);
+    const uint32_t pix = (uint32_t)(y - (int)rg.vy0) * rg.vw + (uint32_t)(x - (int)rg.vx0);
+    float4 cpm = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float4 ch = make_float4(0.0f, __uint_as_float(L << 24), 0.0f, __uint_as_float(L << 24));   // the own handle record
+    const bool own_bg = live && mixed && tile_flag_at(mt, rg, x, y) == 0u;   // a background RIS tile: known, unread
+    if (live) {
+        if (own_bg) {
+            cpm = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(s.num_materials - 1u));
+            ch.y = __uint_as_float(mt.m | (L << 24));
+        } else {
+            cpm = p_mat[pix];
+            ch = hin[pix];
+        }
+    }
+    ntl_stage_window<TH>(rg, n_t, l_nt, ax0, ay0, AW, n_apron);
+    {   // the light table behind the window: positions, zero, colours, zero (h_stage)
+        constexpr uint32_t kThreads = 256u * TH;
+        const uint32_t nd = 2u * L + 2u, w64 = (threadIdx.x >> 6) << 6;
+        for (uint32_t d0 = 0; d0 < nd; d0 += kThreads) {
+            const uint32_t d = d0 + threadIdx.x;
+            if (d < nd && d != L && d != 2u * L + 1u)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(d < L ? s.light_c2 + d : s.light_c2 + (d - 1u)),
+                                                 (__attribute__((address_space(3))) void*)(l_lt + d0 + w64), 16, 0, 0);
+        }
+        if (threadIdx.x < 2u) l_lt[threadIdx.x ? 2u * L + 1u : L] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    const GlTabs tb = gl_stage_tables_dma();
+    const uint32_t K = f.K;   // <= kLeanK (host check)
+    const uint32_t ps = pix_state(key, (uint32_t)y * rg.W + (uint32_t)x);
+    const uint32_t span = 2u * f.R + 1u;
+    uint32_t qi[kLeanK], qp[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        qi[n] = 0u;
+        qp[n] = pix;
+        if (n < K) {
+            const int nx = min(max(x - R + (int)__umulhi(draw(ps, 2u * n), span), xlo), xhi);
+            const int ny = min(max(y - R + (int)__umulhi(draw(ps, 2u * n + 1u), span), ylo), yhi);
+            qi[n] = (uint32_t)(ny - ay0) * AW + (uint32_t)(nx - ax0);
+            qp[n] = (uint32_t)(ny - (int)rg.vy0) * rg.vw + (uint32_t)(nx - (int)rg.vx0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's DMA before the barrier (spatial1_ntl_body)
+    if (mt.m && mt.gbuf) {   // background G-buffer records: spatial1_ntl_body's window fix-up
+        constexpr uint32_t kThreads = 256u * TH, kPer = (apron_max(TH) + kThreads - 1u) / kThreads;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++) {
+            const uint32_t i = threadIdx.x + kThreads * k;
+            if (i < n_apron) {
+                uint32_t r = __umulhi(i, 0xFFFFFFFFu / AW + 1u);
+                if (r * AW > i) r--;
+                const uint32_t c = i - r * AW;
+                if (tile_flag_at(mt, rg, ax0 + (int)c, ay0 + (int)r) == 0u) l_nt[i] = make_float4(0.0f, 0.0f, 0.0f, ROMIS_FLT_MAX);
+            }
+        }
+    }
+    __syncthreads();
+    if (!live) return;   // no barrier follows
+    const float4 cn = l_nt[(uint32_t)(y - ay0) * AW + (uint32_t)(x - ax0)];
+    const float cw[2] = {ch.x, ch.z};
+    const uint32_t cm[2] = {__float_as_uint(ch.y), __float_as_uint(ch.w)};
+    const Px cur = make_px(s, cn, cpm, origin, pix);
+    // primary-ray miss (spatialn_ntl_body): both own inputs go to sub-reservoir 0, nothing is accepted
+    bool miss = cur.mat == s.num_materials - 1u && s.normals_bounded && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z);
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const v3 cc = xyz(l_lt[L + 1u + (cm[j] >> 24)]);
+        miss = miss && __builtin_isfinite(cw[j]) && __builtin_isfinite(cc.x + cc.y + cc.z);
+    }
+    if (miss) {
+        const float W0[2] = {0.0f, 0.0f}, ws[2] = {ROMIS_FLT_MIN, ROMIS_FLT_MIN}, c0[2] = {0.0f, 0.0f};
+        const uint32_t M[2] = {(cm[0] & kHandleM) + (cm[1] & kHandleM), 0u}, li[2] = {L, L};
+        put(pix, W0, M, li, ws, c0);
+        return;
+    }
+    const double rt = rcp_d(cur.t);
+    const bool rt_all = __all(div_fast_ok(cur.t));
+    bool ok[kLeanK];
+    float4 qh[kLeanK];
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        ok[n] = false;
+        qh[n] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (n < K) {
+            const float4 g = l_nt[qi[n]];
+            const float nd = vdot(xyz(g), cur.N);
+            float q = div_by_rcp_d(g.w, rt);
+            if (__builtin_expect(!rt_all, 0)) {
+                if (!div_fast_ok(cur.t)) q = g.w / cur.t;
+            }
+            ok[n] = !(nd < 0.90630778703f) && !(fabsf(1.0f - q) > 0.1f);
+            if (ok[n]) qh[n] = hin[qp[n]];
+        }
+    }
+    Comb2h cmb;
+    cmb.init(ps + 2u * K * 0x9E3779B9u, L);
+    auto take = [&](float W, uint32_t hm) {
+        const uint32_t li = hm >> 24;
+        cmb.take(target_pdf(s, f, cur, xyz(l_lt[li]), xyz(l_lt[L + 1u + li]), tb), W, hm & kHandleM, li);
+    };
+#pragma unroll
+    for (uint32_t n = 0; n < kLeanK; n++) {
+        if (ok[n]) {
+            take(qh[n].x, __float_as_uint(qh[n].y));
+            take(qh[n].z, __float_as_uint(qh[n].w));
+        }
+    }
+    take(cw[0], cm[0]);
+    take(cw[1], cm[1]);
+    float W[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        float p = cmb.pd[j];
+        if (!cmb.has_pd[j])
+            p = (f.shading && !__builtin_isnan(cur.P.x + cur.P.y + cur.P.z))
+                    ? 0.0f : target_pdf(s, f, cur, xyz(l_lt[cmb.li[j]]), xyz(l_lt[L + 1u + cmb.li[j]]), tb);
+        W[j] = contribution_weight(p, cmb.macc[j], cmb.wsum[j]);
+    }
+    put(pix, W, cmb.macc, cmb.li, cmb.wsum, cmb.chosen);
+}
+
+#ifndef ROMIS_SPATIAL2HG_WPE
+#define ROMIS_SPATIAL2HG_WPE 5
+#endif
+#define ROMIS_SPATIAL2HG_KERNEL(DBG, TH, NAME)                                                                         \
+    extern "C" __global__ __launch_bounds__(256 * TH) __attribute__((amdgpu_waves_per_eu(ROMIS_SPATIAL2HG_WPE))) void  \
+    NAME(SceneDev s, Region rg, FeaturesDev f, uint32_t key, float ox, float oy, float oz, const float4* n_t,        \
+         const float4* p_mat, const float4* hin, float4* oa, float4* ob, float2* odbg, float4* hout, MissTiles mt,     \
+         uint32_t odead) {                                                                                            \
+        spatial2hg_body<DBG, TH>(s, rg, f, key, mk(ox, oy, oz), n_t, p_mat, hin, oa, ob, odbg, hout, mt, odead);        \
+    }
+ROMIS_SPATIAL2HG_KERNEL(false, 1, k_spatial2hg)
+ROMIS_SPATIAL2HG_KERNEL(true, 1, k_spatial2hg_dbg)
+ROMIS_SPATIAL2HG_KERNEL(false, 2, k_spatial2hg_t2)
+ROMIS_SPATIAL2HG_KERNEL(true, 2, k_spatial2hg_t2_dbg)
+
 #ifndef ROMIS_SPATIAL2_NTL_WPE
 #define ROMIS_SPATIAL2_NTL_WPE 4
 #endif
@@ -2289,7 +2528,7 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
                         : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
     ROMIS_LAUNCH(k, dim3(items_of(rg)), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
                  cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr, tu.ris_late, tmiss,
-                 tmiss ? skip_res : 0u, (lt == kLtPoint || lt == kLtRegular) && f.N == 1 ? h.w : nullptr,
+                 tmiss ? skip_res : 0u, ((lt == kLtPoint || lt == kLtRegular) && f.N == 1) || (lt == kLtPoint && f.N == 2) ? h.w : nullptr,
                  lt == kLtPoint && f.N == 1 ? h.m : nullptr, h.w && (lt == kLtPoint || lt == kLtRegular) ? h.res_dead : 0u);
     return hipGetLastError();
 }
@@ -2318,11 +2557,15 @@ hipError_t launch_primary_ris_temporal(const SceneDev& s, const Region& rg0, con
 bool primary_ris_fits(const SceneDev& s) { return bvh_lds_bytes(s) <= kLdsBudget; }
 
 int spatial_handle_kind(const SceneDev& s, const FeaturesDev& f, const Tuning& tu, uint32_t passes, uint64_t m0) {
-    if (!tu.spatial_handles || passes == 0 || f.N != 1 || f.unbiased || f.K > kLeanK || f.R > kLdsSpatialR) return -1;
+    if (!tu.spatial_handles || passes == 0 || (f.N != 1 && f.N != 2) || f.unbiased || f.K > kLeanK || f.R > kLdsSpatialR)
+        return -1;
     if (!tu.spatial_lean || !tu.ris_compact || s.num_lights == 0) return -1;
     int hk;
     uint32_t mmax;
-    if (s.light_types == 1u && s.num_lights <= 254u) {   // point lights (k_spatial1h); index L = the zero sample
+    if (f.N == 2) {   // point lights: the 16-byte handle records of k_spatial2hg (spatial.n2h)
+        if (!tu.spatial_n2h || s.light_types != 1u || s.num_lights > 254u) return -1;
+        hk = 2; mmax = kHandleM;
+    } else if (s.light_types == 1u && s.num_lights <= 254u) {   // point lights (k_spatial1h); index L = the zero sample
         hk = 0; mmax = kHandleM;
     } else if (ris_light_form(s, f, tu) == kLtRegular && tu.spatial_th != 1u && s.num_lights <= 1024u) {
         // a regular light grid (RIS's kLtRegular form; k_spatial1g_t2, 32 x 16 tiles, <= 16 KB of colours in LDS)
@@ -2405,6 +2648,19 @@ hipError_t launch_spatial(const SceneDev& s, const Region& rg0, const FeaturesDe
         rg.xcd_rows = tu.spatial_xcd_rows == kXcdRowsAuto ? std::max(1u, std::min(8u, 8192u / std::max(rg.rw, 1u)))
                                                           : tu.spatial_xcd_rows;
         rg.xcd_cols = tu.spatial_xcd_cols == kXcdColsAuto ? 0u : tu.spatial_xcd_cols;
+        if (hin.w) {
+            // handle records (k_spatial2hg[_t2], spatial_handle_kind 2): 32 x 8 TH tiles, TH = spatial.th (auto 1)
+            if (s.light_types != 1u) return hipErrorInvalidValue;
+            const uint32_t th = tu.spatial_th == 2u ? 2u : 1u, ntyh = (rg.rh + th * kTileH - 1) / (th * kTileH);
+            if (th == 2u && rg.xcd_rows && tu.spatial_xcd_rows == kXcdRowsAuto) rg.xcd_rows = std::max(1u, rg.xcd_rows / 2u);
+            grid = rg.xcd_rows ? xcd_grid(rg, ntx, ntyh) : ntx * ntyh;
+            const size_t lds = (size_t)apron_max(th) * 16u + (size_t)(2u * s.num_lights + 2u) * 16u;
+            auto k = th == 2u ? (odbg ? k_spatial2hg_t2_dbg : k_spatial2hg_t2) : (odbg ? k_spatial2hg_dbg : k_spatial2hg);
+            ROMIS_LAUNCH(k, dim3(grid), dim3(th * kBlock), lds, stream, s, rg, f, key, o[0], o[1], o[2], n_t, p_mat,
+                         reinterpret_cast<const float4*>(hin.w), oa, ob, odbg, reinterpret_cast<float4*>(hout.w), mt,
+                         hout.res_dead);
+            return hipGetLastError();
+        }
         if (rg.xcd_rows) grid = xcd_grid(rg, ntx, nty);
         ROMIS_LAUNCH(odbg ? k_spatial2_ntl_dbg : k_spatial2_ntl, dim3(grid), dim3(kBlock), kApronMax * 16u, stream, s, rg, f,
                      key, o[0], o[1], o[2], n_t, p_mat, ia, ib, oa, ob, odbg, mt);

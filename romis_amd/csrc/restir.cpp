@@ -2598,6 +2598,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "spatial.th")) { if (v > 2) return fail(RESTIR_ERR_INVALID, "spatial.th: 0 (auto), 1 or 2"); t.spatial_th = v; }
     else if (!std::strcmp(key, "spatial.handles")) t.spatial_handles = v;
     else if (!std::strcmp(key, "spatial.gather")) t.spatial_gather = v;
+    else if (!std::strcmp(key, "spatial.n2h")) t.spatial_n2h = v;
     else if (!std::strcmp(key, "fuse.primary_ris")) t.fuse_primary_ris = v;
     else if (!std::strcmp(key, "fuse.temporal")) t.fuse_temporal = v;
     else if (!std::strcmp(key, "timing.mask")) t.timing_mask = v;

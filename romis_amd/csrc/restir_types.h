@@ -157,6 +157,7 @@ struct Tuning {
     uint32_t spatial_th = 0;       // N = 1 biased ntl pass: tile height in 8-row units (1: 32x8, 2: 32x16 k_spatial1_ntl_t2; 0: by width)
     uint32_t fuse_temporal = 1;    // restir_render with a predecessor: temporal reuse inside the fused RIS kernel
     uint32_t spatial_handles = 1;  // restir_render, N = 1 biased, point lights: the passes read sample handles (k_spatial1h)
+    uint32_t spatial_n2h = 1;      // N = 2 biased passes over point lights read 16-byte handle records (k_spatial2hg)
     uint32_t spatial_gather = 1;   // the point-light handle pass on 32 x 16 tiles gathers the accepted neighbours' handles
                                    // (k_spatial1hg_t2: 34 KB of LDS, four blocks per CU) instead of staging the handle
                                    // windows in LDS (k_spatial1h_t2: 49.5 KB, three blocks); C2 65.7 -> 64.9 us (round 6)

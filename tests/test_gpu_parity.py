@@ -454,6 +454,37 @@ def test_spatial_handles_frames_match_oracle(gpu, oracle, name, framing, th, w, 
     assert_bits(rgb_ng, want, f"no grid th={th} {w}x{h} passes={passes}")
 
 
+@pytest.mark.parametrize("th", [1, 2])
+@pytest.mark.parametrize("w,h,passes,M", [(96, 64, 1, 32), (37, 23, 2, 32), (130, 70, 3, 1), (64, 1, 1, 16)])
+def test_spatial_n2_handles_frames_match_oracle(gpu, oracle, th, w, h, passes, M):
+    """N = 2 (the reference's default, common.h:105) biased passes over 16-byte handle records (k_spatial2hg[_t2], round
+    6): RIS writes (W_0, M_0 | i_0, W_1, M_1 | i_1) instead of its reservoirs, each pass gathers an accepted neighbour's
+    record and rebuilds both samples from the light table; a pass before the last writes only records.  RGB and the
+    returned grid bit-exact with the oracle (render_utils.cpp:87-140, reservoir.cpp:10-66), and with the handle path off
+    (spatial.n2h = 0: k_spatial2_ntl over the reservoirs)."""
+    name = "nightclub_128pt"
+    s = get_scene(name)
+    gpu.set_scene(s)
+    osc = oracle.OracleScene(s)
+    cam = scene.camera_for(name, w, h)
+    f = _abi.default_features(num_samples_in_reservoir=2, spatial_resampling_passes=passes, temporal_reuse=0,
+                              initial_light_samples=M)
+    gpu.set_tuning("spatial.th", th)
+    try:
+        gpu.set_seed(SEED, 0)
+        rgb, grid = gpu.render_restir(None, cam, w, h, f)
+        gpu.set_tuning("spatial.n2h", 0)
+        gpu.set_seed(SEED, 0)
+        rgb_off, _ = gpu.render_restir(None, cam, w, h, f, want_grid=False)
+    finally:
+        gpu.set_tuning("spatial.th", 0)
+        gpu.set_tuning("spatial.n2h", 1)
+    want, res, _ = oracle.render_frame(osc, cam, f, w, h, SEED, 0)
+    assert_bits(rgb, want, f"N=2 th={th} {w}x{h} passes={passes}")
+    assert_grid(grid, res, f"N=2 th={th} {w}x{h} passes={passes}")
+    assert_bits(rgb_off, want, f"N=2 reservoir form th={th} {w}x{h} passes={passes}")
+
+
 @pytest.mark.parametrize("w,h,N,passes,M", [(1, 1, 1, 2, 32), (37, 23, 2, 2, 32), (33, 9, 1, 1, 1), (40, 24, 32, 1, 8),
                                           (64, 1, 3, 2, 16), (1, 50, 1, 1, 32)])
 def test_odd_sizes_and_extremes_match_oracle(gpu, oracle, w, h, N, passes, M):

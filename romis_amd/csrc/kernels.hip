@@ -2190,7 +2190,9 @@ __device__ __forceinline__ v3 tone_map_rgb(const FeaturesDev& f, v3 color, const
     return g == 1.0f ? mapped : mk(gl_powf(tb, mapped.x, g), gl_powf(tb, mapped.y, g), gl_powf(tb, mapped.z, g));
 }
 
-template <bool LDS_BVH, int NT>
+// QB: the shadow rays walk the 16-byte nodes (occluded_q, SceneDev::nodes_q; round 6) staged in LDS instead of the
+// 32-byte ones -- the walk is bound by LDS throughput (probes/s6)
+template <bool LDS_BVH, int NT, bool QB = false>
 __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Region& rg, const FeaturesDev& f, v3 origin,
                                                   const float4* __restrict__ n_t, const float4* __restrict__ p_mat,
                                                   const float4* __restrict__ ra, const float4* __restrict__ rb,
@@ -2221,7 +2223,14 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
     __shared__ uint32_t s_wsum[4];
     __shared__ float4 s_from[kRays], s_to[kRays];
     __shared__ uint32_t s_vis[kRays];
-    const Bvh bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
+    Bvh bvh;
+    BvhQ bq;
+    if (QB) {
+        bq = stage_bvh_q(s, g_lds);
+        bvh = global_bvh(s);   // target_bin's root box
+    } else {
+        bvh = LDS_BVH ? stage_bvh(s, g_lds) : global_bvh(s);
+    }
     const GlTabs tb = gl_stage_tables();
     const uint32_t t = threadIdx.x;
     uint32_t x, y;
@@ -2309,7 +2318,7 @@ __device__ __forceinline__ void final_sorted_body(const SceneDev& s, const Regio
         const uint32_t i = (uint32_t)j * 256u + t;
         if (i < total) {
             const float4 a = s_from[i], b = s_to[i];
-            s_vis[__float_as_uint(a.w)] = visible(bvh, xyz(a), xyz(b)) ? 1u : 0u;
+            s_vis[__float_as_uint(a.w)] = (QB ? visible_q(bq, xyz(a), xyz(b)) : visible(bvh, xyz(a), xyz(b))) ? 1u : 0u;
         }
     }
     __syncthreads();
@@ -2339,6 +2348,17 @@ extern "C" __global__ __launch_bounds__(256) void k_final_n2_sorted(SceneDev s, 
                                                                    float oz, const float4* n_t, const float4* p_mat,
                                                                    const float4* ra, const float4* rb, float* rgb, MissTiles mt) {
     final_sorted_body<true, 2>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, nullptr, mt);
+}
+extern "C" __global__ __launch_bounds__(256) void k_final_n1_sorted_q(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,
+                                                                     float oz, const float4* n_t, const float4* p_mat,
+                                                                     const float4* ra, const float4* rb, float* rgb,
+                                                                     const uint8_t* vis_in, MissTiles mt) {
+    final_sorted_body<true, 1, true>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, vis_in, mt);
+}
+extern "C" __global__ __launch_bounds__(256) void k_final_n2_sorted_q(SceneDev s, Region rg, FeaturesDev f, float ox, float oy,
+                                                                     float oz, const float4* n_t, const float4* p_mat,
+                                                                     const float4* ra, const float4* rb, float* rgb, MissTiles mt) {
+    final_sorted_body<true, 2, true>(s, rg, f, mk(ox, oy, oz), n_t, p_mat, ra, rb, rgb, nullptr, mt);
 }
 
 #define ROMIS_FINAL_KERNEL(NT, LDS, NAME)                                                                              \
@@ -2791,6 +2811,16 @@ hipError_t launch_final(const SceneDev& s, const Region& rg0, const FeaturesDev&
     if (tu.final_sort && use_lds && (f.N == 1 || f.N == 2) && rg.map2d) {   // one tile per block
         SceneDev sf = s;
         if (!tu.final_miss) sf.miss_shade_zero = 0u;   // final.miss = 0: no miss shortcut (A/B runs)
+        if ((tu.final_qbvh == 1u || (tu.final_qbvh == 2u && f.N == 2)) && s.nodes_q_ok) {   // 16-byte nodes (occluded_q)
+            const size_t lq = ((size_t)s.num_nodes + (size_t)3 * s.num_tris) * 16;
+            if (f.N == 1)
+                ROMIS_LAUNCH(k_final_n1_sorted_q, dim3(items_of(rg)), dim3(kBlock), lq, stream, sf, rg, f, o[0], o[1], o[2],
+                             n_t, p_mat, ra, rb, rgb, vis_in, rg.map2d ? mt : MissTiles{nullptr, 0u, 0u});
+            else
+                ROMIS_LAUNCH(k_final_n2_sorted_q, dim3(items_of(rg)), dim3(kBlock), lq, stream, sf, rg, f, o[0], o[1], o[2],
+                             n_t, p_mat, ra, rb, rgb, rg.map2d ? mt : MissTiles{nullptr, 0u, 0u});
+            return hipGetLastError();
+        }
         if (f.N == 1)
             ROMIS_LAUNCH(k_final_n1_sorted, dim3(items_of(rg)), dim3(kBlock), lds, stream, sf, rg, f, o[0], o[1], o[2], n_t,
                          p_mat, ra, rb, rgb, vis_in, rg.map2d ? mt : MissTiles{nullptr, 0u, 0u});

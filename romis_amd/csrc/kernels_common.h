@@ -141,6 +141,80 @@ __device__ __forceinline__ bool occluded(const Bvh& b, v3 o, v3 d, float tfar) {
     return false;
 }
 
+// The shadow rays' traversal arrays over the 16-byte nodes (SceneDev::nodes_q), global or the workgroup's LDS copy.
+struct BvhQ {
+    const uint4* nodes;
+    const float4* v0;
+    const float4* e1;
+    const float4* e2;
+    uint32_t num_nodes;
+    v3 lo, s;   // coordinate = lo + q * s per axis
+};
+
+// Copy the 16-byte nodes + triangles into LDS (every thread of the block participates; ends with a barrier).
+__device__ __forceinline__ BvhQ stage_bvh_q(const SceneDev& s, float4* lds) {
+    const uint32_t nn = s.num_nodes, nt = s.num_tris;
+    uint4* ln = reinterpret_cast<uint4*>(lds);
+    for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) ln[i] = s.nodes_q[i];
+    for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) {
+        lds[nn + i] = s.tri_v0[i];
+        lds[nn + nt + i] = s.tri_e1[i];
+        lds[nn + 2 * nt + i] = s.tri_e2[i];
+    }
+    __syncthreads();
+    BvhQ b;
+    b.nodes = ln; b.v0 = lds + nn; b.e1 = lds + nn + nt; b.e2 = lds + nn + 2 * nt; b.num_nodes = nn;
+    b.lo = xyz(s.q_lo); b.s = xyz(s.q_s);
+    return b;
+}
+
+// occluded over the 16-byte nodes: the same threaded walk, one 16-byte node read per step instead of two.  The slab
+// distances of a grid coordinate lo + q s are fma(q, s / d, (lo - o) / d): the quantized box contains the padded float
+// box (snapped outward, bvh padding 1e-5 of the scene size beyond the triangles, grid step 1.5e-5 of it), and the
+// rounding of either test is ~2^-22 of the scene size, so every box holding a hit the float test accepts is accepted
+// here; the result, any exact triangle hit in
+// (0, tfar] among the accepted leaves, is occluded's (render_utils.cpp:54-65 -> utils.cpp:41-56).
+__device__ __forceinline__ bool occluded_q(const BvhQ& b, v3 o, v3 d, float tfar) {
+    const v3 invd = safe_inv(d);
+    const float tb = widen(tfar);
+    const v3 A = mk(b.s.x * invd.x, b.s.y * invd.y, b.s.z * invd.z);
+    const v3 C = mk((b.lo.x - o.x) * invd.x, (b.lo.y - o.y) * invd.y, (b.lo.z - o.z) * invd.z);
+    uint32_t i = 0;
+    while (i < b.num_nodes) {
+        const uint4 n = b.nodes[i];
+        const float tx0 = __builtin_fmaf((float)(n.x & 0xFFFFu), A.x, C.x), tx1 = __builtin_fmaf((float)(n.y >> 16), A.x, C.x);
+        const float ty0 = __builtin_fmaf((float)(n.x >> 16), A.y, C.y), ty1 = __builtin_fmaf((float)(n.z & 0xFFFFu), A.y, C.y);
+        const float tz0 = __builtin_fmaf((float)(n.y & 0xFFFFu), A.z, C.z), tz1 = __builtin_fmaf((float)(n.z >> 16), A.z, C.z);
+        const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+        const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tb));
+        const uint32_t cnt = n.w >> 28, miss = n.w & 0xFFFFu;
+        if (tmin <= tmax) {
+            if (cnt) {
+                const uint32_t first = (n.w >> 16) & 0xFFFu;
+                for (uint32_t k = 0; k < cnt; k += 2) {   // two triangles per step, as occluded
+                    bool h = tri_any(b.v0[first + k], b.e1[first + k], b.e2[first + k], o, d, tfar);
+                    if (k + 1 < cnt) h = tri_any(b.v0[first + k + 1], b.e1[first + k + 1], b.e2[first + k + 1], o, d, tfar) || h;
+                    if (h) return true;
+                }
+                i = miss;
+            } else {
+                i = i + 1;
+            }
+        } else {
+            i = miss;
+        }
+    }
+    return false;
+}
+
+// testVisibilityLightSample (utils.cpp:41-56) over the 16-byte nodes
+__device__ __forceinline__ bool visible_q(const BvhQ& b, v3 P, v3 y) {
+    v3 dir = vnormalize(vsub(y, P));
+    v3 P2 = vadd(P, vscale(dir, 1e-3f));
+    float tfar = vdistance(P2, y);
+    return !occluded_q(b, P2, dir, tfar);
+}
+
 // closest hit: minimal t, lowest original triangle index on ties
 __device__ __forceinline__ bool closest(const Bvh& b, v3 o, v3 d, float& t_best, float& u_best, float& v_best,
                                         uint32_t& tri_best) {

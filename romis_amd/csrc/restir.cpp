@@ -227,7 +227,7 @@ struct restir_ctx {
 
     // scene
     DevBuf nodes, tri_v0, tri_e1, tri_e2, tri_n0, tri_n1, tri_n2, materials, lights, light_c2, light_c4, light_col, tex_texels,
-        tex_dims, tri_uv;
+        tex_dims, tri_uv, nodes_q;
     SceneDev sdev{};
     bool has_scene = false;
     uint64_t scene_gen = 0;   // unique per scene upload (frame handles name the light table they index)
@@ -998,7 +998,7 @@ void restir_destroy(restir_ctx* c) {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
         for (DevBuf* b : {&c->vis, &c->tmiss, &c->hnd[0], &c->hnd[1]}) b->release();
-        for (DevBuf* b : {&c->nodes, &c->tri_v0, &c->tri_e1, &c->tri_e2, &c->tri_n0, &c->tri_n1, &c->tri_n2,
+        for (DevBuf* b : {&c->nodes, &c->nodes_q, &c->tri_v0, &c->tri_e1, &c->tri_e2, &c->tri_n0, &c->tri_n1, &c->tri_n2,
                           &c->materials, &c->lights, &c->light_c2, &c->light_c4, &c->light_col, &c->tex_texels, &c->tex_dims, &c->tri_uv, &c->uv, &c->n_t, &c->p_mat, &c->ra[0], &c->ra[1], &c->rb[0], &c->rb[1],
                           &c->dbg[0], &c->dbg[1], &c->rgb, &c->halo_scratch, &c->rec[0], &c->rec[1], &c->rp[0], &c->rp[1]})
             b->release();
@@ -1204,9 +1204,50 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     if (n0.empty()) { n0.assign(4, 0.0f); n1.assign(4, 0.0f); n2.assign(4, 0.0f); }
     std::vector<float> nodes = bvh.nodes;
     if (nodes.empty()) nodes.assign(8, 0.0f);
+    // The shadow rays' 16-byte nodes (SceneDev::nodes_q, kernels_common.h occluded_q): each padded box snapped outward to
+    // a 16-bit grid over the root box, so the quantized box contains the float one -- a test against it accepts every
+    // box the float test accepts (and a few more), and any-hit decides by the exact triangle tests alone, in any order.
+    std::vector<uint32_t> nq;
+    float q_lo[3] = {0.0f, 0.0f, 0.0f}, q_s[3] = {1.0f, 1.0f, 1.0f};
+    bool q_ok = bvh.num_nodes > 0 && bvh.num_nodes < 65536u;
+    for (uint32_t i = 0; q_ok && i < bvh.num_nodes; i++) {
+        const uint32_t leaf = f2u(nodes[8 * i + 7]);
+        q_ok = leaf == 0u || ((leaf >> 24) < 16u && (leaf & 0xFFFFFFu) + (leaf >> 24) <= 4096u);
+    }
+    if (q_ok) {
+        for (int a = 0; a < 3; a++) {
+            const double lo = nodes[a], hi = nodes[4 + a];   // the root's padded box
+            q_lo[a] = (float)lo;
+            if ((double)q_lo[a] > lo) q_lo[a] = std::nextafter(q_lo[a], -INFINITY);
+            q_s[a] = (float)std::max((hi - (double)q_lo[a]) / 65532.0, 1e-30);
+            q_ok = q_ok && std::isfinite(q_lo[a]) && std::isfinite(q_s[a]);
+        }
+    }
+    if (q_ok) {
+        nq.assign(4 * (size_t)bvh.num_nodes, 0u);
+        for (uint32_t i = 0; i < bvh.num_nodes && q_ok; i++) {
+            uint32_t q[6];
+            for (int a = 0; a < 3; a++) {
+                const double lo = nodes[8 * i + a], hi = nodes[8 * i + 4 + a];
+                const double ql = std::floor((lo - (double)q_lo[a]) / (double)q_s[a]);
+                const double qh = std::ceil((hi - (double)q_lo[a]) / (double)q_s[a]);
+                q_ok = q_ok && ql >= -1.0 && qh <= 65535.0;
+                q[a] = (uint32_t)std::max(ql, 0.0);
+                q[3 + a] = (uint32_t)std::min(std::max(qh, 0.0), 65535.0);
+            }
+            const uint32_t miss = f2u(nodes[8 * i + 3]), leaf = f2u(nodes[8 * i + 7]);
+            nq[4 * i + 0] = q[0] | (q[1] << 16);
+            nq[4 * i + 1] = q[2] | (q[3] << 16);
+            nq[4 * i + 2] = q[4] | (q[5] << 16);
+            // miss link (16 bits: bvh.num_nodes < 65536), first triangle (12 bits), count (4 bits; 0 = inner node)
+            nq[4 * i + 3] = std::min(miss, 65535u) | ((leaf & 0xFFFu) << 16) | ((leaf >> 24) << 28);
+        }
+    }
+    if (!q_ok) nq.assign(4, 0u);
 
     HIP_TRY(hipStreamSynchronize(c->stream));   // previous frames (either slot) may still read the old scene
     ST_TRY(c->nodes.upload(nodes.data(), nodes.size() * 4, c->stream));
+    ST_TRY(c->nodes_q.upload(nq.data(), nq.size() * 4, c->stream));
     ST_TRY(c->tri_v0.upload(v0.data(), v0.size() * 4, c->stream));
     ST_TRY(c->tri_e1.upload(e1.data(), e1.size() * 4, c->stream));
     ST_TRY(c->tri_e2.upload(e2.data(), e2.size() * 4, c->stream));
@@ -1273,6 +1314,10 @@ restir_status restir_set_scene_textured(restir_ctx* c, const restir_mesh* meshes
     SceneDev& s = c->sdev;
     s.nodes = c->nodes.as<float4>();
     s.num_nodes = bvh.num_nodes;
+    s.nodes_q = c->nodes_q.as<uint4>();
+    s.nodes_q_ok = q_ok ? 1u : 0u;
+    s.q_lo = make_float4(q_lo[0], q_lo[1], q_lo[2], 0.0f);
+    s.q_s = make_float4(q_s[0], q_s[1], q_s[2], 0.0f);
     s.tri_v0 = c->tri_v0.as<float4>();
     s.tri_e1 = c->tri_e1.as<float4>();
     s.tri_e2 = c->tri_e2.as<float4>();
@@ -2616,6 +2661,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "ris.compact")) t.ris_compact = v;
     else if (!std::strcmp(key, "bvh.max_leaf")) t.bvh_max_leaf = v;
     else if (!std::strcmp(key, "final.sort")) t.final_sort = v;
+    else if (!std::strcmp(key, "final.qbvh")) t.final_qbvh = v;
     else if (!std::strcmp(key, "mis.chunk")) t.mis_chunk = v;   // applies from the next ensure_mis
     else if (!std::strcmp(key, "layout.records")) t.records = v;   // frame-path buffer layout
     else if (!std::strcmp(key, "final.lds")) t.final_lds = v;

@@ -33,6 +33,13 @@ struct SceneDev {
     //                                                  (count << 24) | first triangle (BVH order)
     const float4* nodes;
     uint32_t num_nodes;
+    // The same nodes for shadow rays, 16 bytes each (kernels_common.h occluded_q): the padded box snapped outward to a
+    // 16-bit grid over the root box -- x = lo.x | lo.y << 16, y = lo.z | hi.x << 16, z = hi.y | hi.z << 16, coordinate
+    // = q_lo + q * q_s -- and w = miss link | first triangle << 16 | count << 28 (count 0: inner node).  nodes_q_ok = 0
+    // when the tree does not fit (>= 65,536 nodes, a leaf past triangle 4,096 or of > 15 triangles).
+    const uint4* nodes_q;
+    uint32_t nodes_q_ok;
+    float4 q_lo, q_s;
     // Triangles in BVH order (Moller-Trumbore operands, e1 = v1 - v0, e2 = v2 - v0 computed on the host):
     //   tri_v0.w = bits(original triangle index) -- closest-hit ties resolve to the lowest original index
     const float4* tri_v0;
@@ -170,6 +177,9 @@ struct Tuning {
     uint32_t bvh_max_leaf = 2;     // triangles per BVH leaf (used by restir_set_scene); 2 beat 1/4/8 (kbench)
     uint32_t final_lds = 1;
     uint32_t final_miss = 1;       // k_final_n*_sorted: primary-ray misses read p_mat + (pos, W) only (SceneDev::miss_shade_zero)
+    uint32_t final_qbvh = 2;       // k_final_n*_sorted: shadow rays over the 16-byte nodes (SceneDev::nodes_q) when they fit;
+                                   // 2 (auto): at N = 2 (C2 N = 2 final 153.6 -> 145.8 us; N = 1: C2 80.0 -> 79.5, C4f
+                                   // 265.8 -> 277.4 -- round 6, profiles/r6/probes/s7)
     uint32_t final_sort = 1;       // N = 1: bin each tile's shadow rays by target before tracing (-2.4 %, r2ah)
     uint32_t mis_chunk = 0;        // R-OMIS samples per k_romis_samples / k_romis_accum pair; 0 = the scratch budget
 };

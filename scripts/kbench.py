@@ -22,7 +22,7 @@ from romis_amd import _abi, restir, scene  # noqa: E402
 
 DEFAULTS = {"primary.lds": 1, "ris.lds": 1, "ris.compact": 1, "ris.late": 1, "miss.tiles": 1, "miss.gbuf": 2,
             "spatial.xcd_rows": 255, "spatial.xcd_cols": 255, "spatial.lean": 1, "spatial.th": 0, "spatial.handles": 1, "spatial.gather": 1, "spatial.n2h": 1,
-            "fuse.primary_ris": 1, "fuse.temporal": 1, "bvh.max_leaf": 2, "final.lds": 1, "final.sort": 1, "final.miss": 1, "layout.records": 0}
+            "fuse.primary_ris": 1, "fuse.temporal": 1, "bvh.max_leaf": 2, "final.lds": 1, "final.sort": 1, "final.qbvh": 2, "final.miss": 1, "layout.records": 0}
 
 VARIANTS = {
     "default": {},

@@ -979,7 +979,11 @@ def test_full_size_c3_sequence_band_parity(gpu, oracle, N):
     ("cornell_1024", 1, 0, 0, 0, {"miss.gbuf": 1, "spatial.th": 2}), ("nightclub_128pt", 1, 0, 0, 0, {"miss.gbuf": 1}),
     # N = 2 (the reference default): k_spatial2_ntl and k_final_n2_sorted read the flags too
     ("cornell_1024", 1, 0, 0, 0, {"N": 2}), ("cornell_1024", 2, 0, 0, 0, {"N": 2}), ("nightclub_128pt", 1, 0, 0, 0, {"N": 2}),
-    ("cornell_1024", 2, 0, 0, 1, {"N": 2}), ("cornell_4096", 1, 1, 1, 0, {"N": 2})])
+    ("cornell_1024", 2, 0, 0, 1, {"N": 2}), ("cornell_4096", 1, 1, 1, 0, {"N": 2}),
+    # final shading's shadow rays over the 16-byte quantized nodes at N = 1 (final.qbvh = 1; the default takes them at
+    # N = 2 only) and over the 32-byte float nodes at N = 2 (final.qbvh = 0)
+    ("cornell_1024", 1, 0, 0, 0, {"final.qbvh": 1}), ("nightclub_128pt", 1, 0, 0, 0, {"final.qbvh": 1}),
+    ("nightclub_128pt", 1, 0, 0, 0, {"N": 2, "final.qbvh": 0})])
 def test_miss_tiles_match_full_reads(gpu, oracle, name, passes, unbiased, vis, tiled, tune):
     """MissTiles (miss.tiles = 1, the default): RIS flags the 32 x 8 tiles whose pixels all missed the scene, and the
     spatial passes and final shading write those tiles' known results without reading them.  Frames at 640 x 360
@@ -1013,6 +1017,7 @@ def test_miss_tiles_match_full_reads(gpu, oracle, name, passes, unbiased, vis, t
         gpu.set_tuning("miss.tiles", 1)
         gpu.set_tuning("miss.gbuf", 2)
         gpu.set_tuning("spatial.th", 0)
+        gpu.set_tuning("final.qbvh", 2)
     want, _, _ = oracle.render_frame(oracle.OracleScene(s), cam, f, w, h, SEED, 0, threads=16)
     if tile is not None:   # the tile's rows (row 0 = its top) against the oracle's whole frame (row 0 = global y = h - 1)
         r0 = h - (tile.y0 + tile.height)

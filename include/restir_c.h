@@ -543,7 +543,11 @@ restir_status restir_enable_timing(restir_ctx* ctx, int enable);
  * detects the form bit for bit).  "spatial.xcd_rows|xcd_cols" (the spatial pass's XCD chunk shape; 255 = automatic),
  * "spatial.th" (0: auto, 1: 32x8, 2: 32x16 tiles), "spatial.handles" (N = 1 biased passes over a point-light scene read
  * sample handles, k_spatial1h; with temporal reuse when the predecessor frame carries the handles its last pass wrote
- * -- N = 1 point lights, no ghost ring, the same scene upload -- else its reservoir planes are read; default 1), "ris.late" (stage the light table after the primary rays, only for tiles that
+ * -- N = 1 point lights, no ghost ring, the same scene upload -- else its reservoir planes are read; default 1),
+ * "spatial.gather" (the point-light handle pass on 32x16 tiles gathers the accepted neighbours' handles instead of
+ * staging the handle windows in LDS, k_spatial1hg_t2; default 1), "spatial.n2h" (N = 2 biased passes over a point-light
+ * scene without temporal reuse read 16-byte handle records, k_spatial2hg; default 1), "final.qbvh" (final shading's
+ * shadow rays walk 16-byte quantized BVH nodes: 0 never, 1 always, 2 = at N = 2, the default), "ris.late" (stage the light table after the primary rays, only for tiles that
  * need it), "final.sort" (bin each tile's shadow rays by target), "final.miss" (final shading reads only p_mat and
  * (pos, W) for a primary-ray miss), "miss.tiles" (background-tile flags from RIS to the spatial passes and final
  * shading, N <= 2 without temporal reuse), "miss.gbuf" (0 / 1 / 2 = auto: RIS also skips background tiles' G-buffer

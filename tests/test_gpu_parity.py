@@ -567,15 +567,16 @@ def _temporal_sequence(gpu, oracle, N=1, rescene=False, w=W, h=H, moving=False, 
         prev_gpu, prev_or = grid, res
 
 
-@pytest.mark.parametrize("tiles", [(2, 1), (2, 2), (4, 2)])
-def test_tiles_stitch_to_full_frame(gpu, oracle, tiles):
-    """Screen tiles with ghost zones (the multi-GPU decomposition) reproduce the single-GPU frame bit-exactly."""
+@pytest.mark.parametrize("tiles,N", [((2, 1), 1), ((2, 2), 1), ((4, 2), 1), ((2, 2), 2), ((4, 2), 2)])
+def test_tiles_stitch_to_full_frame(gpu, oracle, tiles, N):
+    """Screen tiles with ghost zones (the multi-GPU decomposition) reproduce the single-GPU frame bit-exactly (N = 2:
+    the handle-record passes, k_spatial2hg, on the ghost-zoned views too)."""
     from romis_amd import restir
     name = "nightclub_128pt"
     s = get_scene(name)
     gpu.set_scene(s)
     cam = scene.camera_for(name, W, H)
-    f = _abi.default_features(num_samples_in_reservoir=1, spatial_resampling_passes=2, temporal_reuse=0)
+    f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=2, temporal_reuse=0)
     gpu.set_seed(SEED, 0)
     full, _ = gpu.render_restir(None, cam, W, H, f, want_grid=False)
     stitched = np.zeros_like(full)

@@ -316,9 +316,20 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                 Sub prev[NT > 0 ? NT : 1];
                 unsigned long long mcur = 0, mprev = 0;
                 uint32_t phidx = L;   // the predecessor's light index (frame handles)
+                uint32_t pidx2[2] = {L, L};   // N = 2: its sub-reservoirs' light indices (the 16-byte frame handle records)
+                float4 prec = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (NT == 2 && LT == kLtPoint && tin.hw) prec = reinterpret_cast<const float4*>(tin.hw)[p];
 #pragma unroll
                 for (uint32_t j = 0; j < (uint32_t)NT; j++) {
-                    if (NT == 1 && LT == kLtPoint && tin.hw) {
+                    if (NT == 2 && LT == kLtPoint && tin.hw) {
+                        // sub-reservoir j from its handle record (W_j, M_j | i_j << 24): the values the planes hold
+                        const uint32_t hv = __float_as_uint(j == 0 ? prec.y : prec.w);
+                        sub_init(prev[j]);
+                        pidx2[j] = hv >> 24;
+                        prev[j].W = j == 0 ? prec.x : prec.z;
+                        prev[j].M = hv & 0x00FFFFFFu;
+                        if (pidx2[j] < L) { prev[j].pos = xyz(lights[pidx2[j]]); prev[j].col = xyz(lights[L + pidx2[j]]); }
+                    } else if (NT == 1 && LT == kLtPoint && tin.hw) {
                         // the predecessor from its handle: the same W, M, position and colour the reservoir planes
                         // hold (index L: the zero sample)
                         const uint32_t hv = tin.hm[p];
@@ -358,6 +369,27 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
                                       __float_as_uint(cmb.out[0].col.z) == __float_as_uint(prev[0].col.z);
                     if (same) hidx = phidx;
                 }
+                if (NT == 2 && LT == kLtPoint && hw) {
+                    // N = 2: each output holds one of the four inputs' samples or the zero sample; its index is that of
+                    // an input holding the same (position, colour) bit for bit -- any such index rebuilds the same sample
+                    auto same = [](const Sub& a, const Sub& b) {
+                        return __float_as_uint(a.pos.x) == __float_as_uint(b.pos.x) &&
+                               __float_as_uint(a.pos.y) == __float_as_uint(b.pos.y) &&
+                               __float_as_uint(a.pos.z) == __float_as_uint(b.pos.z) &&
+                               __float_as_uint(a.col.x) == __float_as_uint(b.col.x) &&
+                               __float_as_uint(a.col.y) == __float_as_uint(b.col.y) &&
+                               __float_as_uint(a.col.z) == __float_as_uint(b.col.z);
+                    };
+                    uint32_t oidx[2];
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const Sub& o = cmb.out[j];
+                        oidx[j] = same(o, prev[0]) ? pidx2[0] : same(o, prev[1]) ? pidx2[1]
+                                : same(o, r[0]) ? hidx : same(o, r[1]) ? hidx1 : L;
+                    }
+                    hidx = oidx[0];
+                    hidx1 = oidx[1];
+                }
 #pragma unroll
                 for (uint32_t j = 0; j < (uint32_t)NT; j++) r[j] = cmb.out[j];
                 if (NT == 1 && rp) rp[p] = pd_out[0];
@@ -369,7 +401,7 @@ __device__ __forceinline__ void ris_pixel(const SceneDev& s, const Region& rg, c
         if (store_res || rdbg)
             for (uint32_t j = 0; j < N; j++) sub_store(r[j], ra, rb, rdbg, ridx(rg, j, p), j * npx + p);
         if (NT == 1 && LT == kLtPoint && hw) { hw[p] = r[0].W; hm[p] = r[0].M | (hidx << 24); }
-        if (NT == 2 && LT == kLtPoint && !TEMP && hw)   // N = 2 handle record (W_0, M_0 | i_0 << 24, W_1, M_1 | i_1 << 24)
+        if (NT == 2 && LT == kLtPoint && hw)   // N = 2 handle record (W_0, M_0 | i_0 << 24, W_1, M_1 | i_1 << 24)
             reinterpret_cast<float4*>(hw)[p] = make_float4(r[0].W, __uint_as_float(r[0].M | (hidx << 24)), r[1].W,
                                                            __uint_as_float(r[1].M | (hidx1 << 24)));
         if (NT == 1 && LT == kLtRegular && hw)   // grid handle: (W, M | i << 19, a, b) in one float4 plane
@@ -2565,7 +2597,7 @@ hipError_t launch_primary_ris_temporal(const SceneDev& s, const Region& rg0, con
                                        Handles h) {
     if (rg0.rw == 0 || rg0.rh == 0) return hipSuccess;
     if (!primary_ris_temporal_fits(s, f, tu)) return hipErrorInvalidValue;   // the caller checks
-    if (f.N != 1 && (h.w || tin.hw)) return hipErrorInvalidValue;          // handles: N = 1
+    if (f.N != 1 && f.N != 2 && (h.w || tin.hw)) return hipErrorInvalidValue;   // handles: N = 1 / 2
     const Region rg = with_map(rg0, 1u);
     const size_t lds = bvh_lds_bytes(s) + ris_lights_lds_bytes(s, kLtPoint);
     auto k = f.N == 1 ? k_primary_ris_n1_lds_pt_temporal : k_primary_ris_n2_lds_pt_temporal;

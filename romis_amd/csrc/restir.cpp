@@ -900,15 +900,18 @@ struct FrameBufs {
         float* w = hnd_()[i].as<float>();
         return w ? Handles{w, reinterpret_cast<uint32_t*>(w + npx), 0u} : Handles{nullptr, nullptr, 0u};
     }
-    // frame handles: the same planes at the tail of rec[i] (N = 1, planes layout, ensure_records), handed on with the
-    // records to the frame restir_render returns -- the next frame's fused temporal reuse reads them (8 B / px, not 32)
+    // frame handles: the same planes at the tail of rec[i] (planes layout, ensure_records), handed on with the records to
+    // the frame restir_render returns -- the next frame's fused temporal reuse reads them: N = 1 the W and M | index
+    // planes (8 B / px, not 32), N = 2 the 16-byte handle records (not 64 B)
     Handles fh(int i) const {
-        if (records || N != 1) return Handles{nullptr, nullptr, 0u};
-        float* w = reinterpret_cast<float*>(rec_()[i].as<float4>() + 2 * npx);
-        return Handles{w, reinterpret_cast<uint32_t*>(w + npx), 0u};
+        if (records || (N != 1 && N != 2)) return Handles{nullptr, nullptr, 0u};
+        float* w = reinterpret_cast<float*>(rec_()[i].as<float4>() + 2 * N * npx);
+        return Handles{w, N == 1 ? reinterpret_cast<uint32_t*>(w + npx) : nullptr, 0u};
     }
-    const float* fhw(const restir_frame* f) const { return reinterpret_cast<const float*>(f->rec.as<float4>() + 2 * npx); }
-    const uint32_t* fhm(const restir_frame* f) const { return reinterpret_cast<const uint32_t*>(fhw(f) + npx); }
+    const float* fhw(const restir_frame* f) const { return reinterpret_cast<const float*>(f->rec.as<float4>() + 2 * N * npx); }
+    const uint32_t* fhm(const restir_frame* f) const {
+        return N == 1 ? reinterpret_cast<const uint32_t*>(fhw(f) + npx) : nullptr;
+    }
     float4* nt(int i) const { return records ? rec_()[i].as<float4>() : n_t_().as<float4>(); }
     float4* ra(int i) const { return rec_()[i].as<float4>() + (records ? 1 : 0); }
     float4* rb(int i) const { return rec_()[i].as<float4>() + (records ? 2 : npx * N); }
@@ -926,8 +929,10 @@ restir_status ensure_records(restir_ctx* c, uint32_t vw, uint32_t vh, uint32_t N
     const hipStream_t st = c->stream;
     ST_TRY(c->p_mat.ensure(npx * 16));
     if (!fb.records) ST_TRY(fb.n_t_().ensure(npx * 16));
-    // (N = 1 planes: + the frame handles' two 4-byte planes and 16 B of slack, FrameBufs::fh)
-    const size_t rec_bytes = npx * (fb.records ? 1u + 2u * N : 2u * N) * 16 + (!fb.records && N == 1 ? npx * 8 + 16 : 0);
+    // (planes, N = 1: + the frame handles' two 4-byte planes and 16 B of slack; N = 2: + the 16-byte handle records and
+    // 16 B; FrameBufs::fh)
+    const size_t rec_bytes = npx * (fb.records ? 1u + 2u * N : 2u * N) * 16 +
+                             (fb.records ? 0 : N == 1 ? npx * 8 + 16 : N == 2 ? npx * 16 + 16 : 0);
     DevBuf* rec = fb.rec_();
     for (int i = 0; i < 2; i++) {
         // a buffer handed to a frame comes back through the pool (stream-ordered against its past users)
@@ -1563,16 +1568,19 @@ restir_status restir_render(restir_ctx* c, const restir_camera* cam, const resti
     // With temporal reuse the passes read handles when the fused temporal kernel can rebuild the predecessor from its
     // frame handles (point lights, the same scene upload): every M then bounded by RIS's plus the clamp's
     const bool no_ghost = t.gwidth == t.width && t.gheight == t.height;
-    const bool temporal_handles = temporal && fused && !fb.records && N == 1 && no_ghost && prev->hgen != 0 &&
+    const bool temporal_handles = temporal && fused && !fb.records && (N == 1 || N == 2) && no_ghost && prev->hgen != 0 &&
                                   prev->hgen == c->scene_gen && primary_ris_temporal_fits(s, f, c->tuning);
-    const uint64_t m_in = temporal ? (uint64_t)f.M + (uint64_t)f.clamp_m * f.M + 1u : 0u;
+    // the M every sub-reservoir can hold entering the passes after temporal reuse: the current M plus each of the N
+    // predecessor sub-reservoirs clamped to clampM M + 1 (kernels.hip ris_pixel TEMP)
+    const uint64_t m_temporal = (uint64_t)f.M + (uint64_t)N * ((uint64_t)f.clamp_m * f.M + 1u);
+    const uint64_t m_in = temporal ? m_temporal : 0u;
     const int hkind = (temporal && !temporal_handles) ? -1 : spatial_handle_kind(s, f, c->tuning, passes, m_in);
-    const bool handles = fused && !fb.records && hkind >= 0 && (!temporal || hkind == 0) &&
+    const bool handles = fused && !fb.records && hkind >= 0 && (!temporal || hkind == 0 || hkind == 2) &&
                          (size_t)t.gwidth * t.gheight * 16u <= 0xFFFFFFFFull;
     // the last pass also writes the returned grid's handles (point lights, no ghost ring) for the next frame, bounded as
     // if that frame's temporal reuse had run (its M bound)
-    const bool frame_handles = handles && hkind == 0 && out_next && no_ghost &&
-                               spatial_handle_kind(s, f, c->tuning, passes, (uint64_t)f.M + (uint64_t)f.clamp_m * f.M + 1u) == 0;
+    const bool frame_handles = handles && (hkind == 0 || hkind == 2) && out_next && no_ghost &&
+                               spatial_handle_kind(s, f, c->tuning, passes, m_temporal) == hkind;
     if (handles)
         for (int i = 0; i < 2; i++) ST_TRY(fb.hnd_()[i].ensure((size_t)t.gwidth * t.gheight * (hkind ? 16u : 8u) + 16u));
     // the handle passes read RIS's samples through the handles alone, and a pass's output is read by the next pass's

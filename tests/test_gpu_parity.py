@@ -510,7 +510,9 @@ def test_odd_sizes_and_extremes_match_oracle(gpu, oracle, w, h, N, passes, M):
 @pytest.mark.parametrize("records,fuse,N,variant", [(0, 1, 1, ""), (0, 1, 1, "rescene"), (0, 1, 1, "nohandles"),
                                                     (1, 1, 1, ""), (0, 0, 1, ""), (0, 1, 2, ""), (0, 0, 2, ""),
                                                     (0, 1, 1, "moving"), (0, 1, 1, "moving_ragged"), (0, 1, 2, "moving_ragged"),
-                                                    (0, 1, 1, "mbound_in"), (0, 1, 1, "mbound_out")])
+                                                    (0, 1, 1, "mbound_in"), (0, 1, 1, "mbound_out"),
+                                                    (0, 1, 2, "rescene"), (0, 1, 2, "nohandles"), (0, 1, 2, "moving"),
+                                                    (0, 1, 2, "mbound_in"), (0, 1, 2, "mbound_out")])
 def test_temporal_sequence_matches_oracle(gpu, oracle, records, fuse, N, variant):
     """C3-style: 4 static frames, temporal reuse threading the previous frame's grid (main.cpp:165); both frame
     buffer layouts (SoA planes, per-pixel records); temporal reuse fused into the primary + RIS kernel (fuse.temporal,
@@ -521,7 +523,9 @@ def test_temporal_sequence_matches_oracle(gpu, oracle, records, fuse, N, variant
     / 32 x 16 tiles, clampM = 1): RIS tiles whose every pixel misses now while the predecessor held real lights there, so
     the fused kernel rebuilds those predecessors from its light table (the table must be staged for such
     tiles too).  "mbound_in" / "mbound_out": 5 and 6 passes at clampM = 20, the last M bound (M + clampM M + 1)(K + 1)^P
-    that fits the handles' 24 bits and the first that does not (frame handles on / reservoir planes)."""
+    that fits the handles' 24 bits and the first that does not (frame handles on / reservoir planes).  N = 2 fused (round 6):
+    the predecessor is rebuilt from the 16-byte frame handle records and the passes read handle records (k_spatial2hg);
+    its M bound counts both predecessor sub-reservoirs, M + 2 (clampM M + 1), and crosses 24 bits at the same pass count."""
     gpu.set_tuning("layout.records", records)
     gpu.set_tuning("fuse.temporal", fuse)
     if variant == "nohandles":

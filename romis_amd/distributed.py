@@ -202,8 +202,10 @@ def balanced_layout(renderer: "restir.Renderer", camera_fn, width: int, height: 
                     align=LAYOUT_ALIGN, time_tile=None, rounds: int = 3):
     """(layout, record): rank 0 of the group measures the geometry (geometry_cost) and cuts the tiles
     (restir_layout_balanced); the cuts are broadcast, so every rank holds the same layout (once per camera).
-    time_tile(layout) -> this rank's frame seconds on its tile of `layout`: then `rounds` rounds of measured
-    refinement follow (refine_cost on rank 0 from the gathered times, new cuts broadcast)."""
+    time_tile(layout) -> this rank's frame seconds on its tile of `layout`: then the layout and `rounds` refinements of it
+    (refine_cost on rank 0 from the gathered times, new cuts broadcast) are each measured, and the layout with the best
+    measured balance (mean / max of the ranks' times) is returned -- noisy or contended timings can make one refinement
+    worse than the one before, and every rank sees the same gathered times, so all choose alike."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -212,12 +214,12 @@ def balanced_layout(renderer: "restir.Renderer", camera_fn, width: int, height: 
     dev = torch.device("cuda", torch.cuda.current_device()) if multi and dist.get_backend(group) == "nccl" else "cpu"
     src = (dist.get_global_rank(group, 0) if group is not None else 0) if multi else 0
 
-    def share(buf):
+    def share(buf):   # rank 0's cuts to every rank: (layout, model efficiency, the buffer every rank now holds)
         if multi:
             t = torch.from_numpy(buf).to(dev)
             dist.broadcast(t, src=src, group=group)
             buf = t.cpu().numpy()
-        return _layout_from_buf(buf, width, height, tiles)
+        return _layout_from_buf(buf, width, height, tiles) + (buf,)
 
     cost = None
     buf = np.zeros(restir._abi.RESTIR_MAX_TILES_X + 1 + restir._abi.RESTIR_MAX_TILES_X * (restir._abi.RESTIR_MAX_TILES_Y + 1)
@@ -225,10 +227,12 @@ def balanced_layout(renderer: "restir.Renderer", camera_fn, width: int, height: 
     if rank == 0:
         cost = geometry_cost(renderer, camera_fn, width, height)
         buf = _layout_buf(*restir.layout_balanced(width, height, tiles[0], tiles[1], cost, align))
-    L, eff = share(buf)
+    L, eff, held = share(buf)
     rec = {"kind": "cost-balanced (restir_layout_balanced)", "model_efficiency": round(eff, 4),
            "cost_grid": list(COST_GRID), "background_weight": BACKGROUND_WEIGHT, "align": list(align), "refinement": []}
-    for _ in range(rounds if time_tile is not None else 0):
+    best = None   # (measured efficiency, round, the layout's buffer)
+    n = rounds + 1 if time_tile is not None else 0
+    for i in range(n):
         mine = float(time_tile(L))
         times = [mine]
         if multi:
@@ -236,12 +240,19 @@ def balanced_layout(renderer: "restir.Renderer", camera_fn, width: int, height: 
             outs = [torch.zeros_like(t) for _ in range(dist.get_world_size(group))]
             dist.all_gather(outs, t, group=group)
             times = [float(o.item()) for o in outs]
+        measured = float(np.mean(times) / max(times))
         rec["refinement"].append({"cuts": L.cuts(), "rank_ms": [round(v * 1e3, 4) for v in times],
-                                  "measured_efficiency": round(float(np.mean(times) / max(times)), 4)})
-        if rank == 0:
-            cost = refine_cost(cost, L, times)
-            buf = _layout_buf(*restir.layout_balanced(width, height, tiles[0], tiles[1], cost, align))
-        L, eff = share(buf)
+                                  "measured_efficiency": round(measured, 4)})
+        if best is None or measured > best[0]:
+            best = (measured, i, held.copy())
+        if i + 1 < n:
+            if rank == 0:
+                cost = refine_cost(cost, L, times)
+                buf = _layout_buf(*restir.layout_balanced(width, height, tiles[0], tiles[1], cost, align))
+            L, eff, held = share(buf)
+    if best is not None:
+        L, _ = _layout_from_buf(best[2], width, height, tiles)
+        rec["chosen_round"] = best[1]
     rec["cuts"] = L.cuts()
     return L, rec
 

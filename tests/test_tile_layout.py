@@ -158,3 +158,54 @@ def test_measured_refinement_converges_on_the_true_cost(abi_lib):
     assert eff0 < 0.85 and eff >= 0.93, (eff0, eff)
     own = distributed.cell_owners(L, cost.shape)
     assert own.min() == 0 and own.max() == 7
+
+
+
+def _true_share_time(L, rank, calls, inflate_call):
+    """A stand-in frame time: this rank's share of a "true" cost whose top-right quadrant is 3x dearer than the model,
+    inflated 5x on rank 1 at one measurement (contention)."""
+    true = _blob_cost()
+    ch, cw = true.shape
+    true[: ch // 2, cw // 2:] *= 3.0
+    calls.append(L.cuts())
+    t = float(restir.layout_shares(L, true)[rank])
+    return t * (5.0 if rank == 1 and len(calls) == inflate_call else 1.0)
+
+
+def _best_round_worker(rank, world, port, result):
+    import json
+    import torch.distributed as dist
+    from romis_amd import distributed
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    distributed.geometry_cost = lambda *a, **k: _blob_cost()
+    calls = []
+    L, rec = distributed.balanced_layout(None, None, 3840, 2160, (2, 1), time_tile=lambda L: _true_share_time(
+        L, rank, calls, 2), rounds=3)
+    with open(f"{result}.{rank}", "w") as fh:
+        json.dump({"cuts": L.cuts(), "rec": rec}, fh)
+    dist.destroy_process_group()
+
+
+def test_balanced_layout_keeps_the_best_measured_round(tmp_path, abi_lib):
+    """distributed.balanced_layout with time_tile over 2 gloo ranks: the model layout and each of its refinements are
+    measured, and every rank returns the same layout -- the best measured one, not the last refinement (a contended
+    measurement, here the first refinement's on rank 1, must not be what the bench times)."""
+    import json
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    result = str(tmp_path / "r")
+    mp.spawn(_best_round_worker, args=(2, port, result), nprocs=2, join=True)
+    outs = []
+    for rank in range(2):
+        with open(f"{result}.{rank}") as fh:
+            outs.append(json.load(fh))
+    assert outs[0] == outs[1]
+    rec = outs[0]["rec"]
+    eff = [r["measured_efficiency"] for r in rec["refinement"]]
+    assert len(eff) == 4 and rec["chosen_round"] == int(np.argmax(eff))
+    assert rec["chosen_round"] != 1 and eff[1] < min(eff[0], eff[2], eff[3])
+    assert outs[0]["cuts"] == rec["refinement"][rec["chosen_round"]]["cuts"]
+    assert max(eff) > eff[0]   # refinement from measured times beats the model's cuts

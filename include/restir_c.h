@@ -547,8 +547,10 @@ restir_status restir_enable_timing(restir_ctx* ctx, int enable);
  * "spatial.gather" (the point-light handle pass on 32x16 tiles gathers the accepted neighbours' handles instead of
  * staging the handle windows in LDS, k_spatial1hg_t2; default 1), "spatial.n2h" (N = 2 biased passes over a point-light
  * scene without temporal reuse read 16-byte handle records, k_spatial2hg; default 1), "final.qbvh" (final shading's
- * shadow rays walk 16-byte quantized BVH nodes: 0 never, 1 always, 2 = at N = 2, the default), "ris.late" (stage the light table after the primary rays, only for tiles that
- * need it), "final.sort" (bin each tile's shadow rays by target), "final.miss" (final shading reads only p_mat and
+ * shadow rays walk 16-byte quantized BVH nodes: 0 never, 1 always, 2 = at N = 2, the default), "primary.tl" (the fused
+ * primary + RIS kernel's primary rays test their 32x8 tile's candidate triangles -- those not wholly outside the tile's
+ * ray pyramid -- instead of walking the BVH; default 1), "ris.late" (stage the light table after the primary rays, only
+ * for tiles that need it), "final.sort" (bin each tile's shadow rays by target), "final.miss" (final shading reads only p_mat and
  * (pos, W) for a primary-ray miss), "miss.tiles" (background-tile flags from RIS to the spatial passes and final
  * shading, N <= 2 without temporal reuse), "miss.gbuf" (0 / 1 / 2 = auto: RIS also skips background tiles' G-buffer
  * stores), "timing.every" / "timing.fence" (event sampling), "mis.chunk" (R-OMIS samples per launch pair).  All default

@@ -17,10 +17,13 @@
 
 // ---------------------------------------------------------------------------------------------------------
 // genPrimaryRayHits for pixel (x, y) at view index p: writes and returns the G-buffer records (n_t, p_mat)
+// tl (nullable): the block's candidate triangles (tile_triangles: four 64-entry segments, tl_cnt[w] entries each),
+// tested instead of walking the BVH
 __device__ __forceinline__ void primary_pixel(const SceneDev& s, const Region& rg, const CameraDev& cam, const Bvh& bvh,
                                               uint32_t x, uint32_t y, size_t p, float4* __restrict__ n_t2,
                                               float4* __restrict__ n_t, float4* __restrict__ p_mat, float4& nt_out,
-                                              float4& pm_out, bool store = true) {
+                                              float4& pm_out, bool store = true, const uint16_t* tl = nullptr,
+                                              const uint32_t* tl_cnt = nullptr) {
     const v3 o = mk(cam.origin[0], cam.origin[1], cam.origin[2]);
     {
         float nx = (float)x / (float)rg.W * 2.0f - 1.0f;
@@ -32,7 +35,7 @@ __device__ __forceinline__ void primary_pixel(const SceneDev& s, const Region& r
         v3 n = mk(0.0f, 0.0f, 0.0f);
         float2 tc = make_float2(0.0f, 0.0f);   // a miss keeps the value-initialised HitInfo::texCoord
         uint32_t m = s.num_materials - 1;
-        if (closest(bvh, o, d, t, u, v, tri)) {
+        if (tl ? closest_list(bvh, tl, tl_cnt, o, d, t, u, v, tri) : closest(bvh, o, d, t, u, v, tri)) {
             float w0 = (1.0f - u) - v;
             float4 a = s.tri_n0[tri], b = s.tri_n1[tri], c = s.tri_n2[tri];
             n = vadd(vadd(vscale(xyz(a), w0), vscale(xyz(b), u)), vscale(xyz(c), v));
@@ -56,6 +59,52 @@ __device__ __forceinline__ void primary_pixel(const SceneDev& s, const Region& r
             p_mat[p] = pm_out;
         }
     }
+}
+
+// Candidate triangles of a 32 x 8 tile's primary rays (round 6, primary.tl).  Every ray of the tile leaves the camera
+// origin o in the direction R (a, b, 1) (primary_pixel: R = the camera rotation, a = -nx half_w, b = ny half_h over the
+// tile's pixel coordinates); the pyramid of those directions, widened by two pixels on each side, is bounded by the
+// four planes through o with the world normals R (1, 0, -a0), R (-1, 0, a1), R (0, 1, -b0), R (0, -1, b1).  A triangle
+// whose three vertices all lie outside one of them (beyond a relative margin of 1e-5, far above the rounding of this
+// test and far below the two pixels) cannot be hit by any ray of the tile; the list keeps the others.  closest_list
+// over it returns closest()'s hit (its selection does not depend on order), as the BVH walk does -- both skip only
+// geometry the rays pass well clear of (the BVH's boxes are padded by 1e-5 of the scene).  Thread t tests triangle t
+// (num_tris <= 256) from global memory and each wave compacts its survivors by ballot into its own 64-entry segment:
+// no atomics, and no barrier of its own -- the caller's BVH staging barrier publishes the lists.
+constexpr uint32_t kTlMaxTris = 256u;
+__device__ __forceinline__ void tile_triangles(const SceneDev& s, const Region& rg, const CameraDev& cam, int x0, int x1,
+                                               int y0, int y1, uint16_t* tl, uint32_t* tl_cnt) {
+    const float W = (float)rg.W, H = (float)rg.H;
+    // pixel coordinates two pixels beyond the tile (primary_pixel's nx = x / W * 2 - 1, ny = y / H * 2 - 1)
+    const float nxl = (float)(x0 - 2) / W * 2.0f - 1.0f, nxh = (float)(x1 + 2) / W * 2.0f - 1.0f;
+    const float nyl = (float)(y0 - 2) / H * 2.0f - 1.0f, nyh = (float)(y1 + 2) / H * 2.0f - 1.0f;
+    const float a0 = fminf(-nxl * cam.half_w, -nxh * cam.half_w), a1 = fmaxf(-nxl * cam.half_w, -nxh * cam.half_w);
+    const float b0 = fminf(nyl * cam.half_h, nyh * cam.half_h), b1 = fmaxf(nyl * cam.half_h, nyh * cam.half_h);
+    // the rotation's columns: the camera axes in world space (the matrix of qrotate)
+    const float qx = cam.quat.x, qy = cam.quat.y, qz = cam.quat.z, qw = cam.quat.w;
+    const v3 rx = mk(1.0f - 2.0f * (qy * qy + qz * qz), 2.0f * (qx * qy + qw * qz), 2.0f * (qx * qz - qw * qy));
+    const v3 ry = mk(2.0f * (qx * qy - qw * qz), 1.0f - 2.0f * (qx * qx + qz * qz), 2.0f * (qy * qz + qw * qx));
+    const v3 rz = mk(2.0f * (qx * qz + qw * qy), 2.0f * (qy * qz - qw * qx), 1.0f - 2.0f * (qx * qx + qy * qy));
+    const v3 pn[4] = {vsub(rx, vscale(rz, a0)), vsub(vscale(rz, a1), rx), vsub(ry, vscale(rz, b0)), vsub(vscale(rz, b1), ry)};
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    bool keep = false;
+    if (t < s.num_tris) {
+        const v3 o = mk(cam.origin[0], cam.origin[1], cam.origin[2]);
+        const v3 v0 = xyz(s.tri_v0[t]);
+        const v3 p0 = vsub(v0, o), p1 = vsub(vadd(v0, xyz(s.tri_e1[t])), o), p2 = vsub(vadd(v0, xyz(s.tri_e2[t])), o);
+        const float l0 = fabsf(p0.x) + fabsf(p0.y) + fabsf(p0.z), l1 = fabsf(p1.x) + fabsf(p1.y) + fabsf(p1.z);
+        const float l2 = fabsf(p2.x) + fabsf(p2.y) + fabsf(p2.z);
+        bool out = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const float m = 1e-5f * (fabsf(pn[k].x) + fabsf(pn[k].y) + fabsf(pn[k].z));
+            out = out || (vdot(pn[k], p0) < -m * l0 && vdot(pn[k], p1) < -m * l1 && vdot(pn[k], p2) < -m * l2);
+        }
+        keep = !out;
+    }
+    const unsigned long long bal = __ballot(keep);
+    if (keep) tl[(t & ~63u) + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)t;
+    if (lane == 0u) tl_cnt[t >> 6] = (uint32_t)__popcll(bal);
 }
 
 // k_primary: persistent blocks stage the BVH into LDS once, then sweep 32x8 tiles; writes n_t / p_mat.
@@ -466,12 +515,24 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
     // run the candidate loop (ris_pixel's miss test) -- at C4 / C5 87 % of the tiles see only background.  The same
     // vote is the tile's MissTiles flag (tmiss, one byte per tile; the launcher passes it only for one tile per block).
     const bool one = gridDim.x >= items;
-    const bool late = LDS_LIGHTS && late_ok && one;
+    const bool late = LDS_LIGHTS && (late_ok & 1u) && one;   // late_ok bit 1: primary.tl (tile_triangles)
     if (LDS_LIGHTS) {
         if (!late) stage_lights<LT>(s, g_lds + bvh_f4);
         lights = g_lds + bvh_f4;
     }
-    const Bvh bvh = stage_bvh(s, g_lds);   // ends with the barrier that also covers the light copy
+    // primary.tl (late_ok bit 1): the tile's candidate triangles, published by the staging barrier below
+    __shared__ uint16_t s_tl[kTlMaxTris];
+    __shared__ uint32_t s_tlc[4];
+    const bool tl = (late || (one && tmiss)) && (late_ok & 2u) && rg.map2d && s.num_tris <= kTlMaxTris &&
+                    blockIdx.x < items && cam.half_w > 0.0f && cam.half_h > 0.0f;   // block-uniform
+    if (tl) {
+        const uint32_t ntx = (rg.rw + kTileW - 1) / kTileW;
+        const int tx0 = (int)(rg.rx0 + (blockIdx.x % ntx) * kTileW), ty0 = (int)(rg.ry0 + (blockIdx.x / ntx) * kTileH);
+        const int tx1 = min(tx0 + (int)kTileW, (int)(rg.rx0 + rg.rw)) - 1, ty1 = min(ty0 + (int)kTileH, (int)(rg.ry0 + rg.rh)) - 1;
+        tile_triangles(s, rg, cam, tx0, tx1, ty0, ty1, s_tl, s_tlc);
+    }
+    // ends with the barrier that also covers the light copy (and the lists); the nodes only for rays that walk them
+    const Bvh bvh = stage_bvh(s, g_lds, !tl || f.initial_vis);
     const GlTabs tb = gl_stage_tables();
     const v3 origin = mk(cam.origin[0], cam.origin[1], cam.origin[2]);
     if (late || (one && tmiss)) {
@@ -481,7 +542,7 @@ __device__ __forceinline__ void primary_ris_body(const SceneDev& s, const Region
         const bool live = work_pixel(rg, blockIdx.x, x, y, p);
         float4 nt = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pm = nt;
         const bool skip_gbuf = tmiss && (skip_res & 2u);   // bit 1: a background tile's G-buffer records too
-        if (live) primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, nt, pm, !skip_gbuf);
+        if (live) primary_pixel(s, rg, cam, bvh, x, y, p, n_t2, n_t, p_mat, nt, pm, !skip_gbuf, tl ? s_tl : nullptr, s_tlc);
         uint32_t m = __float_as_uint(pm.w);
         if (m >= s.num_materials) m = s.num_materials - 1u;
         const bool loop = live && s.num_lights != 0u &&
@@ -2579,7 +2640,8 @@ hipError_t launch_primary_ris(const SceneDev& s, const Region& rg0, const Camera
            : use_lights ? (f.N == 1 ? k_primary_ris_n1_lds : (f.N == 2 ? k_primary_ris_n2_lds : k_primary_ris_n0_lds))
                         : (f.N == 1 ? k_primary_ris_n1 : (f.N == 2 ? k_primary_ris_n2 : k_primary_ris_n0));
     ROMIS_LAUNCH(k, dim3(items_of(rg)), dim3(kBlock), bvh + (use_lights ? lights : 0), stream, s, rg,
-                 cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr, tu.ris_late, tmiss,
+                 cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg, f.N == 1 ? rp : nullptr,
+                 (tu.ris_late ? 1u : 0u) | (tu.primary_tl ? 2u : 0u), tmiss,
                  tmiss ? skip_res : 0u, ((lt == kLtPoint || lt == kLtRegular) && f.N == 1) || (lt == kLtPoint && f.N == 2) ? h.w : nullptr,
                  lt == kLtPoint && f.N == 1 ? h.m : nullptr, h.w && (lt == kLtPoint || lt == kLtRegular) ? h.res_dead : 0u);
     return hipGetLastError();
@@ -2602,7 +2664,8 @@ hipError_t launch_primary_ris_temporal(const SceneDev& s, const Region& rg0, con
     const size_t lds = bvh_lds_bytes(s) + ris_lights_lds_bytes(s, kLtPoint);
     auto k = f.N == 1 ? k_primary_ris_n1_lds_pt_temporal : k_primary_ris_n2_lds_pt_temporal;
     ROMIS_LAUNCH(k, dim3(items_of(rg)), dim3(kBlock), lds, stream, s, rg, cam, f, key, n_t, p_mat, n_t2, ra, rb, rdbg,
-                 f.N == 1 ? rp : nullptr, tu.ris_late, tin, h.w, h.m, h.w ? h.res_dead : 0u);
+                 f.N == 1 ? rp : nullptr, (tu.ris_late ? 1u : 0u) | (tu.primary_tl ? 2u : 0u), tin, h.w, h.m,
+                 h.w ? h.res_dead : 0u);
     return hipGetLastError();
 }
 

@@ -99,10 +99,12 @@ __device__ __forceinline__ Bvh global_bvh(const SceneDev& s) {
     return b;
 }
 
-// Copy nodes + triangles into LDS (every thread of the block participates; ends with a barrier).
-__device__ __forceinline__ Bvh stage_bvh(const SceneDev& s, float4* lds) {
+// Copy nodes + triangles into LDS (every thread of the block participates; ends with a barrier).  nodes = false: the
+// triangles alone, at the same offsets (a block whose rays all test candidate lists, primary.tl)
+__device__ __forceinline__ Bvh stage_bvh(const SceneDev& s, float4* lds, bool nodes = true) {
     const uint32_t nn = 2u * s.num_nodes, nt = s.num_tris;
-    for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = s.nodes[i];
+    if (nodes)
+        for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = s.nodes[i];
     for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) {
         lds[nn + i] = s.tri_v0[i];
         lds[nn + nt + i] = s.tri_e1[i];
@@ -244,6 +246,29 @@ __device__ __forceinline__ bool closest(const Bvh& b, v3 o, v3 d, float& t_best,
             }
         } else {
             i = miss;
+        }
+    }
+    return found;
+}
+
+// closest() over a list of candidate triangles (indices into the traversal arrays): the same tests with the same
+// selection rule (minimal t, lowest original index on ties), which does not depend on the order the triangles are
+// tested in -- so any list that holds every triangle a ray can hit gives closest()'s result (round 6, primary.tl)
+// (the list: four segments of 64 entries, cnt[w] used in segment w; the triangles indexed as the traversal arrays)
+__device__ __forceinline__ bool closest_list(const Bvh& b, const uint16_t* tl, const uint32_t* cnt, v3 o, v3 d,
+                                             float& t_best, float& u_best, float& v_best, uint32_t& tri_best) {
+    bool found = false;
+    t_best = ROMIS_FLT_MAX;
+    tri_best = 0xFFFFFFFFu;
+    for (uint32_t w = 0; w < 4u; w++)
+    for (uint32_t k = 0; k < cnt[w]; k++) {
+        const uint32_t i = tl[64u * w + k];
+        const float4 v0 = b.v0[i];
+        float t, u, v;
+        const bool h = tri_test(v0, b.e1[i], b.e2[i], o, d, ROMIS_FLT_MAX, t, u, v);
+        const uint32_t orig = __float_as_uint(v0.w);
+        if (h && (!found || t < t_best || (t == t_best && orig < tri_best))) {
+            found = true; t_best = t; u_best = u; v_best = v; tri_best = orig;
         }
     }
     return found;

@@ -2670,6 +2670,7 @@ restir_status restir_set_tuning(restir_ctx* c, const char* key, int value) {
     else if (!std::strcmp(key, "bvh.max_leaf")) t.bvh_max_leaf = v;
     else if (!std::strcmp(key, "final.sort")) t.final_sort = v;
     else if (!std::strcmp(key, "final.qbvh")) t.final_qbvh = v;
+    else if (!std::strcmp(key, "primary.tl")) t.primary_tl = v;
     else if (!std::strcmp(key, "mis.chunk")) t.mis_chunk = v;   // applies from the next ensure_mis
     else if (!std::strcmp(key, "layout.records")) t.records = v;   // frame-path buffer layout
     else if (!std::strcmp(key, "final.lds")) t.final_lds = v;

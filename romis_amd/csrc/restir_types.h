@@ -181,6 +181,8 @@ struct Tuning {
                                    // 2 (auto): at N = 2 (C2 N = 2 final 153.6 -> 145.8 us; N = 1: C2 80.0 -> 79.5, C4f
                                    // 265.8 -> 277.4 -- round 6, profiles/r6/probes/s7)
     uint32_t final_sort = 1;       // N = 1: bin each tile's shadow rays by target before tracing (-2.4 %, r2ah)
+    uint32_t primary_tl = 1;       // fused primary + RIS, one tile per block: the primary rays test the tile's candidate
+                                   // triangles (tile_triangles) instead of walking the BVH
     uint32_t mis_chunk = 0;        // R-OMIS samples per k_romis_samples / k_romis_accum pair; 0 = the scratch budget
 };
 

@@ -22,13 +22,14 @@ from romis_amd import _abi, restir, scene  # noqa: E402
 
 DEFAULTS = {"primary.lds": 1, "ris.lds": 1, "ris.compact": 1, "ris.late": 1, "miss.tiles": 1, "miss.gbuf": 2,
             "spatial.xcd_rows": 255, "spatial.xcd_cols": 255, "spatial.lean": 1, "spatial.th": 0, "spatial.handles": 1, "spatial.gather": 1, "spatial.n2h": 1,
-            "fuse.primary_ris": 1, "fuse.temporal": 1, "bvh.max_leaf": 2, "final.lds": 1, "final.sort": 1, "final.qbvh": 2, "final.miss": 1, "layout.records": 0}
+            "fuse.primary_ris": 1, "fuse.temporal": 1, "bvh.max_leaf": 2, "final.lds": 1, "final.sort": 1, "final.qbvh": 2, "primary.tl": 1, "final.miss": 1, "layout.records": 0}
 
 VARIANTS = {
     "default": {},
     "handles_off": {"spatial.handles": 0},
     "handles_t1": {"spatial.th": 1},
     "handles_lds": {"spatial.gather": 0},
+    "tl_off": {"primary.tl": 0},
     "ntl_t2": {"spatial.handles": 0, "spatial.th": 2},
     "feat_no_tonemap": {"@enable_tone_mapping": 0},
     "primary_2d_global": {"primary.lds": 0},

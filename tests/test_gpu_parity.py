@@ -454,6 +454,47 @@ def test_spatial_handles_frames_match_oracle(gpu, oracle, name, framing, th, w, 
     assert_bits(rgb_ng, want, f"no grid th={th} {w}x{h} passes={passes}")
 
 
+@pytest.mark.parametrize("name,framing,N,temporal", [("nightclub_128pt", None, 1, 0), ("nightclub_128pt", None, 2, 0),
+                                                    ("nightclub_128pt", None, 1, 1), ("cornell_1024", "framed", 1, 0),
+                                                    ("cornell_1024", None, 1, 0), ("cornell_parallelogram", None, 1, 0),
+                                                    ("nightclub_512", None, 2, 0)])
+@pytest.mark.parametrize("w,h,tiled", [(96, 64, 0), (37, 23, 0), (333, 190, 1), (640, 360, 0)])
+def test_primary_tile_lists_match_bvh(gpu, oracle, name, framing, N, temporal, w, h, tiled):
+    """primary.tl (round 6): the fused primary + RIS kernel's primary rays test the candidate triangles of their 32 x 8
+    tile (tile_triangles: every triangle not wholly outside one side of the tile's ray pyramid widened by two pixels)
+    instead of walking the BVH; closest_list's selection (minimal t, lowest original index) is closest()'s.  RGB and
+    the returned grid bit-exact with primary.tl = 0 -- whole frames and ghost-zoned tiles, N = 1 / 2, temporal frames
+    (the fused temporal kernel), point lights, light grids, parallelograms, the TOML camera (background tiles) and the
+    camera into the box -- and the RGB with the oracle."""
+    from romis_amd import restir
+    s = get_scene(name)
+    gpu.set_scene(s)
+    cam = scene.camera_for(name, w, h, framing)
+    f = _abi.default_features(num_samples_in_reservoir=N, spatial_resampling_passes=1, temporal_reuse=temporal)
+    tile = restir.tile_plan(w, h, 2, 2, 2, f.spatial_resample_radius) if tiled else None
+    out = {}
+    try:
+        for on in (0, 1):
+            gpu.set_tuning("primary.tl", on)
+            gpu.set_seed(SEED, 0)
+            prev = None
+            for fr in range(2 if temporal else 1):   # a temporal frame needs its predecessor
+                rgb, grid = gpu.render_restir(prev, cam, w, h, f, tile=None if temporal else tile)
+                prev = grid
+            out[on] = (rgb, [np.asarray(a) for a in grid.download()])
+    finally:
+        gpu.set_tuning("primary.tl", 1)
+    assert_bits(out[1][0], out[0][0], f"{name} {w}x{h} rgb tl on / off")
+    for a, b in zip(out[0][1], out[1][1]):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), f"{name} {w}x{h} grid tl on / off"
+    if not temporal and w * h <= 96 * 64:
+        want, _, _ = oracle.render_frame(oracle.OracleScene(s), cam, f, w, h, SEED, 0)
+        if tile is not None:
+            r0 = h - (tile.y0 + tile.height)
+            want = np.ascontiguousarray(want[r0:r0 + tile.height, tile.x0:tile.x0 + tile.width])
+        assert_bits(out[1][0], want, f"{name} {w}x{h} against the oracle")
+
+
 @pytest.mark.parametrize("th", [1, 2])
 @pytest.mark.parametrize("w,h,passes,M", [(96, 64, 1, 32), (37, 23, 2, 32), (130, 70, 3, 1), (64, 1, 1, 16)])
 def test_spatial_n2_handles_frames_match_oracle(gpu, oracle, th, w, h, passes, M):

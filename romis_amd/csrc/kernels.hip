@@ -2261,10 +2261,11 @@ __device__ __forceinline__ void final_body(const SceneDev& s, const Region& rg, 
 // rays by a 256-cell grid of the target position (scene bounds = the BVH root box), lays them out in bin order
 // in LDS, traces ray i on thread i, and hands each result back to its pixel.  Same rays, same arithmetic:
 // only which lane traces which ray changes.  One 32x8 tile per block (every thread reaches the barriers).
+// (The bin only decides which lane traces which ray, never a result: the scale is an approximate reciprocal.)
 __device__ __forceinline__ uint32_t target_bin(const Bvh& b, v3 y) {
     const float4 lo = b.nodes[0], hi = b.nodes[1];
     auto q = [](float v, float l, float h, float cells) {
-        float t = (v - l) / fmaxf(h - l, 1e-30f) * cells;
+        float t = (v - l) * __builtin_amdgcn_rcpf(fmaxf(h - l, 1e-30f)) * cells;
         return (uint32_t)fminf(fmaxf(t, 0.0f), cells - 1.0f);
     };
     const uint32_t qx = q(y.x, lo.x, hi.x, 8.0f), qy = q(y.y, lo.y, hi.y, 8.0f), qz = q(y.z, lo.z, hi.z, 4.0f);
